@@ -1,0 +1,128 @@
+/* omg.h — C-ABI of the MI355X-native octree-mg V-cycle (libomg.so).
+ *
+ * Drop-in boundary for the per-level box loops of the reference octree-mg
+ * (FermiQ/octree-mg @ 2025-06-14).  The reference has no C boundary: its plug
+ * points are Fortran procedure pointers called once per box
+ * (mg%box_op / mg%box_smoother / mg%box_prolong, src/m_data_structures.f90:
+ * 330-336, interfaces :381-407) and the per-level loops of src/m_multigrid.f90.
+ * This header replaces those loops at LEVEL granularity: the host (the Fortran
+ * drop-in m_multigrid in octree-mg_amd/fortran/, or the Python mirror in
+ * octree-mg_amd/) hands over the mg_t tree once, and every per-level step
+ * runs as HIP kernels over level-contiguous device arrays.
+ *
+ * Conventions
+ *   - Plain C types only; every call returns 0 on success, nonzero on error
+ *     with the message in omg_last_error() (the Fortran wrapper turns it into
+ *     `error stop`, like the reference's error stops).
+ *   - Box ids are the reference's 1-based ids; neighbour ids follow the
+ *     reference encoding (>0 box, 0 = mg_no_box (refinement boundary),
+ *     <0 = physical boundary / bc code).  Variables iv are 1-based
+ *     (1 phi, 2 rhs, 3 old, 4 res, 5.. extra), src/m_data_structures.f90:43-65.
+ *   - Box data is exchanged as the reference stores it: cc(0:nc+1,0:nc+1,
+ *     0:nc+1) of one variable, Fortran column-major (i fastest).
+ *   - One context per process/GPU; calls are stream-ordered on the context's
+ *     stream and not re-entrant.  Multi-GPU: one rank per GPU, halos over
+ *     RCCL (ncclSend/ncclRecv, xGMI), bootstrapped from omg_get_unique_id().
+ */
+#ifndef OMG_H
+#define OMG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct omg_ctx omg_ctx;
+
+#define OMG_UNIQUE_ID_BYTES 128
+
+/* Operators / smoothers / bc codes: same values as the reference
+ * (src/m_data_structures.f90:14-37, 73-79). */
+enum { OMG_LAPLACIAN = 1, OMG_VLAPLACIAN = 2, OMG_HELMHOLTZ = 3, OMG_VHELMHOLTZ = 4,
+       OMG_AHELMHOLTZ = 5 };
+enum { OMG_SMOOTHER_GS = 1, OMG_SMOOTHER_GSRB = 2 };
+enum { OMG_BC_DIRICHLET = -10, OMG_BC_NEUMANN = -11, OMG_BC_CONTINUOUS = -12 };
+
+const char *omg_last_error(void);
+
+/* RCCL bootstrap: rank 0 calls this and broadcasts the bytes to all ranks
+ * (replaces mg_comm_init's MPI set-up, src/m_communication.f90:14-35). */
+int omg_get_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
+
+/* Create a context on HIP device `device` for rank `rank` of `n_ranks`.
+ * unique_id may be NULL when n_ranks == 1. */
+int omg_ctx_create(omg_ctx **ctx, int device, int rank, int n_ranks, const void *unique_id);
+int omg_ctx_destroy(omg_ctx *ctx);
+
+/* Hand over the mg_t tree (replaces the device side of mg_allocate_storage,
+ * src/m_allocate_storage.f90:51-99): per-box arrays indexed by id-1
+ * (children 8/box, neighbors 6/box, ix 3/box, rank 1/box), per-level arrays
+ * indexed by lvl-lowest (box_size_lvl, dr 3/level) and, for every level and
+ * list type t in {ids, leaves, parents, ref_bnds}, the slice
+ * lists[list_off[4*(lvl-lowest)+t] .. list_off[4*(lvl-lowest)+t+1]).
+ * Allocates n_vars variables for every box owned by this rank, zeroed. */
+int omg_tree_setup(omg_ctx *ctx, int n_boxes, const int *lvl, const int *parent,
+                   const int *children, const int *neighbors, const int *ix,
+                   const int *rank, int lowest_lvl, int highest_lvl,
+                   int first_normal_lvl, int box_size, const int *box_size_lvl,
+                   const double *dr, const int *list_off, const int *lists,
+                   int n_vars);
+
+/* mg_set_methods equivalents (src/m_multigrid.f90:27-60, m_helmholtz.f90:
+ * 39-46, m_ahelmholtz.f90:59-66). */
+int omg_set_operator(omg_ctx *ctx, int op, double lambda);
+int omg_set_smoother(omg_ctx *ctx, int smoother, int n_cycle_down, int n_cycle_up,
+                     int max_coarse_cycles, double residual_coarse_abs,
+                     double residual_coarse_rel);
+int omg_set_subtract_mean(omg_ctx *ctx, int on);
+
+/* Boundary conditions for variable iv (mg%bc(nb, iv), src/m_data_structures
+ * .f90:235-242).  omg_set_bc_faces tabulates a boundary_cond callback:
+ * face_off[(id-1)*6 + nb-1] = offset of nc*nc values in data (first
+ * tangential index fastest) or -1; face_type = the bc type it returned. */
+int omg_set_bc(omg_ctx *ctx, int iv, int nb, int bc_type, double bc_value);
+int omg_set_bc_faces(omg_ctx *ctx, int iv, const long long *face_off,
+                     const int *face_type, const double *data, long long n_data);
+
+/* Number of boxes this rank owns at lvl (size(mg%lvls(lvl)%my_ids)). */
+int omg_level_size(omg_ctx *ctx, int lvl, int *n_boxes, int *nc);
+
+/* Bulk copy of variable iv of all my_ids boxes at lvl, in my_ids order,
+ * (nc+2)^3 doubles per box, host memory (blocking). */
+int omg_upload_level(omg_ctx *ctx, int lvl, int iv, const double *host);
+int omg_download_level(omg_ctx *ctx, int lvl, int iv, double *host);
+
+/* The hot path (src/m_multigrid.f90): highest_lvl < lowest means default. */
+int omg_fas_vcycle(omg_ctx *ctx, int highest_lvl, int want_max_res, double *max_res,
+                   int standalone);
+int omg_fas_fmg(omg_ctx *ctx, int have_guess, int want_max_res, double *max_res);
+
+/* Per-level steps (each as in the reference routine named). */
+int omg_apply_op(omg_ctx *ctx, int i_out);                       /* mg_apply_op */
+int omg_restrict(omg_ctx *ctx, int iv);                          /* mg_restrict */
+int omg_restrict_lvl(omg_ctx *ctx, int iv, int lvl);             /* mg_restrict_lvl */
+int omg_fill_ghost_cells(omg_ctx *ctx, int iv);                  /* mg_fill_ghost_cells */
+int omg_fill_ghost_cells_lvl(omg_ctx *ctx, int lvl, int iv);     /* mg_fill_ghost_cells_lvl */
+int omg_prolong(omg_ctx *ctx, int lvl, int iv, int iv_to, int add); /* mg_prolong (sparse) */
+int omg_smooth_boxes(omg_ctx *ctx, int lvl, int n_cycle);        /* smooth_boxes */
+int omg_update_coarse(omg_ctx *ctx, int lvl);                    /* update_coarse */
+int omg_correct_children(omg_ctx *ctx, int lvl);                 /* correct_children */
+int omg_residual_lvl(omg_ctx *ctx, int lvl);                     /* residual_box over my_ids */
+int omg_max_residual_lvl(omg_ctx *ctx, int lvl, double *out);    /* max_residual_lvl */
+int omg_get_sum(omg_ctx *ctx, int iv, double *out);              /* get_sum + allreduce */
+int omg_subtract_mean(omg_ctx *ctx, int iv, int include_ghostcells); /* subtract_mean */
+int omg_phi_bc_store(omg_ctx *ctx);                              /* mg_phi_bc_store */
+
+/* Stream / timing helpers for benchmarks. */
+int omg_synchronize(omg_ctx *ctx);
+void *omg_stream(omg_ctx *ctx);                 /* the hipStream_t all work runs on */
+/* Per-kernel HIP-event timing (off by default): when on, every launch of the
+ * named kernel families is bracketed by events on the context stream. */
+int omg_set_profiling(omg_ctx *ctx, int on);
+int omg_kernel_stats(omg_ctx *ctx, const char *name, long long *launches,
+                     double *total_ms, double *cells);
+int omg_reset_stats(omg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1016 @@
+// omg_api.cpp — C-ABI (include/omg.h), device plan builder and the per-level
+// orchestration of the FAS V-cycle / FMG on one GPU per rank.
+//
+// The control flow of every entry point follows the reference routine named in
+// its comment (FermiQ/octree-mg, src/m_multigrid.f90 etc.); each per-box loop
+// of the reference is one level-wide kernel launch here, and every MPI
+// exchange of the reference (m_communication.f90:37-66) is one grouped RCCL
+// send/recv round over xGMI carrying device-packed buffers.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/omg.h"
+#include "omg_kernels.h"
+
+using namespace omg;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct OmgError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                            \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess)                                                                    \
+      throw OmgError(std::string(#x) + ": " + hipGetErrorString(e_) + " (" + __FILE__ + ":" + \
+                     std::to_string(__LINE__) + ")");                                        \
+  } while (0)
+
+#define NCCLCHK(x)                                                                         \
+  do {                                                                                     \
+    ncclResult_t r_ = (x);                                                                 \
+    if (r_ != ncclSuccess) throw OmgError(std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return 1;
+  }
+}
+
+template <typename T>
+T* to_device(const std::vector<T>& v) {
+  if (v.empty()) return nullptr;
+  T* d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(T) * v.size()));
+  HIPCHK(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+  return d;
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+const int kNeighbRev[6] = {2, 1, 4, 3, 6, 5};
+
+inline int pack_dix(const int d[3]) { return d[0] | (d[1] << 10) | (d[2] << 20); }
+
+// ---------------------------------------------------------------------------
+// tree helpers (reference src/m_data_structures.f90)
+struct Tree {
+  omg_ctx* c;
+  int lvl(int id) const { return c->lvl[id - 1]; }
+  int parent(int id) const { return c->parent[id - 1]; }
+  int child(int id, int s) const { return c->children[(id - 1) * 8 + s - 1]; }
+  int nbr(int id, int nb) const { return c->neighbors[(id - 1) * 6 + nb - 1]; }
+  int rank(int id) const { return c->rank_of[id - 1]; }
+  // mg_get_child_offset (m_data_structures.f90:456-467)
+  void child_offset(int id, int d[3]) const {
+    if (lvl(id) <= c->first_normal) {
+      d[0] = d[1] = d[2] = 0;
+    } else {
+      for (int q = 0; q < 3; q++) d[q] = ((c->ix[(id - 1) * 3 + q] - 1) & 1) * (c->box_size >> 1);
+    }
+  }
+};
+
+Level* level_ptr(omg_ctx* c, int l) {
+  auto it = c->levels.find(l);
+  return it == c->levels.end() ? nullptr : &it->second;
+}
+
+LevelView empty_view() {
+  LevelView v;
+  std::memset(&v, 0, sizeof(v));
+  return v;
+}
+
+LevelView view_of(omg_ctx* c, int l) {
+  Level* L = level_ptr(c, l);
+  return L ? L->view() : empty_view();
+}
+
+// Build a Transfer's device arrays from its per-peer lists.
+void finalize_transfer(Transfer& T) {
+  std::vector<int> s, r;
+  int off = 0;
+  for (auto& p : T.send) {
+    p.offset = off;
+    off += (int)p.items.size() / T.send_ints;
+    s.insert(s.end(), p.items.begin(), p.items.end());
+  }
+  T.n_send = off;
+  off = 0;
+  for (auto& p : T.recv) {
+    p.offset = off;
+    off += (int)p.items.size() / T.recv_ints;
+    r.insert(r.end(), p.items.begin(), p.items.end());
+  }
+  T.n_recv = off;
+  T.d_send_items = to_device(s);
+  T.d_recv_items = to_device(r);
+}
+
+// Group key-sorted (peer, key, item...) records into per-peer lists.
+struct Rec {
+  int peer;
+  long long key;
+  int a, b;
+};
+std::vector<PeerList> group(std::vector<Rec>& recs, int ints_per_item) {
+  std::sort(recs.begin(), recs.end(), [](const Rec& x, const Rec& y) {
+    return x.peer != y.peer ? x.peer < y.peer : x.key < y.key;
+  });
+  std::vector<PeerList> out;
+  for (auto& r : recs) {
+    if (out.empty() || out.back().peer != r.peer) {
+      out.push_back(PeerList());
+      out.back().peer = r.peer;
+    }
+    out.back().items.push_back(r.a);
+    if (ints_per_item == 2) out.back().items.push_back(r.b);
+  }
+  return out;
+}
+
+// One grouped RCCL round: send segment i to peer i, receive likewise
+// (replaces sort_and_transfer_buffers, m_communication.f90:37-66).
+void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf) {
+  if (c->n_ranks == 1) return;
+  if (T.send.empty() && T.recv.empty()) return;
+  ncclComm_t comm = (ncclComm_t)c->nccl;
+  const size_t per = (size_t)T.item_doubles;
+  NCCLCHK(ncclGroupStart());
+  for (auto& p : T.send) {
+    size_t n = p.items.size() / (T.send_ints) * per;
+    NCCLCHK(ncclSend(sendbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, c->stream));
+  }
+  for (auto& p : T.recv) {
+    size_t n = p.items.size() / (T.recv_ints) * per;
+    NCCLCHK(ncclRecv(recvbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, c->stream));
+  }
+  NCCLCHK(ncclGroupEnd());
+}
+
+// ---------------------------------------------------------------------------
+// profiling: HIP events around kernel families on the context stream
+struct Prof {
+  omg_ctx* c;
+  const char* name;
+  double cells;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  Prof(omg_ctx* c_, const char* n, double cl) : c(c_), name(n), cells(cl) {
+    if (!c->profiling) return;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, c->stream));
+  }
+  ~Prof() {
+    if (!e0) return;
+    (void)hipEventRecord(e1, c->stream);
+    c->pending.push_back({name, e0, e1, cells});
+  }
+};
+
+void resolve_stats(omg_ctx* c) {
+  if (c->pending.empty()) return;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (auto& p : c->pending) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, p.e0, p.e1));
+    auto& s = c->stats[p.name];
+    s.launches++;
+    s.ms += ms;
+    s.cells += p.cells;
+    (void)hipEventDestroy(p.e0);
+    (void)hipEventDestroy(p.e1);
+  }
+  c->pending.clear();
+}
+
+// ---------------------------------------------------------------------------
+// Per-level steps
+GcBC bc_for(omg_ctx* c, int lvl, int iv) {
+  GcBC g;
+  for (int nb = 0; nb < 6; nb++) {
+    g.type[nb] = c->bc[iv - 1].type[nb];
+    g.value[nb] = c->bc[iv - 1].value[nb];
+  }
+  auto it = c->d_face_off_lvl[iv - 1].find(lvl);
+  g.face_off = it == c->d_face_off_lvl[iv - 1].end() ? nullptr : it->second;
+  auto jt = c->d_face_type_lvl[iv - 1].find(lvl);
+  g.face_type = jt == c->d_face_type_lvl[iv - 1].end() ? nullptr : jt->second;
+  g.face_data = c->d_face_data[iv - 1];
+  g.phi_stored = c->phi_bc_data_stored;
+  return g;
+}
+
+// mg_fill_ghost_cells_lvl (m_ghost_cells.f90:131-175)
+void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
+  if (lvl < c->lowest) throw OmgError("fill_ghost_cells_lvl: lvl < lowest_lvl");
+  if (lvl > c->highest) throw OmgError("fill_ghost_cells_lvl: lvl > highest_lvl");
+  Level* L = level_ptr(c, lvl);
+  if (!L) return;
+  const LevelView V = L->view();
+  if (c->n_ranks > 1 && (L->halo.n_send || L->halo.n_recv)) {
+    launch_pack_faces(V, iv, L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, c->stream);
+    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
+  }
+  if (L->n == 0) return;
+  Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc);
+  launch_fill_gc(V, iv, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_recvbuf, c->stream);
+}
+
+void box_smoother_lvl(omg_ctx* c, int lvl, int cntr) {
+  Level* L = level_ptr(c, lvl);
+  if (!L || L->n == 0) return;
+  const double cells = (double)L->n * L->nc * L->nc * L->nc;
+  if (c->smoother == OMG_SMOOTHER_GSRB) {
+    Prof p(c, "smoother_gsrb", 0.5 * cells);
+    launch_gsrb(L->view(), c->op, c->lambda, cntr, c->stream);
+  } else {
+    Prof p(c, "smoother_gs", cells);
+    launch_gs_lex(L->view(), c->op, c->lambda, c->stream);
+  }
+}
+
+// smooth_boxes (m_multigrid.f90:404-424)
+void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
+  for (int n = 1; n <= n_cycle * c->n_substeps; n++) {
+    box_smoother_lvl(c, lvl, n);
+    fill_gc_lvl(c, lvl, 1);
+  }
+}
+
+void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
+  Level* L = level_ptr(c, lvl);
+  if (!L || L->n == 0) return;
+  Prof p(c, "residual", (double)L->n * L->nc * L->nc * L->nc);
+  launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
+}
+
+// max_residual_lvl (m_multigrid.f90:296-311), this rank only
+double max_residual_lvl(omg_ctx* c, int lvl) {
+  unsigned long long* d = (unsigned long long*)c->d_scalar;
+  HIPCHK(hipMemsetAsync(d, 0, 8, c->stream));
+  residual_lvl(c, lvl, d);
+  HIPCHK(hipMemcpyAsync(c->h_scalar, d, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return c->h_scalar[0];
+}
+
+// mg_restrict_lvl (m_restrict.f90:83-114)
+void restrict_lvl(omg_ctx* c, int iv, int lvl) {
+  if (lvl <= c->lowest) throw OmgError("cannot restrict lvl <= lowest_lvl");
+  Level* F = level_ptr(c, lvl);
+  Level* C = level_ptr(c, lvl - 1);
+  const LevelView FV = view_of(c, lvl), CV = view_of(c, lvl - 1);
+  if (c->n_ranks > 1 && F && C && (F->restr.n_send || F->restr.n_recv)) {
+    launch_restrict_pack(FV, iv, F->restr.d_send_items, F->restr.n_send, F->d_sendbuf, c->stream);
+    exchange(c, F->restr, F->d_sendbuf, C->d_recvbuf);
+    launch_restrict_unpack(CV, iv, F->restr.d_recv_items, F->restr.n_recv, F->nc / 2, C->d_recvbuf,
+                           c->stream);
+  }
+  if (F && F->n_pairs) {
+    Prof p(c, "restrict", (double)F->n_pairs * F->nc * F->nc * F->nc);
+    launch_restrict(FV, CV, iv, F->d_pairs, F->n_pairs, F->d_parent_local, F->d_dix, c->stream);
+  }
+}
+
+// mg_prolong (m_prolong.f90:51-85), lvl -> lvl+1
+void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
+  if (lvl == c->highest) throw OmgError("cannot prolong highest level");
+  if (lvl < c->lowest) throw OmgError("cannot prolong below lowest level");
+  Level* F = level_ptr(c, lvl + 1);
+  Level* C = level_ptr(c, lvl);
+  const LevelView FV = view_of(c, lvl + 1), CV = view_of(c, lvl);
+  if (c->n_ranks > 1 && F && C && (F->prol.n_send || F->prol.n_recv)) {
+    launch_prolong_pack(CV, iv, F->nc, F->prol.d_send_items, F->prol.n_send, C->d_sendbuf, c->stream);
+    exchange(c, F->prol, C->d_sendbuf, F->d_recvbuf);
+    launch_prolong_unpack(FV, iv_to, add, F->prol.d_recv_items, F->prol.n_recv, F->d_recvbuf,
+                          c->stream);
+  }
+  if (F && F->n_pairs) {
+    Prof p(c, "prolong", (double)F->n_pairs * F->nc * F->nc * F->nc);
+    launch_prolong(CV, FV, iv, iv_to, add, F->d_pairs, F->n_pairs, F->d_parent_local, F->d_dix,
+                   c->stream);
+  }
+}
+
+// update_coarse (m_multigrid.f90:347-384)
+void update_coarse(omg_ctx* c, int lvl) {
+  residual_lvl(c, lvl, nullptr);
+  restrict_lvl(c, 1, lvl);
+  restrict_lvl(c, 4, lvl);
+  fill_gc_lvl(c, lvl - 1, 1);
+  Level* C = level_ptr(c, lvl - 1);
+  if (C && !C->parents.empty()) {
+    Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc);
+    launch_coarse_rhs(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream);
+  }
+}
+
+// correct_children (m_multigrid.f90:387-402)
+void correct_children(omg_ctx* c, int lvl) {
+  Level* C = level_ptr(c, lvl);
+  if (C && !C->parents.empty())
+    launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
+  prolong(c, lvl, 4, 1, 1);
+}
+
+// MPI_Allreduce of one double: max exactly; sum in the recursive-doubling
+// pairwise order of MPICH for power-of-two communicators.
+double allreduce(omg_ctx* c, double v, bool is_max) {
+  if (c->n_ranks == 1) return v;
+  double* d = c->d_scalar + 8;
+  c->h_scalar[1] = v;
+  HIPCHK(hipMemcpyAsync(d, &c->h_scalar[1], 8, hipMemcpyHostToDevice, c->stream));
+  NCCLCHK(ncclAllGather(d, d + 1, 1, ncclDouble, (ncclComm_t)c->nccl, c->stream));
+  std::vector<double> all(c->n_ranks);
+  HIPCHK(hipMemcpyAsync(all.data(), d + 1, 8 * c->n_ranks, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (is_max) return *std::max_element(all.begin(), all.end());
+  for (int w = 1; w < c->n_ranks; w *= 2)
+    for (int r = 0; r + w < c->n_ranks; r += 2 * w) all[r] = all[r] + all[r + w];
+  return all[0];
+}
+
+// get_sum (m_multigrid.f90:278-294) + MPI_Allreduce(sum) (:255)
+double get_sum(omg_ctx* c, int iv) {
+  double* acc = c->d_scalar + 2;
+  HIPCHK(hipMemsetAsync(acc, 0, 8, c->stream));
+  for (int l = 1; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->leaves.empty()) continue;
+    const double w = L->dr[0] * L->dr[1] * L->dr[2];
+    launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
+    launch_seq_sum(L->d_scratch, (int)L->leaves.size(), w, acc, c->stream);
+  }
+  HIPCHK(hipMemcpyAsync(c->h_scalar + 2, acc, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return allreduce(c, c->h_scalar[2], false);
+}
+
+// subtract_mean (m_multigrid.f90:245-276)
+void subtract_mean(omg_ctx* c, int iv, int ghosts) {
+  const int nc = c->box_size;
+  double mean = get_sum(c, iv);
+  const auto& d1 = c->drl[1];
+  const double volume = (double)(nc * nc * nc) * (d1[0] * d1[1] * d1[2]) * (double)c->ids[1].size();
+  mean = mean / volume;
+  c->h_scalar[3] = mean;
+  HIPCHK(hipMemcpyAsync(c->d_scalar + 3, c->h_scalar + 3, 8, hipMemcpyHostToDevice, c->stream));
+  for (int l = c->lowest; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (L && L->n) launch_subtract(L->view(), iv, c->d_scalar + 3, ghosts, c->stream);
+  }
+}
+
+// mg_fas_vcycle (m_multigrid.f90:150-243)
+double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalone) {
+  const bool has_highest = highest_lvl >= c->lowest;
+  if (c->subtract_mean && !has_highest) subtract_mean(c, 2, 0);
+  const int min_lvl = c->lowest, max_lvl = has_highest ? highest_lvl : c->highest;
+  if (standalone) fill_gc_lvl(c, max_lvl, 1);
+  for (int l = max_lvl; l >= min_lvl + 1; l--) {
+    smooth_boxes(c, l, c->n_cycle_down);
+    update_coarse(c, l);
+  }
+  // coarse grid: all its boxes live on one rank (error stop otherwise, :197-200)
+  {
+    const auto& ids = c->ids[min_lvl];
+    for (int id : ids)
+      if (c->rank_of[id - 1] != c->rank_of[ids[0] - 1])
+        throw OmgError("Multiple CPUs for coarse grid (not implemented yet)");
+    double init_res = max_residual_lvl(c, min_lvl);
+    for (int i = 1; i <= c->max_coarse_cycles; i++) {
+      smooth_boxes(c, min_lvl, c->n_cycle_up + c->n_cycle_down);
+      double res = max_residual_lvl(c, min_lvl);
+      if (res < c->res_rel * init_res || res < c->res_abs) break;
+    }
+  }
+  for (int l = min_lvl + 1; l <= max_lvl; l++) {
+    correct_children(c, l - 1);
+    fill_gc_lvl(c, l, 1);
+    smooth_boxes(c, l, c->n_cycle_up);
+  }
+  double max_res = 0.0;
+  if (want_max_res) {
+    double m = 0.0;
+    for (int l = min_lvl; l <= max_lvl; l++) m = std::max(max_residual_lvl(c, l), m);
+    max_res = allreduce(c, m, true);
+  }
+  if (c->subtract_mean) subtract_mean(c, 1, 1);
+  return max_res;
+}
+
+// mg_fas_fmg (m_multigrid.f90:84-147)
+double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
+  if (!have_guess)
+    for (int l = c->highest; l >= c->lowest; l--) {
+      Level* L = level_ptr(c, l);
+      if (L && L->n) launch_copy_var(L->view(), 0, 1, c->stream);
+    }
+  fill_gc_lvl(c, c->highest, 1);
+  for (int l = c->highest; l >= c->lowest + 1; l--) update_coarse(c, l);
+  if (c->subtract_mean) subtract_mean(c, 2, 0);
+  double max_res = 0.0;
+  for (int l = c->lowest; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (L && L->n) launch_copy_var(L->view(), 1, 3, c->stream);
+    if (l > c->lowest) {
+      correct_children(c, l - 1);
+      fill_gc_lvl(c, l, 1);
+    }
+    if (l == c->highest)
+      max_res = fas_vcycle(c, l, want_max_res, false);
+    else
+      fas_vcycle(c, l, false, false);
+  }
+  return max_res;
+}
+
+// ---------------------------------------------------------------------------
+// Plan builder (device side of mg_allocate_storage, m_allocate_storage.f90:51-99,
+// and of the three buffer dry runs m_ghost_cells.f90:17-62, m_restrict.f90:
+// 16-69, m_prolong.f90:16-48).
+void free_levels(omg_ctx* c) {
+  for (auto& kv : c->levels) {
+    Level& L = kv.second;
+    dfree(L.d_data); dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_rb);
+    dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
+    dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch);
+    for (Transfer* T : {&L.halo, &L.restr, &L.prol}) {
+      dfree(T->d_send_items);
+      dfree(T->d_recv_items);
+    }
+  }
+  c->levels.clear();
+  for (int iv = 0; iv < kMaxVars; iv++) {
+    for (auto& kv : c->d_face_off_lvl[iv]) dfree(kv.second);
+    for (auto& kv : c->d_face_type_lvl[iv]) dfree(kv.second);
+    c->d_face_off_lvl[iv].clear();
+    c->d_face_type_lvl[iv].clear();
+    dfree(c->d_face_data[iv]);
+  }
+}
+
+void build_plan(omg_ctx* c) {
+  Tree T{c};
+  const int me = c->rank;
+  c->local_index.assign(c->n_boxes + 1, -1);
+  for (int l = c->lowest; l <= c->highest; l++) {
+    Level& L = c->levels[l];
+    L.lvl = l;
+    L.nc = c->bsl[l];
+    for (int d = 0; d < 3; d++) L.dr[d] = c->drl[l][d];
+    for (int id : c->ids[l])
+      if (T.rank(id) == me) {
+        c->local_index[id] = (int)L.ids.size();
+        L.ids.push_back(id);
+      }
+    L.n = (int)L.ids.size();
+    const long long s = L.nc + 2;
+    L.stride = ((s * s * s + 63) / 64) * 64;
+  }
+  for (int l = c->lowest; l <= c->highest; l++) {
+    Level& L = c->levels[l];
+    const int nc = L.nc;
+    // arena
+    if (L.n) {
+      const size_t bytes = sizeof(double) * (size_t)c->n_vars * L.n * L.stride;
+      HIPCHK(hipMalloc(&L.d_data, bytes));
+      HIPCHK(hipMemset(L.d_data, 0, bytes));
+    }
+    // neighbour table + halo receive plan
+    L.h_nbk.assign((size_t)L.n * 6, NB_LOCAL);
+    L.h_nba.assign((size_t)L.n * 6, 0);
+    std::vector<Rec> hrecv, hsend;
+    for (int b = 0; b < L.n; b++) {
+      const int id = L.ids[b];
+      for (int nb = 1; nb <= 6; nb++) {
+        const int nid = T.nbr(id, nb);
+        const size_t f = (size_t)b * 6 + nb - 1;
+        if (nid > 0) {
+          if (T.rank(nid) == me) {
+            L.h_nbk[f] = NB_LOCAL;
+            L.h_nba[f] = c->local_index[nid];
+          } else {
+            L.h_nbk[f] = NB_REMOTE;
+            hrecv.push_back({T.rank(nid), (long long)id * 6 + nb, (int)f, 0});
+            // the neighbour sends the face of its own box toward us; we send ours
+            hsend.push_back({T.rank(nid), (long long)nid * 6 + kNeighbRev[nb - 1], (int)f, 0});
+          }
+        } else if (nid == 0) {
+          // refinement boundary: parent's neighbour at lvl-1 (fill_refinement_bnd :287-328)
+          const int p_id = T.parent(id);
+          const int p_nb = p_id > 0 ? T.nbr(p_id, nb) : 0;
+          if (p_nb <= 0) throw OmgError("refinement boundary without coarse neighbour");
+          if (T.rank(p_nb) != me)
+            throw OmgError("refinement boundary across ranks is not supported yet");
+          RBRec r;
+          r.coarse_idx = c->local_index[p_nb];
+          T.child_offset(id, r.dix);
+          L.h_nbk[f] = NB_RB;
+          L.h_nba[f] = (int)L.h_rb.size();
+          L.h_rb.push_back(r);
+        } else {
+          L.h_nbk[f] = NB_PHYS;
+          L.h_nba[f] = nid;
+        }
+      }
+    }
+    L.halo.recv = group(hrecv, 1);
+    L.halo.send = group(hsend, 1);
+    L.halo.send_ints = L.halo.recv_ints = 1;
+    L.halo.item_doubles = nc * nc;
+    // receive slot of every remote face = its position in the receive buffer
+    {
+      int pos = 0;
+      for (auto& p : L.halo.recv)
+        for (int& it : p.items) {
+          const int f = it;
+          L.h_nba[f] = pos++;
+        }
+    }
+    finalize_transfer(L.halo);
+    L.d_nbk = to_device(L.h_nbk);
+    L.d_nba = to_device(L.h_nba);
+    L.d_rb = to_device(L.h_rb);
+    // parents / leaves (my_parents, my_leaves) as local indices
+    for (int id : c->parents[l])
+      if (T.rank(id) == me) L.parents.push_back(c->local_index[id]);
+    for (int id : c->leaves[l])
+      if (T.rank(id) == me) L.leaves.push_back(c->local_index[id]);
+    L.d_parents = to_device(L.parents);
+    L.d_leaves = to_device(L.leaves);
+    if (!L.leaves.empty()) HIPCHK(hipMalloc(&L.d_scratch, sizeof(double) * L.leaves.size()));
+  }
+  // grid transfers between lvl-1 (coarse) and lvl (fine)
+  for (int l = c->lowest + 1; l <= c->highest; l++) {
+    Level& F = c->levels[l];
+    Level& C = c->levels[l - 1];
+    const int nc = F.nc, hnc = nc / 2;
+    F.parent_local.assign(F.n, -1);
+    F.dix_packed.assign(F.n, 0);
+    std::vector<int> pairs;
+    std::vector<Rec> rsend, rrecv, psend, precv;
+    for (int b = 0; b < F.n; b++) {
+      const int id = F.ids[b], p = T.parent(id);
+      int d[3];
+      T.child_offset(id, d);
+      F.dix_packed[b] = pack_dix(d);
+      int slot = 0;
+      for (int s = 1; s <= 8; s++)
+        if (T.child(p, s) == id) slot = s;
+      if (T.rank(p) == me) {
+        F.parent_local[b] = c->local_index[p];
+        pairs.push_back(b);
+      } else {
+        rsend.push_back({T.rank(p), (long long)p * 8 + slot, b, 0});   // restrict_set_buffer
+        precv.push_back({T.rank(p), (long long)id, b, 0});             // prolong_onto remote
+      }
+    }
+    for (int pb = 0; pb < C.n; pb++) {
+      const int p = C.ids[pb];
+      for (int s = 1; s <= 8; s++) {
+        const int ch = T.child(p, s);
+        if (ch <= 0 || T.rank(ch) == me) continue;
+        int d[3];
+        T.child_offset(ch, d);
+        rrecv.push_back({T.rank(ch), (long long)p * 8 + s, pb, pack_dix(d)});   // restrict_onto
+        psend.push_back({T.rank(ch), (long long)ch, pb, pack_dix(d)});          // prolong_set_buffer
+      }
+    }
+    F.restr.send = group(rsend, 1);
+    F.restr.recv = group(rrecv, 2);
+    F.restr.send_ints = 1;
+    F.restr.recv_ints = 2;
+    F.restr.item_doubles = hnc * hnc * hnc;
+    finalize_transfer(F.restr);
+    F.prol.send = group(psend, 2);
+    F.prol.recv = group(precv, 1);
+    F.prol.send_ints = 2;
+    F.prol.recv_ints = 1;
+    F.prol.item_doubles = nc * nc * nc;
+    finalize_transfer(F.prol);
+    F.n_pairs = (int)pairs.size();
+    F.d_pairs = to_device(pairs);
+    F.d_parent_local = to_device(F.parent_local);
+    F.d_dix = to_device(F.dix_packed);
+  }
+  // communication buffers, sized for the largest transfer touching each level
+  if (c->n_ranks > 1) {
+    std::map<int, size_t> sendn, recvn;
+    for (int l = c->lowest; l <= c->highest; l++) {
+      Level& L = c->levels[l];
+      auto upd = [](std::map<int, size_t>& m, int k, size_t v) { m[k] = std::max(m[k], v); };
+      upd(sendn, l, (size_t)L.halo.n_send * L.halo.item_doubles);
+      upd(recvn, l, (size_t)L.halo.n_recv * L.halo.item_doubles);
+      if (l > c->lowest) {
+        upd(sendn, l, (size_t)L.restr.n_send * L.restr.item_doubles);      // fine side packs
+        upd(recvn, l - 1, (size_t)L.restr.n_recv * L.restr.item_doubles);  // coarse side receives
+        upd(sendn, l - 1, (size_t)L.prol.n_send * L.prol.item_doubles);    // coarse side packs
+        upd(recvn, l, (size_t)L.prol.n_recv * L.prol.item_doubles);        // fine side receives
+      }
+    }
+    for (int l = c->lowest; l <= c->highest; l++) {
+      Level& L = c->levels[l];
+      L.sendbuf_doubles = sendn[l];
+      L.recvbuf_doubles = recvn[l];
+      if (sendn[l]) HIPCHK(hipMalloc(&L.d_sendbuf, sizeof(double) * sendn[l]));
+      if (recvn[l]) HIPCHK(hipMalloc(&L.d_recvbuf, sizeof(double) * recvn[l]));
+    }
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+extern "C" {
+
+const char* omg_last_error(void) { return g_last_error.c_str(); }
+
+int omg_get_unique_id(void* out) {
+  return guarded([&] {
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+  });
+}
+
+int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void* unique_id) {
+  return guarded([&] {
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw OmgError("bad rank / n_ranks");
+    if (n_ranks > 1 && !unique_id) throw OmgError("unique_id required for n_ranks > 1");
+    omg_ctx* c = new omg_ctx();
+    c->device = device;
+    c->rank = rank;
+    c->n_ranks = n_ranks;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
+    HIPCHK(hipHostMalloc(&c->h_scalar, sizeof(double) * 64));
+    for (int iv = 0; iv < kMaxVars; iv++)
+      for (int nb = 0; nb < 6; nb++) {
+        c->bc[iv].type[nb] = OMG_BC_DIRICHLET;
+        c->bc[iv].value[nb] = 0.0;
+      }
+    if (n_ranks > 1) {
+      ncclUniqueId id;
+      std::memcpy(&id, unique_id, sizeof(id));
+      ncclComm_t comm;
+      NCCLCHK(ncclCommInitRank(&comm, n_ranks, id, rank));
+      c->nccl = comm;
+    }
+    *out = c;
+  });
+}
+
+int omg_ctx_destroy(omg_ctx* c) {
+  return guarded([&] {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_levels(c);
+    dfree(c->d_scalar);
+    if (c->h_scalar) (void)hipHostFree(c->h_scalar);
+    if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+  });
+}
+
+int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, const int* children,
+                   const int* neighbors, const int* ix, const int* rank, int lowest_lvl,
+                   int highest_lvl, int first_normal_lvl, int box_size, const int* box_size_lvl,
+                   const double* dr, const int* list_off, const int* lists, int n_vars) {
+  return guarded([&] {
+    if (n_vars < 4 || n_vars > kMaxVars) throw OmgError("n_vars out of range");
+    (void)hipSetDevice(c->device);
+    free_levels(c);
+    c->n_boxes = n_boxes;
+    c->lvl.assign(lvl, lvl + n_boxes);
+    c->parent.assign(parent, parent + n_boxes);
+    c->children.assign(children, children + 8 * (size_t)n_boxes);
+    c->neighbors.assign(neighbors, neighbors + 6 * (size_t)n_boxes);
+    c->ix.assign(ix, ix + 3 * (size_t)n_boxes);
+    c->rank_of.assign(rank, rank + n_boxes);
+    c->lowest = lowest_lvl;
+    c->highest = highest_lvl;
+    c->first_normal = first_normal_lvl;
+    c->box_size = box_size;
+    c->n_vars = n_vars;
+    c->bsl.clear();
+    c->drl.clear();
+    c->ids.clear(); c->leaves.clear(); c->parents.clear(); c->ref_bnds.clear();
+    for (int l = lowest_lvl; l <= highest_lvl; l++) {
+      const int li = l - lowest_lvl;
+      c->bsl[l] = box_size_lvl[li];
+      c->drl[l] = {dr[3 * li], dr[3 * li + 1], dr[3 * li + 2]};
+      std::map<int, std::vector<int>>* dst[4] = {&c->ids, &c->leaves, &c->parents, &c->ref_bnds};
+      for (int t = 0; t < 4; t++) {
+        const int a = list_off[4 * li + t], b = list_off[4 * li + t + 1];
+        (*dst[t])[l] = std::vector<int>(lists + a, lists + b);
+      }
+    }
+    build_plan(c);
+    HIPCHK(hipDeviceSynchronize());
+  });
+}
+
+int omg_set_operator(omg_ctx* c, int op, double lambda) {
+  return guarded([&] {
+    if (op != OMG_LAPLACIAN && op != OMG_HELMHOLTZ && op != OMG_AHELMHOLTZ)
+      throw OmgError("mg_set_methods: unsupported operator");
+    if (lambda < 0) throw OmgError("helmholtz_set_lambda: lambda < 0 not allowed");
+    if (op == OMG_AHELMHOLTZ && c->n_vars < 7 && c->n_boxes > 0)
+      throw OmgError("ahelmholtz_set_methods: needs 3 extra variables");
+    c->op = op;
+    c->lambda = lambda;
+  });
+}
+
+int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up, int max_coarse_cycles,
+                     double res_abs, double res_rel) {
+  return guarded([&] {
+    if (smoother != OMG_SMOOTHER_GS && smoother != OMG_SMOOTHER_GSRB)
+      throw OmgError("unsupported smoother type");
+    c->smoother = smoother;
+    c->n_substeps = smoother == OMG_SMOOTHER_GSRB ? 2 : 1;
+    c->n_cycle_down = n_cycle_down;
+    c->n_cycle_up = n_cycle_up;
+    c->max_coarse_cycles = max_coarse_cycles;
+    c->res_abs = res_abs;
+    c->res_rel = res_rel;
+  });
+}
+
+int omg_set_subtract_mean(omg_ctx* c, int on) {
+  return guarded([&] { c->subtract_mean = on; });
+}
+
+int omg_set_bc(omg_ctx* c, int iv, int nb, int bc_type, double bc_value) {
+  return guarded([&] {
+    if (iv < 1 || iv > kMaxVars || nb < 1 || nb > 6) throw OmgError("omg_set_bc: bad iv/nb");
+    c->bc[iv - 1].type[nb - 1] = bc_type;
+    c->bc[iv - 1].value[nb - 1] = bc_value;
+  });
+}
+
+int omg_set_bc_faces(omg_ctx* c, int iv, const long long* face_off, const int* face_type,
+                     const double* data, long long n_data) {
+  return guarded([&] {
+    if (iv < 1 || iv > kMaxVars) throw OmgError("omg_set_bc_faces: bad iv");
+    const int k = iv - 1;
+    for (auto& kv : c->d_face_off_lvl[k]) dfree(kv.second);
+    for (auto& kv : c->d_face_type_lvl[k]) dfree(kv.second);
+    c->d_face_off_lvl[k].clear();
+    c->d_face_type_lvl[k].clear();
+    dfree(c->d_face_data[k]);
+    if (!face_off) return;
+    // only the faces of my boxes travel to the device, re-packed
+    std::vector<double> packed;
+    for (auto& kv : c->levels) {
+      Level& L = kv.second;
+      if (!L.n) continue;
+      std::vector<long long> off(L.n * 6, -1);
+      std::vector<int> typ(L.n * 6, 0);
+      const long long n2 = (long long)L.nc * L.nc;
+      for (int b = 0; b < L.n; b++)
+        for (int nb = 0; nb < 6; nb++) {
+          const long long o = face_off[(size_t)(L.ids[b] - 1) * 6 + nb];
+          if (o < 0) continue;
+          if (o + n2 > n_data) throw OmgError("omg_set_bc_faces: offset out of range");
+          off[b * 6 + nb] = (long long)packed.size();
+          typ[b * 6 + nb] = face_type[(size_t)(L.ids[b] - 1) * 6 + nb];
+          packed.insert(packed.end(), data + o, data + o + n2);
+        }
+      c->d_face_off_lvl[k][kv.first] = to_device(off);
+      c->d_face_type_lvl[k][kv.first] = to_device(typ);
+    }
+    c->d_face_data[k] = to_device(packed);
+  });
+}
+
+int omg_level_size(omg_ctx* c, int lvl, int* n_boxes, int* nc) {
+  return guarded([&] {
+    Level* L = level_ptr(c, lvl);
+    if (!L) throw OmgError("no such level");
+    *n_boxes = L->n;
+    *nc = L->nc;
+  });
+}
+
+int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
+  return guarded([&] {
+    Level* L = level_ptr(c, lvl);
+    if (!L) throw OmgError("no such level");
+    if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
+    if (!L->n) return;
+    const long long s = L->nc + 2, n3 = s * s * s;
+    HIPCHK(hipMemcpy2DAsync(L->d_data + (size_t)(iv - 1) * L->n * L->stride, sizeof(double) * L->stride,
+                            host, sizeof(double) * n3, sizeof(double) * n3, L->n,
+                            hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
+  return guarded([&] {
+    Level* L = level_ptr(c, lvl);
+    if (!L) throw OmgError("no such level");
+    if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
+    if (!L->n) return;
+    const long long s = L->nc + 2, n3 = s * s * s;
+    HIPCHK(hipMemcpy2DAsync(host, sizeof(double) * n3,
+                            L->d_data + (size_t)(iv - 1) * L->n * L->stride, sizeof(double) * L->stride,
+                            sizeof(double) * n3, L->n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int omg_fas_vcycle(omg_ctx* c, int highest_lvl, int want_max_res, double* max_res, int standalone) {
+  return guarded([&] {
+    const double r = fas_vcycle(c, highest_lvl, want_max_res != 0, standalone != 0);
+    if (want_max_res && max_res) *max_res = r;
+  });
+}
+
+int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
+  return guarded([&] {
+    const double r = fas_fmg(c, have_guess != 0, want_max_res != 0);
+    if (want_max_res && max_res) *max_res = r;
+  });
+}
+
+int omg_apply_op(omg_ctx* c, int i_out) {
+  return guarded([&] {
+    for (int l = c->lowest; l <= c->highest; l++) {
+      Level* L = level_ptr(c, l);
+      if (L && L->n) launch_box_op(L->view(), c->op, c->lambda, i_out, c->stream);
+    }
+  });
+}
+
+int omg_restrict(omg_ctx* c, int iv) {
+  return guarded([&] {
+    for (int l = c->highest; l >= c->lowest + 1; l--) restrict_lvl(c, iv, l);
+  });
+}
+int omg_restrict_lvl(omg_ctx* c, int iv, int lvl) {
+  return guarded([&] { restrict_lvl(c, iv, lvl); });
+}
+int omg_fill_ghost_cells(omg_ctx* c, int iv) {
+  return guarded([&] {
+    for (int l = c->lowest; l <= c->highest; l++) fill_gc_lvl(c, l, iv);
+  });
+}
+int omg_fill_ghost_cells_lvl(omg_ctx* c, int lvl, int iv) {
+  return guarded([&] { fill_gc_lvl(c, lvl, iv); });
+}
+int omg_prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
+  return guarded([&] { prolong(c, lvl, iv, iv_to, add); });
+}
+int omg_smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
+  return guarded([&] { smooth_boxes(c, lvl, n_cycle); });
+}
+int omg_update_coarse(omg_ctx* c, int lvl) {
+  return guarded([&] { update_coarse(c, lvl); });
+}
+int omg_correct_children(omg_ctx* c, int lvl) {
+  return guarded([&] { correct_children(c, lvl); });
+}
+int omg_residual_lvl(omg_ctx* c, int lvl) {
+  return guarded([&] { residual_lvl(c, lvl, nullptr); });
+}
+int omg_max_residual_lvl(omg_ctx* c, int lvl, double* out) {
+  return guarded([&] { *out = max_residual_lvl(c, lvl); });
+}
+int omg_get_sum(omg_ctx* c, int iv, double* out) {
+  return guarded([&] { *out = get_sum(c, iv); });
+}
+int omg_subtract_mean(omg_ctx* c, int iv, int include_ghostcells) {
+  return guarded([&] { subtract_mean(c, iv, include_ghostcells); });
+}
+
+// mg_phi_bc_store (m_ghost_cells.f90:66-117): bc values of phi go into the
+// rhs ghost cells, the bc type into the neighbour slot.
+int omg_phi_bc_store(omg_ctx* c) {
+  return guarded([&] {
+    for (auto& kv : c->levels) {
+      Level& L = kv.second;
+      if (!L.n) continue;
+      // store bc values into rhs ghosts: fill var 2's ghost faces of physical
+      // boundaries with the bc values (box_set_gc), then the types.
+      GcBC g = bc_for(c, kv.first, 1);
+      // write bc values via a Dirichlet-free path: c0=1,c1=c2=0 is not a bc
+      // type, so do it on the host for the (few) physical faces.
+      const long long s = L.nc + 2, n3 = s * s * s;
+      std::vector<double> rhs((size_t)L.n * n3);
+      HIPCHK(hipMemcpy2D(rhs.data(), sizeof(double) * n3, L.d_data + (size_t)L.n * L.stride,
+                         sizeof(double) * L.stride, sizeof(double) * n3, L.n, hipMemcpyDeviceToHost));
+      std::vector<long long> off;
+      std::vector<int> typ;
+      if (g.face_off) {
+        off.resize(L.n * 6);
+        typ.resize(L.n * 6);
+        HIPCHK(hipMemcpy(off.data(), g.face_off, sizeof(long long) * L.n * 6, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(typ.data(), g.face_type, sizeof(int) * L.n * 6, hipMemcpyDeviceToHost));
+      }
+      std::vector<double> fdata;
+      if (g.face_data) {
+        size_t tot = 0;
+        for (size_t q = 0; q < off.size(); q++)
+          if (off[q] >= 0) tot = std::max(tot, (size_t)off[q] + (size_t)L.nc * L.nc);
+        fdata.resize(tot);
+        if (tot) HIPCHK(hipMemcpy(fdata.data(), g.face_data, sizeof(double) * tot, hipMemcpyDeviceToHost));
+      }
+      const int nc = L.nc;
+      for (int b = 0; b < L.n; b++)
+        for (int nb = 1; nb <= 6; nb++) {
+          const size_t f = (size_t)b * 6 + nb - 1;
+          if (L.h_nbk[f] != NB_PHYS) continue;
+          int type;
+          const bool tab = !off.empty() && off[f] >= 0;
+          type = tab ? typ[f] : c->bc[0].type[nb - 1];
+          const int d = (nb + 1) / 2;
+          const int g0 = (nb & 1) ? 0 : nc + 1;
+          for (int cc = 1; cc <= nc; cc++)
+            for (int a = 1; a <= nc; a++) {
+              const double v = tab ? fdata[off[f] + (a - 1) + (size_t)nc * (cc - 1)] : c->bc[0].value[nb - 1];
+              long long idx;
+              if (d == 1) idx = g0 + s * (a + s * cc);
+              else if (d == 2) idx = a + s * (g0 + s * cc);
+              else idx = a + s * (cc + s * g0);
+              rhs[(size_t)b * n3 + idx] = v;
+            }
+          L.h_nba[f] = type;
+          c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = type;
+        }
+      HIPCHK(hipMemcpy2D(L.d_data + (size_t)L.n * L.stride, sizeof(double) * L.stride, rhs.data(),
+                         sizeof(double) * n3, sizeof(double) * n3, L.n, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(L.d_nba, L.h_nba.data(), sizeof(int) * L.h_nba.size(), hipMemcpyHostToDevice));
+    }
+    c->phi_bc_data_stored = 1;
+  });
+}
+
+int omg_synchronize(omg_ctx* c) {
+  return guarded([&] { HIPCHK(hipStreamSynchronize(c->stream)); });
+}
+
+void* omg_stream(omg_ctx* c) { return (void*)c->stream; }
+
+int omg_set_profiling(omg_ctx* c, int on) {
+  return guarded([&] {
+    resolve_stats(c);
+    c->profiling = on != 0;
+  });
+}
+
+int omg_kernel_stats(omg_ctx* c, const char* name, long long* launches, double* total_ms, double* cells) {
+  return guarded([&] {
+    resolve_stats(c);
+    auto it = c->stats.find(name);
+    if (it == c->stats.end()) {
+      *launches = 0;
+      *total_ms = 0;
+      *cells = 0;
+      return;
+    }
+    *launches = it->second.launches;
+    *total_ms = it->second.ms;
+    *cells = it->second.cells;
+  });
+}
+
+int omg_reset_stats(omg_ctx* c) {
+  return guarded([&] {
+    resolve_stats(c);
+    c->stats.clear();
+  });
+}
+
+}  // extern "C"

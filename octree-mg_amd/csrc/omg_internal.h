@@ -1,0 +1,168 @@
+// omg_internal.h — device data model of the MI355X octree-mg V-cycle.
+//
+// Every octree level that this rank owns boxes on is one contiguous HBM arena
+//     data[var][box][stride]        stride = pad64((nc+2)^3) doubles
+// with boxes in the reference's my_ids order and each box stored exactly like
+// the reference's cc(0:nc+1,0:nc+1,0:nc+1) (i fastest).  Per-level topology
+// tables let one kernel launch cover a whole level: for every (box, face) a
+// kind + argument (local neighbour index / physical bc code / refinement-
+// boundary record / halo receive slot), parent and child offsets for the grid
+// transfers, and the per-peer RCCL pack lists for multi-GPU halos.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace omg {
+
+enum NbKind : int8_t { NB_LOCAL = 0, NB_PHYS = 1, NB_RB = 2, NB_REMOTE = 3 };
+
+enum Op : int { OP_LPL = 1, OP_VLPL = 2, OP_HELM = 3, OP_VHELM = 4, OP_AHELM = 5 };
+
+constexpr int kMaxVars = 16;
+
+// Physical boundary condition of one variable (mg%bc(:, iv)).
+struct BCVar {
+  int type[6];
+  double value[6];
+  long long* d_face_off = nullptr;   // per level: [n*6] offsets (or -1), device
+  int* d_face_type = nullptr;
+};
+
+// A view of one level, passed to kernels by value.
+struct LevelView {
+  double* data;          // [n_vars][n][stride]
+  long long stride;      // doubles per box
+  long long vstride;     // doubles per variable = n * stride
+  int n;                 // local boxes
+  int nc;                // box size (cells per dim)
+  double idr2[3];        // 1/dr^2 per dim
+  double dr[3];
+  const int8_t* nbk;     // [n*6]
+  const int* nba;        // [n*6]
+};
+
+// Grid-transfer records.
+struct RBRec {             // refinement boundary: coarse neighbour + child offset
+  int coarse_idx;          // local index at lvl-1 of the parent's neighbour
+  int dix[3];
+};
+
+struct PeerList {          // one peer's part of a transfer, in wire order
+  int peer;
+  std::vector<int> items;  // meaning depends on the transfer type
+  int offset = 0;          // first item in the device list / buffer
+};
+
+struct Transfer {          // one p2p pattern (halo, restrict, prolong)
+  std::vector<PeerList> send, recv;
+  int* d_send_items = nullptr;  // concatenated send items
+  int* d_recv_items = nullptr;
+  int n_send = 0, n_recv = 0;   // total items
+  int item_doubles = 0;         // payload per item
+  int send_ints = 1, recv_ints = 1;  // ints per item in the send / recv lists
+};
+
+struct Level {
+  int lvl = 0, nc = 0, n = 0;
+  long long stride = 0;
+  double dr[3] = {0, 0, 0};
+  std::vector<int> ids;                 // global ids of my boxes (my_ids order)
+  double* d_data = nullptr;
+  int8_t* d_nbk = nullptr;
+  int* d_nba = nullptr;
+  std::vector<int8_t> h_nbk;
+  std::vector<int> h_nba;
+  // refinement boundary records (fine side)
+  RBRec* d_rb = nullptr;
+  std::vector<RBRec> h_rb;
+  // my_parents / my_leaves as local indices
+  std::vector<int> parents, leaves;
+  int* d_parents = nullptr;
+  int* d_leaves = nullptr;
+  // restriction onto this level from lvl+1 happens per fine box: for each of my
+  // boxes at this level, the parent (local idx at lvl-1, or -1 if remote) and
+  // its child offset inside the parent.
+  std::vector<int> parent_local;        // [n]
+  std::vector<int> dix_packed;          // [n]  dx | dy<<10 | dz<<20
+  int* d_parent_local = nullptr;
+  int* d_dix = nullptr;
+  // local (child, parent) pairs for restriction / prolongation at this level
+  // (this level = fine level)
+  int* d_pairs = nullptr;               // [n_pairs] child local idx
+  int n_pairs = 0;
+  // transfers
+  Transfer halo;        // ghost faces of this level (items: box*6+nb)
+  Transfer restr;       // restriction this level -> lvl-1 (send: child idx; recv: parent*8+slot)
+  Transfer prol;        // prolongation lvl-1 -> this level (send: child global → parent idx*8+slot; recv: my child idx)
+  double* d_sendbuf = nullptr;
+  double* d_recvbuf = nullptr;
+  size_t sendbuf_doubles = 0, recvbuf_doubles = 0;
+  // per-leaf partial sums scratch
+  double* d_scratch = nullptr;
+
+  LevelView view() const {
+    LevelView v;
+    v.data = d_data;
+    v.stride = stride;
+    v.vstride = stride * n;
+    v.n = n;
+    v.nc = nc;
+    for (int d = 0; d < 3; d++) {
+      v.idr2[d] = 1 / (dr[d] * dr[d]);
+      v.dr[d] = dr[d];
+    }
+    v.nbk = d_nbk;
+    v.nba = d_nba;
+    return v;
+  }
+};
+
+struct PendingEv {
+  const char* name;
+  hipEvent_t e0, e1;
+  double cells;
+};
+
+struct KStat {
+  long long launches = 0;
+  double ms = 0, cells = 0;
+};
+
+}  // namespace omg
+
+struct omg_ctx {
+  int device = 0, rank = 0, n_ranks = 1;
+  hipStream_t stream = nullptr;
+  void* nccl = nullptr;  // ncclComm_t
+  // tree (global, host)
+  int n_boxes = 0, lowest = 0, highest = 0, first_normal = 0, box_size = 0, n_vars = 4;
+  std::vector<int> lvl, parent, children, neighbors, ix, rank_of;
+  std::map<int, int> bsl;                   // box_size_lvl
+  std::map<int, std::vector<double>> drl;   // dr per level
+  std::map<int, std::vector<int>> ids, leaves, parents, ref_bnds;
+  std::vector<int> local_index;             // id -> local index at its level (or -1)
+  std::map<int, omg::Level> levels;
+  // method configuration
+  int op = omg::OP_LPL, smoother = 1, n_substeps = 1;
+  int n_cycle_down = 2, n_cycle_up = 2, max_coarse_cycles = 1000;
+  double lambda = 0, res_abs = 1e-8, res_rel = 1e-8;
+  int subtract_mean = 0, phi_bc_data_stored = 0;
+  omg::BCVar bc[omg::kMaxVars];
+  std::vector<long long> h_face_off[omg::kMaxVars];
+  std::vector<int> h_face_type[omg::kMaxVars];
+  double* d_face_data[omg::kMaxVars] = {};
+  std::map<int, long long*> d_face_off_lvl[omg::kMaxVars];
+  std::map<int, int*> d_face_type_lvl[omg::kMaxVars];
+  // scalars
+  double* d_scalar = nullptr;          // small device scratch
+  double* h_scalar = nullptr;          // pinned host scratch
+  // profiling
+  bool profiling = false;
+  std::map<std::string, omg::KStat> stats;
+  std::vector<omg::PendingEv> pending;
+};

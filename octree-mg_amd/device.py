@@ -1,0 +1,145 @@
+"""ctypes binding of libomg.so (the HIP library behind include/omg.h).
+
+The product path always goes through this library: if it is missing or fails
+to load, every call raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_P, _I, _D, _LL = C.c_void_p, C.c_int, C.c_double, C.c_longlong
+_IP = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_DP = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_LP = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+
+# every symbol include/omg.h declares, with its ctypes signature
+SIGNATURES = {
+    "omg_last_error": (C.c_char_p, []),
+    "omg_get_unique_id": (_I, [C.c_char_p]),
+    "omg_ctx_create": (_I, [C.POINTER(_P), _I, _I, _I, C.c_char_p]),
+    "omg_ctx_destroy": (_I, [_P]),
+    "omg_tree_setup": (_I, [_P, _I, _IP, _IP, _IP, _IP, _IP, _IP, _I, _I, _I, _I, _IP, _DP,
+                            _IP, _IP, _I]),
+    "omg_set_operator": (_I, [_P, _I, _D]),
+    "omg_set_smoother": (_I, [_P, _I, _I, _I, _I, _D, _D]),
+    "omg_set_subtract_mean": (_I, [_P, _I]),
+    "omg_set_bc": (_I, [_P, _I, _I, _I, _D]),
+    "omg_set_bc_faces": (_I, [_P, _I, _LP, _IP, _DP, _LL]),
+    "omg_level_size": (_I, [_P, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "omg_upload_level": (_I, [_P, _I, _I, _DP]),
+    "omg_download_level": (_I, [_P, _I, _I, _DP]),
+    "omg_fas_vcycle": (_I, [_P, _I, _I, C.POINTER(_D), _I]),
+    "omg_fas_fmg": (_I, [_P, _I, _I, C.POINTER(_D)]),
+    "omg_apply_op": (_I, [_P, _I]),
+    "omg_restrict": (_I, [_P, _I]),
+    "omg_restrict_lvl": (_I, [_P, _I, _I]),
+    "omg_fill_ghost_cells": (_I, [_P, _I]),
+    "omg_fill_ghost_cells_lvl": (_I, [_P, _I, _I]),
+    "omg_prolong": (_I, [_P, _I, _I, _I, _I]),
+    "omg_smooth_boxes": (_I, [_P, _I, _I]),
+    "omg_update_coarse": (_I, [_P, _I]),
+    "omg_correct_children": (_I, [_P, _I]),
+    "omg_residual_lvl": (_I, [_P, _I]),
+    "omg_max_residual_lvl": (_I, [_P, _I, C.POINTER(_D)]),
+    "omg_get_sum": (_I, [_P, _I, C.POINTER(_D)]),
+    "omg_subtract_mean": (_I, [_P, _I, _I]),
+    "omg_phi_bc_store": (_I, [_P]),
+    "omg_synchronize": (_I, [_P]),
+    "omg_stream": (_P, [_P]),
+    "omg_set_profiling": (_I, [_P, _I]),
+    "omg_kernel_stats": (_I, [_P, C.c_char_p, C.POINTER(_LL), C.POINTER(_D), C.POINTER(_D)]),
+    "omg_reset_stats": (_I, [_P]),
+}
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "libomg.so")
+
+
+def lib():
+    """Load libomg.so (raises if absent — no fallback)."""
+    global _LIB
+    if _LIB is None:
+        p = lib_path()
+        if not os.path.exists(p):
+            raise RuntimeError(f"octree-mg HIP library not built: {p} (run __graft_entry__.build())")
+        L = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+class OmgError(RuntimeError):
+    pass
+
+
+def check(rc: int):
+    if rc != 0:
+        raise OmgError(lib().omg_last_error().decode())
+
+
+def unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check(lib().omg_get_unique_id(buf))
+    return buf.raw
+
+
+class Context:
+    """One device context (one rank, one GPU)."""
+
+    def __init__(self, device=0, rank=0, n_ranks=1, uid: bytes | None = None):
+        self.L = lib()
+        h = _P()
+        check(self.L.omg_ctx_create(C.byref(h), device, rank, n_ranks, uid))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            check(self.L.omg_ctx_destroy(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def call(self, name, *args):
+        check(getattr(self.L, "omg_" + name)(self.h, *args))
+
+    def stream(self) -> int:
+        return self.L.omg_stream(self.h) or 0
+
+    def level_size(self, lvl):
+        n, nc = _I(), _I()
+        self.call("level_size", lvl, C.byref(n), C.byref(nc))
+        return n.value, nc.value
+
+    def upload_level(self, lvl, iv, data):
+        self.call("upload_level", lvl, iv, np.ascontiguousarray(data, dtype=np.float64).reshape(-1))
+
+    def download_level(self, lvl, iv):
+        n, nc = self.level_size(lvl)
+        out = np.empty(n * (nc + 2) ** 3)
+        if n:
+            self.call("download_level", lvl, iv, out)
+        return out.reshape(n, nc + 2, nc + 2, nc + 2)
+
+    def scalar(self, name, *args):
+        r = _D(0.0)
+        self.call(name, *args, C.byref(r))
+        return r.value
+
+    def kernel_stats(self, name):
+        n, ms, cells = _LL(0), _D(0), _D(0)
+        self.call("kernel_stats", name.encode(), C.byref(n), C.byref(ms), C.byref(cells))
+        return n.value, ms.value, cells.value

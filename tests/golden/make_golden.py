@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors in tests/golden/golden.json.
+
+Runs the REFERENCE octree-mg itself (compiled from /root/reference/src by
+`make -C oracle ref`, amdflang -O2 + MPICH) through oracle/omg_golden for
+every configuration below, and records per-iteration max error / max residual
+/ max_res as exact IEEE-754 bit patterns, plus the sha256 of the final phi of
+every box (ids order per level, lowest..highest, i fastest) where dumped.
+
+Only the numbers are committed (tests/golden/golden.json); the reference's
+sources and binaries never enter the repository.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.path.join(HERE, "..", "..", "oracle", "_ref")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+# name: (box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres), dump?, ranks
+CONFIGS = {
+    # tests/test_uniform_grid 8 64 64 64 10 f, as shipped (GS)
+    "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
+    "c1_gsrb_v": ("8 64 64 64 10 v gsrb lpl 0 sol sol 1 lb 0", False, [1]),
+    "c1_gs_f": ("8 64 64 64 10 f gs lpl 0 sol sol 1 lb 0", False, [1]),
+    "c1_gsrb_f_maxres": ("8 64 64 64 5 f gsrb lpl 0 sol sol 1 lb 1", False, [1]),
+    "u32_gsrb_v": ("8 32 32 32 6 v gsrb lpl 0 sol sol 1 lb 1", True, [1]),
+    "u32_gs_d0_one": ("8 32 32 32 4 v gs lpl 0 d0 one 1 lbp 1", True, [1]),
+    "u64_box16_gsrb_d0_one": ("16 64 64 64 3 v gsrb lpl 0 d0 one 1 lbp 1", True, [1]),
+    "nonsquare_gsrb": ("8 64 32 32 6 v gsrb lpl 0 sol sol 1 lb 1", True, [1]),
+    "odd48_gsrb": ("8 48 48 48 4 v gsrb lpl 0 d0 sol 1 lb 0", True, [1]),
+    "odd48_gs": ("8 48 48 48 4 v gs lpl 0 d0 sol 1 lb 0", True, [1]),
+    # C3-like periodic GSRB (subtract_mean), rank counts pin the allreduce order
+    "per32_gsrb_v": ("8 32 32 32 10 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
+    "per32_gs_f": ("8 32 32 32 5 f gs lpl 0 per sol 1 lb 1", True, [1]),
+    # C5: Helmholtz, lambda = 10
+    "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
+    "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1]),
+    "helm32_gs_c0": ("8 32 32 32 5 v gs helm 10 c0 sol 1 lb 0", True, [1]),
+    # C4-like: tests/test_refinement (centre-refined AMR tree)
+    "ref2_gs_v": ("8 32 32 32 6 v gs lpl 0 sol sol 2 lb 0", True, [1, 4]),
+    "ref3_gs_f": ("8 32 32 32 5 f gs lpl 0 sol sol 3 lb 1", True, [1]),
+    "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1]),
+    "c4_ref2_box16": ("16 128 128 128 4 v gs lpl 0 sol sol 2 lb 0", False, [1]),
+}
+
+
+def run(args, ranks, dump):
+    cmd = [os.path.join(REF, "omg_golden")] + args.split() + [dump or "x"]
+    if ranks > 1:
+        cmd = [MPIEXEC, "-n", str(ranks)] + cmd
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+    its, t = [], None
+    for line in out.splitlines():
+        f = line.split()
+        if f and f[0] == "IT":
+            its.append({"it": int(f[1]), "err": f[2], "res": f[3], "max_res": f[4]})
+        elif f and f[0] == "TIME":
+            t = float(f[1])
+    return its, t
+
+
+def main():
+    if not os.path.exists(os.path.join(REF, "omg_golden")):
+        sys.exit("build the reference first: make -C oracle ref")
+    golden = {}
+    for name, (args, dump, ranks) in CONFIGS.items():
+        entry = {"args": args, "runs": {}}
+        for r in ranks:
+            with tempfile.TemporaryDirectory() as td:
+                fn = os.path.join(td, "phi.bin") if (dump and r == 1) else None
+                its, t = run(args, r, fn)
+                run_entry = {"history": its, "ref_seconds_per_cycle": t}
+                if fn:
+                    with open(fn, "rb") as f:
+                        b = f.read()
+                    run_entry["phi_sha256"] = hashlib.sha256(b).hexdigest()
+                    run_entry["phi_bytes"] = len(b)
+            entry["runs"][str(r)] = run_entry
+            print(name, r, its[-1]["err"], its[-1]["res"], file=sys.stderr)
+        golden[name] = entry
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py",
+                   "reference": "FermiQ/octree-mg @ 2025-06-14, amdflang -O2, MPICH 3.3.2",
+                   "configs": golden}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

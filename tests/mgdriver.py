@@ -1,0 +1,286 @@
+"""Problem runner shared by the parity tests, smoke() and bench.py.
+
+It replays oracle/omg_golden.f90 (the golden-vector driver that runs the
+reference itself) on either backend:
+
+* ``device`` — the product: the Python host mirror (octree_mg_amd.MG) driving
+  libomg.so on the GPU through the C-ABI;
+* ``oracle`` — the C restatement (oracle/liboracle.so), the checker.
+
+Both start from bit-identical inputs, so their per-iteration histories (and
+the sha256 of the final phi of every box) must agree exactly with each other
+and with tests/golden/golden.json.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import struct
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import __graft_entry__  # noqa: E402
+
+omg = __graft_entry__.load_package()
+T = omg.tree
+P = omg.problems
+
+
+def hexbits(x: float) -> str:
+    return "%016X" % struct.unpack("<Q", struct.pack("<d", float(x)))[0]
+
+
+def parse(args: str) -> dict:
+    f = args.split()
+    return dict(box=int(f[0]), domain=[int(f[1]), int(f[2]), int(f[3])], n_its=int(f[4]),
+                cycle=f[5], smoother=f[6], op=f[7], lam=float(f[8]), bc=f[9], rhs=f[10],
+                n_levels=int(f[11]), lb=f[12], maxres=int(f[13]))
+
+
+def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0):
+    """The tree set-up of omg_golden (reference tests' mg_build_rectangle or
+    build_amr_tree, tests/test_refinement.f90:191-247, then load balance)."""
+    tree.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
+    tree.n_cpu, tree.my_rank = n_ranks, my_rank
+    dom = np.array(cfg["domain"], dtype=np.int64)
+    dr = 1.0 / dom.astype(np.float64)
+    periodic = [cfg["bc"] == "per"] * 3
+    box = cfg["box"]
+    if cfg["n_levels"] <= 1:
+        tree.build_rectangle(dom, box, dr, [0.0, 0.0, 0.0], periodic, 0)
+    else:
+        nl = cfg["n_levels"]
+        n_finer = nl * int(np.prod(dom // box)) + 1000
+        domain_len = dom * dr
+        tree.build_rectangle(dom, box, dr, [0.0, 0.0, 0.0], periodic, n_finer)
+        for lvl in range(1, nl):
+            for id_ in tree.lvls[lvl].ids:
+                r0 = 0.5 * domain_len - domain_len * 0.5 ** (lvl + 1)
+                r1 = 0.5 * domain_len + domain_len * 0.5 ** (lvl + 1)
+                center = tree.box_r_min[id_] + 0.5 * box * tree.box_dr[id_]
+                if np.all((center >= r0) & (center <= r1)):
+                    tree.add_children(int(id_))
+            tree.set_leaves_parents(lvl)
+            tree.set_next_level_ids(lvl)
+            tree.set_neighbors_lvl(lvl + 1)
+        tree.set_leaves_parents(nl)
+        tree.highest_lvl = nl
+        for lvl in range(1, nl + 1):
+            tree.set_refinement_boundaries(lvl)
+    tree.load_balance()
+    if cfg["lb"] == "lbp":
+        tree.load_balance_parents()
+    return tree
+
+
+I_SOL = 5
+N_VARS = 5
+
+
+class OracleBackend:
+    def __init__(self, cfg, n_ranks=1):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle  # checker only
+        self.cfg = cfg
+        self.tree = build_tree(cfg, T.MGTree(), n_ranks)
+        self.o = pyoracle.Oracle(self.tree, N_VARS, n_ranks)
+        op = pyoracle.HELMHOLTZ if cfg["op"] == "helm" else pyoracle.LAPLACIAN
+        sm = pyoracle.GSRB if cfg["smoother"] == "gsrb" else pyoracle.GS
+        sub = bool(self.tree.subtract_mean) or (op == pyoracle.LAPLACIAN and cfg["bc"] == "per")
+        if op == pyoracle.HELMHOLTZ:
+            sub = False
+        self.o.configure(op=op, lam=cfg["lam"], smoother=sm, subtract_mean=sub)
+        _apply_bc(cfg, self.tree, lambda iv, nb, t, v: self.o.set_bc(iv, nb, t, v),
+                  lambda iv, a, b, c: self.o.set_bc_faces(iv, a, b, c))
+
+    def levels(self):
+        return range(self.tree.lowest_lvl, self.tree.highest_lvl + 1)
+
+    def my_ids(self, lvl):
+        return self.tree.lvls[lvl].ids
+
+    def set_level(self, lvl, iv, data):
+        self.o.set_level(lvl, iv, data)
+
+    def get_level(self, lvl, iv):
+        return self.o.get_level(lvl, iv)
+
+    def restrict(self, iv):
+        self.o.restrict(iv)
+
+    def fill_ghost_cells(self, iv):
+        self.o.fill_ghost_cells(iv)
+
+    def apply_op(self, iv):
+        self.o.apply_op(iv)
+
+    def vcycle(self, want):
+        return self.o.fas_vcycle(want_max_res=bool(want))
+
+    def fmg(self, have_guess, want):
+        return self.o.fas_fmg(have_guess, bool(want))
+
+
+class DeviceBackend:
+    def __init__(self, cfg, n_ranks=1, my_rank=0):
+        self.cfg = cfg
+        mg = omg.MG()
+        mg.n_extra_vars = 1
+        mg.operator_type = T.MG_HELMHOLTZ if cfg["op"] == "helm" else T.MG_LAPLACIAN
+        mg.helmholtz_lambda = cfg["lam"]
+        mg.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
+        omg.mg_set_methods(mg)
+        omg.mg_comm_init(mg)
+        build_tree(cfg, mg, mg.n_cpu, mg.my_rank)
+        omg.mg_set_methods(mg)
+
+        def set_bc(iv, nb, t, v):
+            mg.bc[nb][iv] = omg.BC(t, v)
+
+        faces = {}
+
+        def set_faces(iv, off, typ, data):
+            faces[iv] = (off, typ, data)
+
+        _apply_bc(cfg, mg, set_bc, set_faces)
+        omg.mg_allocate_storage(mg)
+        for iv, (off, typ, data) in faces.items():
+            mg.ctx.call("set_bc_faces", iv, off, typ, data, len(data))
+        self.mg = mg
+        self.tree = mg
+
+    def levels(self):
+        return range(self.mg.lowest_lvl, self.mg.highest_lvl + 1)
+
+    def my_ids(self, lvl):
+        return self.mg.lvls[lvl].my_ids
+
+    def set_level(self, lvl, iv, data):
+        if len(self.my_ids(lvl)):
+            self.mg.set_level(lvl, iv, data)
+
+    def get_level(self, lvl, iv):
+        return self.mg.get_level(lvl, iv) if len(self.my_ids(lvl)) else None
+
+    def restrict(self, iv):
+        omg.mg_restrict(self.mg, iv)
+
+    def fill_ghost_cells(self, iv):
+        omg.mg_fill_ghost_cells(self.mg, iv)
+
+    def apply_op(self, iv):
+        omg.mg_apply_op(self.mg, iv)
+
+    def vcycle(self, want):
+        return omg.mg_fas_vcycle(self.mg, max_res=bool(want)) or 0.0
+
+    def fmg(self, have_guess, want):
+        return omg.mg_fas_fmg(self.mg, have_guess, max_res=bool(want)) or 0.0
+
+
+def _apply_bc(cfg, tree, set_bc, set_faces):
+    bc = cfg["bc"]
+    if bc == "sol":
+        off, typ, data = P.callback_bc_faces(tree)
+        set_faces(T.MG_IPHI, off, typ, data)
+    elif bc in ("d0", "n0", "c0"):
+        t = {"d0": T.MG_BC_DIRICHLET, "n0": T.MG_BC_NEUMANN, "c0": T.MG_BC_CONTINUOUS}[bc]
+        for nb in range(1, 7):
+            set_bc(T.MG_IPHI, nb, t, 0.0)
+
+
+def setup_problem(be):
+    """set_solution + compute_rhs_and_reset (tests/test_uniform_grid.f90:
+    137-170), or set_rhs (tests/test_performance.f90:102-115)."""
+    cfg, tree = be.cfg, be.tree
+    if cfg["rhs"] == "sol":
+        for lvl in be.levels():
+            ids = be.my_ids(lvl)
+            if len(ids):
+                be.set_level(lvl, I_SOL, P.level_solution(tree, lvl, ids))
+        if cfg["n_levels"] > 1:
+            be.restrict(I_SOL)
+            be.fill_ghost_cells(I_SOL)
+        for lvl in be.levels():
+            if len(be.my_ids(lvl)):
+                be.set_level(lvl, T.MG_IPHI, be.get_level(lvl, I_SOL))
+        be.apply_op(T.MG_IRHS)
+        for lvl in be.levels():
+            ids = be.my_ids(lvl)
+            if len(ids):
+                nc = tree.box_size_lvl[lvl]
+                be.set_level(lvl, T.MG_IPHI, np.zeros((len(ids), nc + 2, nc + 2, nc + 2)))
+    else:
+        for lvl in be.levels():
+            ids = be.my_ids(lvl)
+            if len(ids):
+                nc = tree.box_size_lvl[lvl]
+                a = np.zeros((len(ids), nc + 2, nc + 2, nc + 2))
+                a[:, 1:nc + 1, 1:nc + 1, 1:nc + 1] = 1.0
+                be.set_level(lvl, T.MG_IRHS, a)
+
+
+def measure(be):
+    """print_state of omg_golden: max |phi-u| and max |res| over the leaves of
+    levels >= 1 (this rank's boxes)."""
+    tree = be.tree
+    err = res = 0.0
+    for lvl in range(1, tree.highest_lvl + 1):
+        ids = list(be.my_ids(lvl))
+        if not ids:
+            continue
+        nc = tree.box_size_lvl[lvl]
+        leaves = set(int(x) for x in tree.lvls[lvl].leaves)
+        sel = [n for n, i in enumerate(ids) if int(i) in leaves]
+        if not sel:
+            continue
+        phi = be.get_level(lvl, T.MG_IPHI)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        sol = be.get_level(lvl, I_SOL)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        r = be.get_level(lvl, T.MG_IRES)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        err = max(err, float(np.max(np.abs(phi - sol))))
+        res = max(res, float(np.max(np.abs(r))))
+    return err, res
+
+
+def phi_digest(be):
+    h = hashlib.sha256()
+    for lvl in be.levels():
+        ids = be.my_ids(lvl)
+        if not len(ids):
+            continue
+        nc = be.tree.box_size_lvl[lvl]
+        phi = be.get_level(lvl, T.MG_IPHI)[:, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        h.update(np.ascontiguousarray(phi).tobytes())
+    return h.hexdigest()
+
+
+def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None):
+    """Run one omg_golden configuration; returns {'history': [...], 'phi_sha256'}.
+
+    reduce(err, res) -> (err, res) combines per-rank maxima for multi-rank runs."""
+    cfg = parse(args)
+    if n_its is not None:
+        cfg["n_its"] = n_its
+    be = OracleBackend(cfg, n_ranks) if backend == "oracle" else DeviceBackend(cfg)
+    setup_problem(be)
+    hist = []
+
+    def record(it, mres):
+        e, r = measure(be)
+        if reduce is not None:
+            e, r = reduce(e, r)
+        hist.append({"it": it, "err": hexbits(e), "res": hexbits(r), "max_res": hexbits(mres)})
+
+    record(0, 0.0)
+    for n in range(1, cfg["n_its"] + 1):
+        if cfg["cycle"] == "f":
+            m = be.fmg(n > 1, cfg["maxres"])
+        else:
+            m = be.vcycle(cfg["maxres"])
+        record(n, m if cfg["maxres"] else 0.0)
+    return {"history": hist, "phi_sha256": phi_digest(be), "backend": be}
