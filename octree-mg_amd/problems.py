@@ -43,11 +43,18 @@ def box_solution(tree, id_: int) -> np.ndarray:
 
 
 def level_solution(tree, lvl: int, ids=None) -> np.ndarray:
-    ids = tree.lvls[lvl].ids if ids is None else ids
+    """u on every box of a level, [box, k, j, i].  u is separable, so the three
+    sines are evaluated per box row and multiplied as (s_x*s_y)*s_z — the
+    same roundings as box_solution() cell by cell."""
+    ids = np.asarray(tree.lvls[lvl].ids if ids is None else ids, dtype=np.int64)
     nc = tree.box_size_lvl[lvl]
     if len(ids) == 0:
         return np.zeros((0, nc + 2, nc + 2, nc + 2))
-    return np.stack([box_solution(tree, int(i)) for i in ids])
+    dr = tree.dr[lvl]
+    idx = np.arange(0, nc + 2, dtype=np.float64) - 0.5
+    rmin = tree.box_r_min[ids]                                   # [b, 3]
+    s = [np.sin(TWO_PI_N * (rmin[:, d:d + 1] + idx[None, :] * dr[d])) for d in range(3)]
+    return (s[0][:, None, None, :] * s[1][:, None, :, None]) * s[2][:, :, None, None]
 
 
 def callback_bc_faces(tree, boxes=None):
