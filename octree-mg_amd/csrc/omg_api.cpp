@@ -225,40 +225,70 @@ GcBC bc_for(omg_ctx* c, int lvl, int iv) {
   return g;
 }
 
-// mg_fill_ghost_cells_lvl (m_ghost_cells.f90:131-175)
+// phi was written on a level: its ghost faces may no longer match a fill
+void phi_dirty(omg_ctx* c, int lvl) {
+  if (Level* L = level_ptr(c, lvl)) L->phi_gc_ok = false;
+}
+void phi_dirty_all(omg_ctx* c) {
+  for (auto& kv : c->levels) kv.second.phi_gc_ok = false;
+}
+
+// halo exchange of the faces packed by the last fill/substep kernel, then
+// fill_buffered_nb (m_ghost_cells.f90:163-174, 424-454)
+void finish_halo(omg_ctx* c, Level* L, int iv) {
+  if (c->n_ranks == 1 || !(L->halo.n_send || L->halo.n_recv)) return;
+  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
+  launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+}
+
+// mg_fill_ghost_cells_lvl (m_ghost_cells.f90:131-175): same-GPU faces are
+// pushed by their owner, physical / refinement-boundary ghosts recomputed,
+// remote faces packed, exchanged over RCCL and unpacked.
 void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (lvl < c->lowest) throw OmgError("fill_ghost_cells_lvl: lvl < lowest_lvl");
   if (lvl > c->highest) throw OmgError("fill_ghost_cells_lvl: lvl > highest_lvl");
   Level* L = level_ptr(c, lvl);
   if (!L) return;
-  const LevelView V = L->view();
-  if (c->n_ranks > 1 && (L->halo.n_send || L->halo.n_recv)) {
-    launch_pack_faces(V, iv, L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, c->stream);
-    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
+  if (iv == 1) L->phi_gc_ok = true;
+  if (L->n) {
+    Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc);
+    launch_fill_gc(L->view(), iv, 3, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_sendbuf,
+                   c->stream);
   }
-  if (L->n == 0) return;
-  Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc);
-  launch_fill_gc(V, iv, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_recvbuf, c->stream);
-}
-
-void box_smoother_lvl(omg_ctx* c, int lvl, int cntr) {
-  Level* L = level_ptr(c, lvl);
-  if (!L || L->n == 0) return;
-  const double cells = (double)L->n * L->nc * L->nc * L->nc;
-  if (c->smoother == OMG_SMOOTHER_GSRB) {
-    Prof p(c, "smoother_gsrb", 0.5 * cells);
-    launch_gsrb(L->view(), c->op, c->lambda, cntr, c->stream);
-  } else {
-    Prof p(c, "smoother_gs", cells);
-    launch_gs_lex(L->view(), c->op, c->lambda, c->stream);
-  }
+  finish_halo(c, L, iv);
 }
 
 // smooth_boxes (m_multigrid.f90:404-424)
 void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
-  for (int n = 1; n <= n_cycle * c->n_substeps; n++) {
-    box_smoother_lvl(c, lvl, n);
-    fill_gc_lvl(c, lvl, 1);
+  Level* L = level_ptr(c, lvl);
+  const int n_sub = n_cycle * c->n_substeps;
+  if (!L) return;
+  if (c->smoother != OMG_SMOOTHER_GSRB) {
+    for (int n = 1; n <= n_sub; n++) {
+      if (L->n) {
+        Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream);
+      }
+      fill_gc_lvl(c, lvl, 1);
+    }
+    return;
+  }
+  for (int n = 1; n <= n_sub; n++) {
+    // substep n updates the cells with i+j+k+n even, i.e. colour e = n mod 2,
+    // and ends with the ghost fill; same-GPU neighbours only need colour e
+    // when their ghost faces were consistent before the substep.
+    // For odd box sizes the box-local colouring is not global (a ghost has the
+    // colour of the cell it is read by), so nothing is pushed during the
+    // substep and a full fill follows it.
+    const int e = n & 1;
+    const bool odd = L->nc & 1;
+    if (L->n) {
+      Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc);
+      launch_gs_substep(L->view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
+                        L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, c->stream);
+    }
+    finish_halo(c, L, 1);
+    if (odd || !L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
   }
 }
 
@@ -282,6 +312,7 @@ double max_residual_lvl(omg_ctx* c, int lvl) {
 // mg_restrict_lvl (m_restrict.f90:83-114)
 void restrict_lvl(omg_ctx* c, int iv, int lvl) {
   if (lvl <= c->lowest) throw OmgError("cannot restrict lvl <= lowest_lvl");
+  if (iv == 1) phi_dirty(c, lvl - 1);
   Level* F = level_ptr(c, lvl);
   Level* C = level_ptr(c, lvl - 1);
   const LevelView FV = view_of(c, lvl), CV = view_of(c, lvl - 1);
@@ -301,11 +332,12 @@ void restrict_lvl(omg_ctx* c, int iv, int lvl) {
 void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
   if (lvl == c->highest) throw OmgError("cannot prolong highest level");
   if (lvl < c->lowest) throw OmgError("cannot prolong below lowest level");
+  if (iv_to == 1) phi_dirty(c, lvl + 1);
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
   const LevelView FV = view_of(c, lvl + 1), CV = view_of(c, lvl);
   if (c->n_ranks > 1 && F && C && (F->prol.n_send || F->prol.n_recv)) {
-    launch_prolong_pack(CV, iv, F->nc, F->prol.d_send_items, F->prol.n_send, C->d_sendbuf, c->stream);
+    launch_prolong_pack(CV, FV, iv, F->prol.d_send_items, F->prol.n_send, C->d_sendbuf, c->stream);
     exchange(c, F->prol, C->d_sendbuf, F->d_recvbuf);
     launch_prolong_unpack(FV, iv_to, add, F->prol.d_recv_items, F->prol.n_recv, F->d_recvbuf,
                           c->stream);
@@ -374,6 +406,7 @@ double get_sum(omg_ctx* c, int iv) {
 // subtract_mean (m_multigrid.f90:245-276)
 void subtract_mean(omg_ctx* c, int iv, int ghosts) {
   const int nc = c->box_size;
+  if (iv == 1) phi_dirty_all(c);
   double mean = get_sum(c, iv);
   const auto& d1 = c->drl[1];
   const double volume = (double)(nc * nc * nc) * (d1[0] * d1[1] * d1[2]) * (double)c->ids[1].size();
@@ -426,6 +459,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
 
 // mg_fas_fmg (m_multigrid.f90:84-147)
 double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
+  if (!have_guess) phi_dirty_all(c);
   if (!have_guess)
     for (int l = c->highest; l >= c->lowest; l--) {
       Level* L = level_ptr(c, l);
@@ -457,7 +491,7 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
 void free_levels(omg_ctx* c) {
   for (auto& kv : c->levels) {
     Level& L = kv.second;
-    dfree(L.d_data); dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_rb);
+    dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol}) {
@@ -490,8 +524,7 @@ void build_plan(omg_ctx* c) {
         L.ids.push_back(id);
       }
     L.n = (int)L.ids.size();
-    const long long s = L.nc + 2;
-    L.stride = ((s * s * s + 63) / 64) * 64;
+    L.stride = ((stored_cells(L.nc) + 63) / 64) * 64;   // 512-B aligned boxes
   }
   for (int l = c->lowest; l <= c->highest; l++) {
     Level& L = c->levels[l];
@@ -544,16 +577,22 @@ void build_plan(omg_ctx* c) {
     L.halo.send = group(hsend, 1);
     L.halo.send_ints = L.halo.recv_ints = 1;
     L.halo.item_doubles = nc * nc;
-    // receive slot of every remote face = its position in the receive buffer
+    // receive slot of every remote face = its position in the receive buffer;
+    // send slot = its position in the send buffer (wire order of each peer)
+    std::vector<int> sendpos((size_t)L.n * 6, -1);
     {
       int pos = 0;
       for (auto& p : L.halo.recv)
-        for (int& it : p.items) {
-          const int f = it;
-          L.h_nba[f] = pos++;
-        }
+        for (int f : p.items) L.h_nba[f] = pos++;
+      pos = 0;
+      for (auto& p : L.halo.send)
+        for (int f : p.items) sendpos[f] = pos++;
     }
     finalize_transfer(L.halo);
+    L.has_rb = !L.h_rb.empty();
+    L.has_remote = L.halo.n_send || L.halo.n_recv;
+    L.d_phi = L.d_data;
+    L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);
     L.d_nba = to_device(L.h_nba);
     L.d_rb = to_device(L.h_rb);
@@ -695,6 +734,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     free_levels(c);
     dfree(c->d_scalar);
+    dfree(c->d_stage);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
     (void)hipStreamDestroy(c->stream);
@@ -773,6 +813,7 @@ int omg_set_subtract_mean(omg_ctx* c, int on) {
 
 int omg_set_bc(omg_ctx* c, int iv, int nb, int bc_type, double bc_value) {
   return guarded([&] {
+    phi_dirty_all(c);
     if (iv < 1 || iv > kMaxVars || nb < 1 || nb > 6) throw OmgError("omg_set_bc: bad iv/nb");
     c->bc[iv - 1].type[nb - 1] = bc_type;
     c->bc[iv - 1].value[nb - 1] = bc_value;
@@ -783,6 +824,7 @@ int omg_set_bc_faces(omg_ctx* c, int iv, const long long* face_off, const int* f
                      const double* data, long long n_data) {
   return guarded([&] {
     if (iv < 1 || iv > kMaxVars) throw OmgError("omg_set_bc_faces: bad iv");
+    phi_dirty_all(c);
     const int k = iv - 1;
     for (auto& kv : c->d_face_off_lvl[k]) dfree(kv.second);
     for (auto& kv : c->d_face_type_lvl[k]) dfree(kv.second);
@@ -823,16 +865,27 @@ int omg_level_size(omg_ctx* c, int lvl, int* n_boxes, int* nc) {
   });
 }
 
+// staging buffer in the reference's box layout
+double* stage(omg_ctx* c, size_t n) {
+  if (n > c->stage_n) {
+    dfree(c->d_stage);
+    HIPCHK(hipMalloc(&c->d_stage, sizeof(double) * n));
+    c->stage_n = n;
+  }
+  return c->d_stage;
+}
+
 int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
   return guarded([&] {
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
     if (!L->n) return;
-    const long long s = L->nc + 2, n3 = s * s * s;
-    HIPCHK(hipMemcpy2DAsync(L->d_data + (size_t)(iv - 1) * L->n * L->stride, sizeof(double) * L->stride,
-                            host, sizeof(double) * n3, sizeof(double) * n3, L->n,
-                            hipMemcpyHostToDevice, c->stream));
+    const size_t s = L->nc + 2, n = s * s * s * L->n;
+    if (iv == 1) L->phi_gc_ok = false;
+    double* st = stage(c, n);
+    HIPCHK(hipMemcpyAsync(st, host, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    launch_from_ref(L->view(), iv, st, c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
   });
 }
@@ -843,10 +896,10 @@ int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
     if (!L->n) return;
-    const long long s = L->nc + 2, n3 = s * s * s;
-    HIPCHK(hipMemcpy2DAsync(host, sizeof(double) * n3,
-                            L->d_data + (size_t)(iv - 1) * L->n * L->stride, sizeof(double) * L->stride,
-                            sizeof(double) * n3, L->n, hipMemcpyDeviceToHost, c->stream));
+    const size_t s = L->nc + 2, n = s * s * s * L->n;
+    double* st = stage(c, n);
+    launch_to_ref(L->view(), iv, st, c->stream);
+    HIPCHK(hipMemcpyAsync(host, st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   });
 }
@@ -867,6 +920,7 @@ int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
 
 int omg_apply_op(omg_ctx* c, int i_out) {
   return guarded([&] {
+    if (i_out == 1) phi_dirty_all(c);
     for (int l = c->lowest; l <= c->highest; l++) {
       Level* L = level_ptr(c, l);
       if (L && L->n) launch_box_op(L->view(), c->op, c->lambda, i_out, c->stream);
@@ -915,63 +969,24 @@ int omg_subtract_mean(omg_ctx* c, int iv, int include_ghostcells) {
   return guarded([&] { subtract_mean(c, iv, include_ghostcells); });
 }
 
-// mg_phi_bc_store (m_ghost_cells.f90:66-117): bc values of phi go into the
-// rhs ghost cells, the bc type into the neighbour slot.
+// mg_phi_bc_store (m_ghost_cells.f90:66-117): the bc values of phi go into
+// the rhs ghost cells and the bc type into the neighbour slot.
 int omg_phi_bc_store(omg_ctx* c) {
   return guarded([&] {
+    phi_dirty_all(c);
     for (auto& kv : c->levels) {
       Level& L = kv.second;
       if (!L.n) continue;
-      // store bc values into rhs ghosts: fill var 2's ghost faces of physical
-      // boundaries with the bc values (box_set_gc), then the types.
       GcBC g = bc_for(c, kv.first, 1);
-      // write bc values via a Dirichlet-free path: c0=1,c1=c2=0 is not a bc
-      // type, so do it on the host for the (few) physical faces.
-      const long long s = L.nc + 2, n3 = s * s * s;
-      std::vector<double> rhs((size_t)L.n * n3);
-      HIPCHK(hipMemcpy2D(rhs.data(), sizeof(double) * n3, L.d_data + (size_t)L.n * L.stride,
-                         sizeof(double) * L.stride, sizeof(double) * n3, L.n, hipMemcpyDeviceToHost));
-      std::vector<long long> off;
-      std::vector<int> typ;
-      if (g.face_off) {
-        off.resize(L.n * 6);
-        typ.resize(L.n * 6);
-        HIPCHK(hipMemcpy(off.data(), g.face_off, sizeof(long long) * L.n * 6, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(typ.data(), g.face_type, sizeof(int) * L.n * 6, hipMemcpyDeviceToHost));
-      }
-      std::vector<double> fdata;
-      if (g.face_data) {
-        size_t tot = 0;
-        for (size_t q = 0; q < off.size(); q++)
-          if (off[q] >= 0) tot = std::max(tot, (size_t)off[q] + (size_t)L.nc * L.nc);
-        fdata.resize(tot);
-        if (tot) HIPCHK(hipMemcpy(fdata.data(), g.face_data, sizeof(double) * tot, hipMemcpyDeviceToHost));
-      }
-      const int nc = L.nc;
+      g.phi_stored = 0;
+      launch_phi_bc_store(L.view(), g, L.d_nba, c->stream);
+      HIPCHK(hipMemcpyAsync(L.h_nba.data(), L.d_nba, sizeof(int) * L.h_nba.size(), hipMemcpyDeviceToHost,
+                            c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
       for (int b = 0; b < L.n; b++)
-        for (int nb = 1; nb <= 6; nb++) {
-          const size_t f = (size_t)b * 6 + nb - 1;
-          if (L.h_nbk[f] != NB_PHYS) continue;
-          int type;
-          const bool tab = !off.empty() && off[f] >= 0;
-          type = tab ? typ[f] : c->bc[0].type[nb - 1];
-          const int d = (nb + 1) / 2;
-          const int g0 = (nb & 1) ? 0 : nc + 1;
-          for (int cc = 1; cc <= nc; cc++)
-            for (int a = 1; a <= nc; a++) {
-              const double v = tab ? fdata[off[f] + (a - 1) + (size_t)nc * (cc - 1)] : c->bc[0].value[nb - 1];
-              long long idx;
-              if (d == 1) idx = g0 + s * (a + s * cc);
-              else if (d == 2) idx = a + s * (g0 + s * cc);
-              else idx = a + s * (cc + s * g0);
-              rhs[(size_t)b * n3 + idx] = v;
-            }
-          L.h_nba[f] = type;
-          c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = type;
-        }
-      HIPCHK(hipMemcpy2D(L.d_data + (size_t)L.n * L.stride, sizeof(double) * L.stride, rhs.data(),
-                         sizeof(double) * n3, sizeof(double) * n3, L.n, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(L.d_nba, L.h_nba.data(), sizeof(int) * L.h_nba.size(), hipMemcpyHostToDevice));
+        for (int nb = 1; nb <= 6; nb++)
+          if (L.h_nbk[(size_t)b * 6 + nb - 1] == NB_PHYS)
+            c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = L.h_nba[(size_t)b * 6 + nb - 1];
     }
     c->phi_bc_data_stored = 1;
   });

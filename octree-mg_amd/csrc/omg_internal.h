@@ -33,18 +33,29 @@ struct BCVar {
   int* d_face_type = nullptr;
 };
 
-// A view of one level, passed to kernels by value.
+// A view of one level, passed to kernels by value (layout: omg_device.h).
 struct LevelView {
   double* data;          // [n_vars][n][stride]
-  long long stride;      // doubles per box
+  double* phi;           // phi (= var 1 of data)
+  long long stride;      // doubles per box and variable
   long long vstride;     // doubles per variable = n * stride
   int n;                 // local boxes
   int nc;                // box size (cells per dim)
+  int h, hf;             // ceil(nc/2): cells of one colour per row / per face row
+  int hv;                // h*nc*nc: slots of one colour of the interior
+  int fs;                // 2*hf*nc: slots of one ghost face
   double idr2[3];        // 1/dr^2 per dim
   double dr[3];
   const int8_t* nbk;     // [n*6]
   const int* nba;        // [n*6]
+  const int* sendpos;    // [n*6] halo send slot of remote faces (or -1)
 };
+
+// stored doubles per box and variable for box size nc (2 colours + 6 faces)
+inline int stored_cells(int nc) {
+  const int h = (nc + 1) / 2;
+  return 2 * h * nc * nc + 6 * 2 * h * nc;
+}
 
 // Grid-transfer records.
 struct RBRec {             // refinement boundary: coarse neighbour + child offset
@@ -73,8 +84,12 @@ struct Level {
   double dr[3] = {0, 0, 0};
   std::vector<int> ids;                 // global ids of my boxes (my_ids order)
   double* d_data = nullptr;
+  double* d_phi = nullptr;              // phi (d_data's var 1)
+  bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
+  bool has_rb = false, has_remote = false;
   int8_t* d_nbk = nullptr;
   int* d_nba = nullptr;
+  int* d_sendpos = nullptr;
   std::vector<int8_t> h_nbk;
   std::vector<int> h_nba;
   // refinement boundary records (fine side)
@@ -108,16 +123,21 @@ struct Level {
   LevelView view() const {
     LevelView v;
     v.data = d_data;
+    v.phi = d_phi;
     v.stride = stride;
     v.vstride = stride * n;
     v.n = n;
     v.nc = nc;
+    v.h = v.hf = (nc + 1) / 2;
+    v.hv = v.h * nc * nc;
+    v.fs = 2 * v.hf * nc;
     for (int d = 0; d < 3; d++) {
       v.idr2[d] = 1 / (dr[d] * dr[d]);
       v.dr[d] = dr[d];
     }
     v.nbk = d_nbk;
     v.nba = d_nba;
+    v.sendpos = d_sendpos;
     return v;
   }
 };
@@ -161,6 +181,8 @@ struct omg_ctx {
   // scalars
   double* d_scalar = nullptr;          // small device scratch
   double* h_scalar = nullptr;          // pinned host scratch
+  double* d_stage = nullptr;           // upload/download staging (reference layout)
+  size_t stage_n = 0;
   // profiling
   bool profiling = false;
   std::map<std::string, omg::KStat> stats;

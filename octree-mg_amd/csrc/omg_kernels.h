@@ -1,11 +1,11 @@
-// omg_kernels.h — launchers of the level kernels (omg_kernels.hip).
+// omg_kernels.h — launchers of the level kernels (omg_kernels.hip, omg_sweep.hip).
 #pragma once
 
 #include "omg_internal.h"
 
 namespace omg {
 
-// Physical-boundary description passed to the ghost-cell kernel.
+// Physical-boundary description passed to the ghost-cell kernels.
 struct GcBC {
   int type[6];
   double value[6];
@@ -15,14 +15,20 @@ struct GcBC {
   int phi_stored;              // mg%phi_bc_data_stored
 };
 
-void launch_gsrb(const LevelView& L, int op, double lambda, int cntr, hipStream_t st);
+// red-black substep (colour e) + the ghost fill after it; picks the LDS-tiled
+// kernel (omg_sweep.hip) when the level allows, else the generic one
+void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
+                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, hipStream_t st);
+void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
+                   const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st);
 void launch_box_op(const LevelView& L, int op, double lambda, int i_out, hipStream_t st);
 void launch_residual(const LevelView& L, int op, double lambda, unsigned long long* maxbits,
                      hipStream_t st);
-void launch_fill_gc(const LevelView& L, int iv, const LevelView& C, const RBRec* rb, const GcBC& bc,
-                    const double* recv, hipStream_t st);
-void launch_pack_faces(const LevelView& L, int iv, const int* items, int n, double* buf, hipStream_t st);
+void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C, const RBRec* rb,
+                    const GcBC& bc, double* sendbuf, hipStream_t st);
+void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, const double* recv,
+                         hipStream_t st);
 void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* pairs, int n_pairs,
                      const int* parent_local, const int* dixp, hipStream_t st);
 void launch_restrict_pack(const LevelView& F, int iv, const int* items, int n, double* buf,
@@ -34,13 +40,16 @@ void launch_coarse_rhs(const LevelView& C, int op, double lambda, const int* par
 void launch_sub_parents(const LevelView& C, const int* parents, int n_par, hipStream_t st);
 void launch_prolong(const LevelView& C, const LevelView& F, int iv, int iv_to, int add, const int* pairs,
                     int n_pairs, const int* parent_local, const int* dixp, hipStream_t st);
-void launch_prolong_pack(const LevelView& C, int iv, int nc, const int* items, int n, double* buf,
-                         hipStream_t st);
+void launch_prolong_pack(const LevelView& C, const LevelView& F, int iv, const int* items, int n,
+                         double* buf, hipStream_t st);
 void launch_prolong_unpack(const LevelView& F, int iv_to, int add, const int* items, int n,
                            const double* buf, hipStream_t st);
 void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
 void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st);
 void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts, hipStream_t st);
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st);
+void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t st);
+void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st);
+void launch_phi_bc_store(const LevelView& L, const GcBC& bc, int* nba, hipStream_t st);
 
 }  // namespace omg

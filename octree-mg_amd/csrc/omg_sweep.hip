@@ -1,0 +1,175 @@
+// omg_sweep.hip — the LDS-tiled red-black Gauss-Seidel substep (the hot kernel).
+//
+// One launch = one substep of smooth_boxes over a whole level plus the ghost
+// fill the reference runs after it (src/m_multigrid.f90:412-423):
+//   for every box: colour e = (substep counter) mod 2 is updated from colour
+//   1-e (box_gs_lpl / box_gs_helmh, m_laplacian.f90:52-114,
+//   m_helmholtz.f90:49-108), then the box pushes its new colour-e boundary
+//   values into the ghost faces of its same-GPU neighbours, recomputes its
+//   physical-boundary ghosts (bc_to_gc, m_ghost_cells.f90:665-766) and packs
+//   its faces toward other GPUs for the RCCL halo exchange.
+//
+// Traffic per box of 16^3 (colour-split layout, omg_device.h): colour 1-e of
+// phi (16 KB) + its ghost halves (6 KB) + colour e of rhs (16 KB) in, colour e
+// of phi (16 KB) + pushed ghost halves (6 KB) out: ~60 KB per substep, all
+// contiguous, against the 48 KB the 12 B/cell algorithmic figure counts.
+//
+// Workgroup = one box; blockIdx is remapped so that each XCD walks one
+// contiguous (Morton-ordered) run of boxes and neighbours share its L2.
+// Colour e reads only colour 1-e and neighbours receive only colour e, so the
+// in-place update and the pushes are race-free across workgroups.
+#include "omg_device.h"
+#include "omg_kernels.h"
+
+namespace omg {
+
+__device__ __forceinline__ int xcd_box(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7, pos = bid >> 3;
+  return x * q + min(x, r) + pos;
+}
+
+// physical ghost (set_ghost_cells + bc_to_gc, m_ghost_cells.f90:264-283, 682-766)
+__device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc, int b, long long f, int nb,
+                                             int arg, int a, int c, int gi, double x1v, double x2v) {
+  double bv;
+  int type;
+  if (bc.phi_stored) {
+    bv = L.data[L.vstride + (long long)b * L.stride + gi];
+    type = arg;
+  } else if (bc.face_off && bc.face_off[f] >= 0) {
+    bv = bc.face_data[bc.face_off[f] + (a - 1) + (long long)L.nc * (c - 1)];
+    type = bc.face_type[f];
+  } else {
+    bv = bc.value[nb - 1];
+    type = bc.type[nb - 1];
+  }
+  double c0, c1, c2;
+  if (type == -10) {
+    c0 = 2; c1 = -1; c2 = 0;
+  } else if (type == -11) {
+    c0 = L.dr[(nb - 1) >> 1] * ((nb & 1) ? -1.0 : 1.0); c1 = 1; c2 = 0;
+  } else {
+    c0 = 0; c1 = 2; c2 = -1;
+  }
+  return c0 * bv + c1 * x1v + c2 * x2v;
+}
+
+template <int NC, int OP>
+__global__ void __launch_bounds__(256) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
+                                                   double* __restrict__ sendbuf) {
+  constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
+  constexpr int NP2 = (HV / 2 + 255) / 256;    // double2 cell pairs per thread
+  __shared__ double so[HV];                    // colour 1-e of the interior
+  __shared__ double se[HV];                    // colour e, updated
+  __shared__ double sg[6 * FH];                // colour 1-e halves of the ghost faces
+  const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x, o = 1 - e;
+  const long long boff = (long long)b * L.stride;
+  double* __restrict__ u = L.phi + boff;
+  const double* __restrict__ f = L.data + L.vstride + boff;
+  const OpCoef<OP> K(L, lambda);
+
+  // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
+  {
+    const double2* src = reinterpret_cast<const double2*>(u + o * HV);
+    double2* dst = reinterpret_cast<double2*>(so);
+    for (int q = tid; q < HV / 2; q += 256) dst[q] = src[q];
+    for (int q = tid; q < 3 * FH; q += 256) {   // 6 faces x FH/2 double2
+      const int nb = q / (FH / 2), r = q % (FH / 2);
+      reinterpret_cast<double2*>(sg + nb * FH)[r] =
+          reinterpret_cast<const double2*>(u + 2 * HV + nb * FS + o * FH)[r];
+    }
+  }
+  double2 fr[NP2];
+#pragma unroll
+  for (int r = 0; r < NP2; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 < HV / 2) fr[r] = reinterpret_cast<const double2*>(f + e * HV)[q2];
+  }
+  __syncthreads();
+
+  // ---- colour e update ----------------------------------------------------
+#pragma unroll
+  for (int r = 0; r < NP2; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 >= HV / 2) continue;
+    double nv[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int q = 2 * q2 + s;
+      const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+      const int i = 2 * ih + 1 + ((1 + j + k + e) & 1);
+      const int tj = (i - 1) >> 1;                      // colour-1-e index of (i, j, k)
+      Nbr7 st;
+      st.xm = i > 1 ? so[((i - 2) >> 1) + H * row] : sg[0 * FH + ((j - 1) >> 1) + H * (k - 1)];
+      st.xp = i < NC ? so[(i >> 1) + H * row] : sg[1 * FH + ((j - 1) >> 1) + H * (k - 1)];
+      st.ym = j > 1 ? so[tj + H * (row - 1)] : sg[2 * FH + tj + H * (k - 1)];
+      st.yp = j < NC ? so[tj + H * (row + 1)] : sg[3 * FH + tj + H * (k - 1)];
+      st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
+      st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
+      const double fv = s ? fr[r].y : fr[r].x;
+      nv[s] = gs_value<OP>(K, st, fv);
+      se[q] = nv[s];
+    }
+    reinterpret_cast<double2*>(u + e * HV)[q2] = make_double2(nv[0], nv[1]);
+  }
+  __syncthreads();
+
+  // ---- ghost fill after the substep ---------------------------------------
+  for (int p = tid; p < 6 * NC * NC; p += 256) {
+    const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
+    const int a = cell % NC + 1, c = cell / NC + 1;
+    const long long fidx = (long long)b * 6 + nb - 1;
+    const int kind = L.nbk[fidx], arg = L.nba[fidx];
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1;
+    // boundary cell x1 (and x2) of this face: colour and index
+    const int x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
+    int i1, j1, k1;
+    if (d == 1) { i1 = x1; j1 = a; k1 = c; }
+    else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
+    else { i1 = a; j1 = c; k1 = x1; }
+    const int c1 = (i1 + j1 + k1) & 1;
+    const int idx1 = ((i1 - 1) >> 1) + H * ((j1 - 1) + NC * (k1 - 1));
+    const double v1 = c1 == e ? se[idx1] : so[idx1];
+    if (kind == NB_LOCAL) {
+      if ((colours >> c1) & 1)
+        L.phi[(long long)arg * L.stride + off_gh(L, low ? nb + 1 : nb - 1, a, c)] = v1;
+    } else if (kind == NB_REMOTE) {
+      sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
+    } else {  // NB_PHYS (refinement boundaries take the generic kernel)
+      const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
+      const int idx2 = ((i2 - 1) >> 1) + H * ((j2 - 1) + NC * (k2 - 1));
+      const double v2 = c1 == e ? so[idx2] : se[idx2];   // x2 has the other colour
+      const int gi = off_gh(L, nb, a, c);
+      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, v2);
+    }
+  }
+}
+
+void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
+                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, hipStream_t st) {
+  if (L.n == 0) return;
+  const bool tiled = !has_rb && (op == OP_LPL || op == OP_HELM) &&
+                     (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2);
+  if (!tiled) {
+    launch_gs_sub(L, op, lambda, e, colours, C, rb, bc, sendbuf, st);
+    return;
+  }
+  GcBC b2 = bc;
+  b2.phi_stored = bc.phi_stored;  // iv == 1 here
+  const dim3 g(L.n), blk(256);
+#define OMG_TILE(NC)                                                                          \
+  if (op == OP_HELM)                                                                          \
+    k_gsrb_tile<NC, OP_HELM><<<g, blk, 0, st>>>(L, lambda, e, colours, b2, sendbuf);          \
+  else                                                                                        \
+    k_gsrb_tile<NC, OP_LPL><<<g, blk, 0, st>>>(L, lambda, e, colours, b2, sendbuf);
+  switch (L.nc) {
+    case 16: OMG_TILE(16) break;
+    case 8: OMG_TILE(8) break;
+    case 4: OMG_TILE(4) break;
+    default: OMG_TILE(2) break;
+  }
+#undef OMG_TILE
+}
+
+}  // namespace omg

@@ -37,13 +37,25 @@ def _random_fill(be, rng, ivs=(1, 2, 5)):
             be.set_level(lvl, iv, rng.standard_normal((len(ids), nc + 2, nc + 2, nc + 2)))
 
 
+def _stored_mask(nc):
+    """Interior + face ghosts of a (nc+2)^3 box: the cells any operator of the
+    reference reads.  Edge/corner ghosts are dead data (never read, never
+    written by a fill) and the device layout does not store them."""
+    s = nc + 2
+    ix = np.arange(s)
+    bnd = ((ix == 0) | (ix == s - 1)).astype(int)
+    nb = bnd[:, None, None] + bnd[None, :, None] + bnd[None, None, :]
+    return nb < 2
+
+
 def _assert_same(dev, orc, ivs=(1, 2, 3, 4, 5)):
     for lvl in dev.levels():
         if not len(dev.my_ids(lvl)):
             continue
+        m = _stored_mask(dev.tree.box_size_lvl[lvl])
         for iv in ivs:
             a, b = dev.get_level(lvl, iv), orc.get_level(lvl, iv)
-            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (lvl, iv)
+            assert np.array_equal(a[:, m].view(np.uint64), b[:, m].view(np.uint64)), (lvl, iv)
 
 
 OPS_CASES = [
@@ -83,3 +95,18 @@ def test_per_operation_bitwise(args):
     assert c.scalar("get_sum", 1) == orc.o.get_sum(1)
     c.call("subtract_mean", 1, 1); orc.o.subtract_mean(1, 1)
     _assert_same(dev, orc)
+
+
+@pytest.mark.parametrize("args", [OPS_CASES[0], OPS_CASES[1], "16 64 64 64 1 v gsrb helm 2 d0 sol 1 lb 0"])
+def test_smoother_with_stale_ghosts(args):
+    """smooth_boxes right after phi was overwritten (ghosts not refilled): the
+    reference reads the stale ghosts in the first substep; so must we."""
+    cfg = parse(args)
+    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+    for be in (dev, orc):
+        _random_fill(be, np.random.default_rng(11))
+    hi = dev.tree.highest_lvl
+    for n_cycle in (1, 2, 3):
+        dev.mg.ctx.call("smooth_boxes", hi, n_cycle)
+        orc.o.smooth_boxes(hi, n_cycle)
+        _assert_same(dev, orc)
