@@ -174,12 +174,15 @@ void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recv
 
 // ---------------------------------------------------------------------------
 // profiling: HIP events around kernel families on the context stream
+constexpr int NO_LVL = -1 << 30;
+
 struct Prof {
   omg_ctx* c;
   const char* name;
   double cells;
+  int lvl;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  Prof(omg_ctx* c_, const char* n, double cl) : c(c_), name(n), cells(cl) {
+  Prof(omg_ctx* c_, const char* n, double cl, int l = NO_LVL) : c(c_), name(n), cells(cl), lvl(l) {
     if (!c->profiling) return;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -188,7 +191,7 @@ struct Prof {
   ~Prof() {
     if (!e0) return;
     (void)hipEventRecord(e1, c->stream);
-    c->pending.push_back({name, e0, e1, cells});
+    c->pending.push_back({name, e0, e1, cells, lvl});
   }
 };
 
@@ -198,10 +201,12 @@ void resolve_stats(omg_ctx* c) {
   for (auto& p : c->pending) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p.e0, p.e1));
-    auto& s = c->stats[p.name];
-    s.launches++;
-    s.ms += ms;
-    s.cells += p.cells;
+    for (int pass = 0; pass < (p.lvl == NO_LVL ? 1 : 2); pass++) {
+      auto& s = c->stats[pass ? std::string(p.name) + "@" + std::to_string(p.lvl) : std::string(p.name)];
+      s.launches++;
+      s.ms += ms;
+      s.cells += p.cells;
+    }
     (void)hipEventDestroy(p.e0);
     (void)hipEventDestroy(p.e1);
   }
@@ -251,7 +256,7 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (!L) return;
   if (iv == 1) L->phi_gc_ok = true;
   if (L->n) {
-    Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc);
+    Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc, lvl);
     launch_fill_gc(L->view(), iv, 3, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_sendbuf,
                    c->stream);
   }
@@ -266,7 +271,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
   if (c->smoother != OMG_SMOOTHER_GSRB) {
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
-        Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc);
+        Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
         launch_gs_lex(L->view(), c->op, c->lambda, c->stream);
       }
       fill_gc_lvl(c, lvl, 1);
@@ -283,7 +288,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
     const int e = n & 1;
     const bool odd = L->nc & 1;
     if (L->n) {
-      Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc);
+      Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc, lvl);
       launch_gs_substep(L->view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
                         L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, c->stream);
     }
@@ -292,11 +297,18 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
   }
 }
 
+bool tiled_level(omg_ctx* c, const Level* L) {
+  return L && tiled_nc(L->nc) && (c->op == OP_LPL || c->op == OP_HELM);
+}
+
 void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
   Level* L = level_ptr(c, lvl);
   if (!L || L->n == 0) return;
-  Prof p(c, "residual", (double)L->n * L->nc * L->nc * L->nc);
-  launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
+  Prof p(c, "residual", (double)L->n * L->nc * L->nc * L->nc, lvl);
+  if (tiled_level(c, L))
+    launch_resid_restrict(L->view(), empty_view(), c->op, c->lambda, maxbits, 0, nullptr, nullptr, c->stream);
+  else
+    launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
 // max_residual_lvl (m_multigrid.f90:296-311), this rank only
@@ -309,22 +321,30 @@ double max_residual_lvl(omg_ctx* c, int lvl) {
   return c->h_scalar[0];
 }
 
+// the remote part of mg_restrict_lvl: children whose parent lives on another
+// rank are restricted into a buffer, exchanged and unpacked (m_restrict.f90:
+// 94-108, 196-211)
+void restrict_remote(omg_ctx* c, int iv, int lvl) {
+  Level* F = level_ptr(c, lvl);
+  Level* C = level_ptr(c, lvl - 1);
+  if (c->n_ranks > 1 && F && C && (F->restr.n_send || F->restr.n_recv)) {
+    launch_restrict_pack(F->view(), iv, F->restr.d_send_items, F->restr.n_send, F->d_sendbuf, c->stream);
+    exchange(c, F->restr, F->d_sendbuf, C->d_recvbuf);
+    launch_restrict_unpack(C->view(), iv, F->restr.d_recv_items, F->restr.n_recv, F->nc / 2, C->d_recvbuf,
+                           c->stream);
+  }
+}
+
 // mg_restrict_lvl (m_restrict.f90:83-114)
 void restrict_lvl(omg_ctx* c, int iv, int lvl) {
   if (lvl <= c->lowest) throw OmgError("cannot restrict lvl <= lowest_lvl");
   if (iv == 1) phi_dirty(c, lvl - 1);
   Level* F = level_ptr(c, lvl);
-  Level* C = level_ptr(c, lvl - 1);
-  const LevelView FV = view_of(c, lvl), CV = view_of(c, lvl - 1);
-  if (c->n_ranks > 1 && F && C && (F->restr.n_send || F->restr.n_recv)) {
-    launch_restrict_pack(FV, iv, F->restr.d_send_items, F->restr.n_send, F->d_sendbuf, c->stream);
-    exchange(c, F->restr, F->d_sendbuf, C->d_recvbuf);
-    launch_restrict_unpack(CV, iv, F->restr.d_recv_items, F->restr.n_recv, F->nc / 2, C->d_recvbuf,
-                           c->stream);
-  }
+  restrict_remote(c, iv, lvl);
   if (F && F->n_pairs) {
-    Prof p(c, "restrict", (double)F->n_pairs * F->nc * F->nc * F->nc);
-    launch_restrict(FV, CV, iv, F->d_pairs, F->n_pairs, F->d_parent_local, F->d_dix, c->stream);
+    Prof p(c, "restrict", (double)F->n_pairs * F->nc * F->nc * F->nc, lvl);
+    launch_restrict(F->view(), view_of(c, lvl - 1), iv, F->d_pairs, F->n_pairs, F->d_parent_local, F->d_dix,
+                    c->stream);
   }
 }
 
@@ -343,7 +363,7 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
                           c->stream);
   }
   if (F && F->n_pairs) {
-    Prof p(c, "prolong", (double)F->n_pairs * F->nc * F->nc * F->nc);
+    Prof p(c, "prolong", (double)F->n_pairs * F->nc * F->nc * F->nc, lvl + 1);
     launch_prolong(CV, FV, iv, iv_to, add, F->d_pairs, F->n_pairs, F->d_parent_local, F->d_dix,
                    c->stream);
   }
@@ -351,13 +371,26 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
 
 // update_coarse (m_multigrid.f90:347-384)
 void update_coarse(omg_ctx* c, int lvl) {
-  residual_lvl(c, lvl, nullptr);
-  restrict_lvl(c, 1, lvl);
-  restrict_lvl(c, 4, lvl);
+  Level* F = level_ptr(c, lvl);
+  if (F && F->n && tiled_level(c, F)) {
+    // residual + restriction of phi and res in one pass (omg_tiles.hip)
+    phi_dirty(c, lvl - 1);
+    {
+      Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
+      launch_resid_restrict(F->view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+                            F->d_dix, c->stream);
+    }
+    restrict_remote(c, 1, lvl);
+    restrict_remote(c, 4, lvl);
+  } else {
+    residual_lvl(c, lvl, nullptr);
+    restrict_lvl(c, 1, lvl);
+    restrict_lvl(c, 4, lvl);
+  }
   fill_gc_lvl(c, lvl - 1, 1);
   Level* C = level_ptr(c, lvl - 1);
   if (C && !C->parents.empty()) {
-    Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc);
+    Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl - 1);
     launch_coarse_rhs(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream);
   }
 }
@@ -368,6 +401,29 @@ void correct_children(omg_ctx* c, int lvl) {
   if (C && !C->parents.empty())
     launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
   prolong(c, lvl, 4, 1, 1);
+}
+
+// correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
+// V-cycle and FMG run them (m_multigrid.f90:127-136, 216-219); fused when every
+// box of lvl+1 has its parent on this GPU and no refinement boundary.
+void correct_and_fill(omg_ctx* c, int lvl) {
+  Level* F = level_ptr(c, lvl + 1);
+  Level* C = level_ptr(c, lvl);
+  if (F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
+      !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv))) {
+    if (!C->parents.empty())
+      launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
+    {
+      Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
+      launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
+                          F->d_sendbuf, c->stream);
+    }
+    finish_halo(c, F, 1);
+    F->phi_gc_ok = true;
+    return;
+  }
+  correct_children(c, lvl);
+  fill_gc_lvl(c, lvl + 1, 1);
 }
 
 // MPI_Allreduce of one double: max exactly; sum in the recursive-doubling
@@ -395,8 +451,11 @@ double get_sum(omg_ctx* c, int iv) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     const double w = L->dr[0] * L->dr[1] * L->dr[2];
-    launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
-    launch_seq_sum(L->d_scratch, (int)L->leaves.size(), w, acc, c->stream);
+    if (L->nc % 4 == 0)
+      launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
+    else
+      launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
+    launch_seq_sum2(L->d_scratch, (int)L->leaves.size(), w, acc, c->stream);
   }
   HIPCHK(hipMemcpyAsync(c->h_scalar + 2, acc, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -406,7 +465,11 @@ double get_sum(omg_ctx* c, int iv) {
 // subtract_mean (m_multigrid.f90:245-276)
 void subtract_mean(omg_ctx* c, int iv, int ghosts) {
   const int nc = c->box_size;
-  if (iv == 1) phi_dirty_all(c);
+  // subtracting from interior and ghosts keeps same-GPU / remote face ghosts
+  // equal to a fill; physical and refinement-boundary ghosts are not.
+  if (iv == 1)
+    for (auto& kv : c->levels)
+      if (!ghosts || kv.second.has_phys || kv.second.has_rb) kv.second.phi_gc_ok = false;
   double mean = get_sum(c, iv);
   const auto& d1 = c->drl[1];
   const double volume = (double)(nc * nc * nc) * (d1[0] * d1[1] * d1[2]) * (double)c->ids[1].size();
@@ -424,7 +487,11 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   const bool has_highest = highest_lvl >= c->lowest;
   if (c->subtract_mean && !has_highest) subtract_mean(c, 2, 0);
   const int min_lvl = c->lowest, max_lvl = has_highest ? highest_lvl : c->highest;
-  if (standalone) fill_gc_lvl(c, max_lvl, 1);
+  if (standalone) {
+    // the fill is idempotent: skip it when the ghosts already equal its result
+    Level* L = level_ptr(c, max_lvl);
+    if (!(L && L->phi_gc_ok && !L->has_rb && !L->has_remote)) fill_gc_lvl(c, max_lvl, 1);
+  }
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     smooth_boxes(c, l, c->n_cycle_down);
     update_coarse(c, l);
@@ -443,8 +510,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
   }
   for (int l = min_lvl + 1; l <= max_lvl; l++) {
-    correct_children(c, l - 1);
-    fill_gc_lvl(c, l, 1);
+    correct_and_fill(c, l - 1);
     smooth_boxes(c, l, c->n_cycle_up);
   }
   double max_res = 0.0;
@@ -472,10 +538,7 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
   for (int l = c->lowest; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (L && L->n) launch_copy_var(L->view(), 1, 3, c->stream);
-    if (l > c->lowest) {
-      correct_children(c, l - 1);
-      fill_gc_lvl(c, l, 1);
-    }
+    if (l > c->lowest) correct_and_fill(c, l - 1);
     if (l == c->highest)
       max_res = fas_vcycle(c, l, want_max_res, false);
     else
@@ -591,6 +654,7 @@ void build_plan(omg_ctx* c) {
     finalize_transfer(L.halo);
     L.has_rb = !L.h_rb.empty();
     L.has_remote = L.halo.n_send || L.halo.n_recv;
+    L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
     L.d_phi = L.d_data;
     L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);

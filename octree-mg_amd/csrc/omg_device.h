@@ -78,6 +78,36 @@ __device__ __forceinline__ bool cell_of(const LevelView& L, int q, int& i, int& 
   return true;
 }
 
+// The same layout with a compile-time (even) box size, for LDS-tiled kernels
+// that stage a whole stored box.
+template <int NC>
+struct Tl {
+  static constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH, NST = 2 * HV + 6 * FS;
+  __device__ static __forceinline__ int oint(int i, int j, int k) {
+    return ((i + j + k) & 1) * HV + ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
+  }
+  __device__ static __forceinline__ int ogh(int nb, int a, int c) {
+    const int g = (nb & 1) ? 0 : NC + 1;
+    return 2 * HV + (nb - 1) * FS + ((g + a + c) & 1) * FH + ((a - 1) >> 1) + H * (c - 1);
+  }
+  __device__ static __forceinline__ int ocell(int i, int j, int k) {
+    if (i == 0) return ogh(1, j, k);
+    if (i == NC + 1) return ogh(2, j, k);
+    if (j == 0) return ogh(3, i, k);
+    if (j == NC + 1) return ogh(4, i, k);
+    if (k == 0) return ogh(5, i, j);
+    if (k == NC + 1) return ogh(6, i, j);
+    return oint(i, j, k);
+  }
+  // interior slot q (< 2*HV) -> (i, j, k)
+  __device__ static __forceinline__ void decode(int q, int& i, int& j, int& k) {
+    const int e = q >= HV, r = q - e * HV, ih = r % H, row = r / H;
+    j = row % NC + 1;
+    k = row / NC + 1;
+    i = 2 * ih + 1 + ((1 + j + k + e) & 1);
+  }
+};
+
 __device__ __forceinline__ void atomic_max_nonneg(unsigned long long* p, double v) {
   // |res| >= 0: IEEE bit patterns of non-negative doubles order like uint64
   atomicMax(p, (unsigned long long)__double_as_longlong(v));

@@ -86,7 +86,7 @@ struct Level {
   double* d_data = nullptr;
   double* d_phi = nullptr;              // phi (d_data's var 1)
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
-  bool has_rb = false, has_remote = false;
+  bool has_rb = false, has_remote = false, has_phys = false;
   int8_t* d_nbk = nullptr;
   int* d_nba = nullptr;
   int* d_sendpos = nullptr;
@@ -146,6 +146,7 @@ struct PendingEv {
   const char* name;
   hipEvent_t e0, e1;
   double cells;
+  int lvl;   // level of the launch (stats are kept per name and per name@lvl)
 };
 
 struct KStat {

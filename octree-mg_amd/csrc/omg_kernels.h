@@ -52,4 +52,14 @@ void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t 
 void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st);
 void launch_phi_bc_store(const LevelView& L, const GcBC& bc, int* nba, hipStream_t st);
 
+// LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16
+bool tiled_nc(int nc);
+void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
+                           unsigned long long* maxbits, int restrict_on, const int* parent_local,
+                           const int* dixp, hipStream_t st);
+void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
+                         const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st);
+void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
+void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st);
+
 }  // namespace omg

@@ -19,40 +19,10 @@
 // Colour e reads only colour 1-e and neighbours receive only colour e, so the
 // in-place update and the pushes are race-free across workgroups.
 #include "omg_device.h"
+#include "omg_face.h"
 #include "omg_kernels.h"
 
 namespace omg {
-
-__device__ __forceinline__ int xcd_box(int bid, int nb) {
-  const int q = nb >> 3, r = nb & 7, x = bid & 7, pos = bid >> 3;
-  return x * q + min(x, r) + pos;
-}
-
-// physical ghost (set_ghost_cells + bc_to_gc, m_ghost_cells.f90:264-283, 682-766)
-__device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc, int b, long long f, int nb,
-                                             int arg, int a, int c, int gi, double x1v, double x2v) {
-  double bv;
-  int type;
-  if (bc.phi_stored) {
-    bv = L.data[L.vstride + (long long)b * L.stride + gi];
-    type = arg;
-  } else if (bc.face_off && bc.face_off[f] >= 0) {
-    bv = bc.face_data[bc.face_off[f] + (a - 1) + (long long)L.nc * (c - 1)];
-    type = bc.face_type[f];
-  } else {
-    bv = bc.value[nb - 1];
-    type = bc.type[nb - 1];
-  }
-  double c0, c1, c2;
-  if (type == -10) {
-    c0 = 2; c1 = -1; c2 = 0;
-  } else if (type == -11) {
-    c0 = L.dr[(nb - 1) >> 1] * ((nb & 1) ? -1.0 : 1.0); c1 = 1; c2 = 0;
-  } else {
-    c0 = 0; c1 = 2; c2 = -1;
-  }
-  return c0 * bv + c1 * x1v + c2 * x2v;
-}
 
 template <int NC, int OP>
 __global__ void __launch_bounds__(256) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,

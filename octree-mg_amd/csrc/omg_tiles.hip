@@ -1,0 +1,250 @@
+// omg_tiles.hip — LDS-tiled fused level kernels around the smoother.
+//
+//  k_resid_restrict: update_coarse's fine-level part (src/m_multigrid.f90:
+//    356-363): residual_box over every box of the level, then mg_restrict_lvl
+//    of phi and of the residual onto the parents, in one pass over phi.
+//  k_prolong_fill:   correct_children's fine-level part + the ghost fill the
+//    V-cycle runs right after it (:216-219): phi += prolong(res_coarse)
+//    (mg_prolong_sparse, m_prolong.f90:159-240), then the new boundary values
+//    go to the neighbours' ghost faces (both colours) and physical ghosts are
+//    recomputed.  Nothing reads fine ghosts during the launch: race-free.
+//  k_box_sums2 / k_seq_sum2: get_sum (:278-294) in the reference's exact
+//    sequential order, with wide loads and the products off the add chain.
+#include "omg_face.h"
+#include "omg_kernels.h"
+
+namespace omg {
+
+template <int NC, int OP>
+__global__ void __launch_bounds__(256) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
+                                                        unsigned long long* maxbits, int restrict_on,
+                                                        const int* parent_local, const int* dixp) {
+  using TL = Tl<NC>;
+  constexpr int NST = TL::NST, HV = TL::HV, NR = (HV + 255) / 256, HN = NC / 2;
+  __shared__ double sb[NST];
+  const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
+  const long long boff = (long long)b * F.stride;
+  const double* __restrict__ u = F.phi + boff;
+  const double* __restrict__ f = F.data + F.vstride + boff;
+  double* __restrict__ res = F.data + 3 * F.vstride + boff;
+  for (int q = tid; q < NST / 2; q += 256)
+    reinterpret_cast<double2*>(sb)[q] = reinterpret_cast<const double2*>(u)[q];
+  double2 fr[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 < HV) fr[r] = reinterpret_cast<const double2*>(f)[q2];
+  }
+  __syncthreads();
+
+  // residual_box (m_multigrid.f90:426-436) with box_lpl / box_helmh
+  const OpCoef<OP> K(F, lambda);
+  double mx = 0.0;
+  double2 rv[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 >= HV) continue;
+    double out[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int q = 2 * q2 + s;
+      int i, j, k;
+      TL::decode(q, i, j, k);
+      Nbr7 st;
+      st.c = sb[q];
+      st.xm = sb[TL::ocell(i - 1, j, k)];
+      st.xp = sb[TL::ocell(i + 1, j, k)];
+      st.ym = sb[TL::ocell(i, j - 1, k)];
+      st.yp = sb[TL::ocell(i, j + 1, k)];
+      st.zm = sb[TL::ocell(i, j, k - 1)];
+      st.zp = sb[TL::ocell(i, j, k + 1)];
+      out[s] = (s ? fr[r].y : fr[r].x) - op_value<OP>(K, st);
+      mx = fmax(mx, fabs(out[s]));
+    }
+    rv[r] = make_double2(out[0], out[1]);
+    reinterpret_cast<double2*>(res)[q2] = rv[r];
+  }
+  if (maxbits) {
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+    if ((tid & 63) == 0) atomic_max_nonneg(maxbits, mx);
+  }
+  if (!restrict_on || parent_local[b] < 0) return;
+
+  // restrict_onto (m_restrict.f90:165-214): phi, then res, onto the parent's
+  // octant at offset dix (sequential column-major 8-cell sum from +0.0)
+  const int pb = parent_local[b], dp = dixp[b];
+  const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
+  const long long poff = (long long)pb * Cv.stride;
+  for (int pass = 0; pass < 2; pass++) {
+    double* __restrict__ dst = pass == 0 ? Cv.phi + poff : Cv.data + 3 * Cv.vstride + poff;
+    for (int q = tid; q < HN * HN * HN; q += 256) {
+      const int i = q % HN + 1, j = (q / HN) % HN + 1, k = q / (HN * HN) + 1;
+      double acc = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int jj = 0; jj < 2; jj++)
+#pragma unroll
+          for (int ii = 0; ii < 2; ii++) acc += sb[TL::oint(2 * i - 1 + ii, 2 * j - 1 + jj, 2 * k - 1 + kk)];
+      dst[off_int(Cv, dx + i, dy + j, dz + k)] = 0.125 * acc;
+    }
+    if (pass == 0) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < NR; r++) {
+        const int q2 = tid + 256 * r;
+        if (q2 < HV) reinterpret_cast<double2*>(sb)[q2] = rv[r];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) k_prolong_fill(LevelView Cv, LevelView F, int iv,
+                                                      const int* parent_local, const int* dixp, GcBC bc,
+                                                      double* sendbuf) {
+  using TL = Tl<NC>;
+  constexpr int HV = TL::HV, NR = (HV + 255) / 256, HN = NC / 2, CB = HN + 2;
+  __shared__ double cb[CB * CB * CB];   // the parent's octant + one face layer around it
+  __shared__ double sb[2 * HV];         // the corrected fine interior
+  const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
+  const int pb = parent_local[b], dp = dixp[b];
+  const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
+  const double* __restrict__ cu = boxp(Cv, iv, pb);
+  for (int q = tid; q < CB * CB * CB; q += 256) {
+    const int p = q % CB, s = (q / CB) % CB, t = q / (CB * CB);
+    const int nbnd = (p == 0 || p == CB - 1) + (s == 0 || s == CB - 1) + (t == 0 || t == CB - 1);
+    if (nbnd < 2) cb[q] = cu[off_cell(Cv, dx + p, dy + s, dz + t)];
+  }
+  double* __restrict__ u = F.phi + (long long)b * F.stride;
+  double2 old[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 < HV) old[r] = reinterpret_cast<const double2*>(u)[q2];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + 256 * r;
+    if (q2 >= HV) continue;
+    double nv[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int q = 2 * q2 + s;
+      int i, j, k;
+      TL::decode(q, i, j, k);
+      const int ic = (i + 1) >> 1, jc = (j + 1) >> 1, kc = (k + 1) >> 1;   // 1..HN inside the octant
+      const int c0 = ic + CB * (jc + CB * kc);
+      const double f0 = 0.25 * cb[c0];
+      const double fx = 0.25 * cb[(i & 1) ? c0 - 1 : c0 + 1];
+      const double fy = 0.25 * cb[(j & 1) ? c0 - CB : c0 + CB];
+      const double fz = 0.25 * cb[(k & 1) ? c0 - CB * CB : c0 + CB * CB];
+      const double o = s ? old[r].y : old[r].x;
+      nv[s] = o + (f0 + fx + fy + fz);
+      sb[q] = nv[s];
+    }
+    reinterpret_cast<double2*>(u)[q2] = make_double2(nv[0], nv[1]);
+  }
+  __syncthreads();
+  tile_face_fill<NC>(F, b, sb, 3, bc, sendbuf);
+}
+
+// get_sum's per-leaf interior sums, sequential column-major as the reference
+// (amdflang -O2 emits one accumulator from +0.0), 16-B loads per row.
+__global__ void __launch_bounds__(64) k_box_sums2(LevelView L, int iv, const int* leaves, int n_leaves,
+                                                  double* out) {
+  const int nc = L.nc, h = L.h;
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= n_leaves) return;
+  const double* u = boxp(L, iv, leaves[q]);
+  double acc = 0.0;
+  for (int k = 1; k <= nc; k++) {
+#pragma unroll 2
+    for (int j = 1; j <= nc; j++) {
+      const int r0 = h * ((j - 1) + nc * (k - 1));
+      const double2* A = reinterpret_cast<const double2*>(u + ((1 + j + k) & 1) * L.hv + r0);  // odd i
+      const double2* B = reinterpret_cast<const double2*>(u + ((j + k) & 1) * L.hv + r0);      // even i
+      for (int m = 0; m < h / 2; m++) {
+        const double2 a = A[m], bb = B[m];
+        acc += a.x;
+        acc += bb.x;
+        acc += a.y;
+        acc += bb.y;
+      }
+    }
+  }
+  out[q] = acc;
+}
+
+// acc = acc + w*s_q in order (get_sum's loop); the products are formed off
+// the dependent add chain.
+__global__ void __launch_bounds__(256) k_seq_sum2(const double* box_sums, int n, double w, double* acc) {
+  __shared__ double stage[2048];
+  double a = *acc;
+  for (int base = 0; base < n; base += 2048) {
+    const int m = min(2048, n - base);
+    for (int q = threadIdx.x; q < m; q += blockDim.x) stage[q] = w * box_sums[base + q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int q = 0;
+      for (; q + 8 <= m; q += 8) {
+        const double t0 = stage[q], t1 = stage[q + 1], t2 = stage[q + 2], t3 = stage[q + 3];
+        const double t4 = stage[q + 4], t5 = stage[q + 5], t6 = stage[q + 6], t7 = stage[q + 7];
+        a = a + t0; a = a + t1; a = a + t2; a = a + t3;
+        a = a + t4; a = a + t5; a = a + t6; a = a + t7;
+      }
+      for (; q < m; q++) a = a + stage[q];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *acc = a;
+}
+
+bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }
+
+void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
+                           unsigned long long* maxbits, int restrict_on, const int* parent_local,
+                           const int* dixp, hipStream_t st) {
+  if (F.n == 0) return;
+  const dim3 g(F.n), blk(256);
+#define OMG_RR(NC)                                                                                     \
+  if (op == OP_HELM)                                                                                   \
+    k_resid_restrict<NC, OP_HELM><<<g, blk, 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, \
+                                                      dixp);                                           \
+  else                                                                                                 \
+    k_resid_restrict<NC, OP_LPL><<<g, blk, 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, dixp);
+  switch (F.nc) {
+    case 16: OMG_RR(16) break;
+    case 8: OMG_RR(8) break;
+    case 4: OMG_RR(4) break;
+    default: OMG_RR(2) break;
+  }
+#undef OMG_RR
+}
+
+void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
+                         const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st) {
+  if (F.n == 0) return;
+  const dim3 g(F.n), blk(256);
+  switch (F.nc) {
+    case 16: k_prolong_fill<16><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 8: k_prolong_fill<8><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 4: k_prolong_fill<4><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    default: k_prolong_fill<2><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+  }
+}
+
+void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
+  if (n == 0) return;
+  k_box_sums2<<<(n + 63) / 64, 64, 0, st>>>(L, iv, leaves, n, out);
+}
+
+void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
+  if (n == 0) return;
+  k_seq_sum2<<<1, 256, 0, st>>>(box_sums, n, w, acc);
+}
+
+}  // namespace omg
