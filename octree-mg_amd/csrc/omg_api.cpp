@@ -174,7 +174,7 @@ void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recv
 
 // ---------------------------------------------------------------------------
 // profiling: HIP events around kernel families on the context stream
-constexpr int NO_LVL = -1 << 30;
+constexpr int NO_LVL = INT_MIN;
 
 struct Prof {
   omg_ctx* c;
@@ -451,10 +451,11 @@ double get_sum(omg_ctx* c, int iv) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     const double w = L->dr[0] * L->dr[1] * L->dr[2];
-    if (L->nc % 4 == 0)
+    {
+      Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
       launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
-    else
-      launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
+    }
+    Prof p(c, "seq_sum", (double)L->leaves.size(), l);
     launch_seq_sum2(L->d_scratch, (int)L->leaves.size(), w, acc, c->stream);
   }
   HIPCHK(hipMemcpyAsync(c->h_scalar + 2, acc, 8, hipMemcpyDeviceToHost, c->stream));

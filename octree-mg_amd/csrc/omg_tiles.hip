@@ -8,7 +8,7 @@
 //    (mg_prolong_sparse, m_prolong.f90:159-240), then the new boundary values
 //    go to the neighbours' ghost faces (both colours) and physical ghosts are
 //    recomputed.  Nothing reads fine ghosts during the launch: race-free.
-//  k_box_sums2 / k_seq_sum2: get_sum (:278-294) in the reference's exact
+//  k_box_sums3 / k_seq_sum3: get_sum (:278-294) in the reference's exact
 //    sequential order, with wide loads and the products off the add chain.
 #include "omg_face.h"
 #include "omg_kernels.h"
@@ -152,55 +152,130 @@ __global__ void __launch_bounds__(256) k_prolong_fill(LevelView Cv, LevelView F,
   tile_face_fill<NC>(F, b, sb, 3, bc, sendbuf);
 }
 
-// get_sum's per-leaf interior sums, sequential column-major as the reference
-// (amdflang -O2 emits one accumulator from +0.0), 16-B loads per row.
-__global__ void __launch_bounds__(64) k_box_sums2(LevelView L, int iv, const int* leaves, int n_leaves,
-                                                  double* out) {
-  const int nc = L.nc, h = L.h;
+// get_sum's per-leaf interior sums (m_multigrid.f90:286-290): one lane per
+// leaf, each summing its box sequentially in column-major order from +0.0
+// (amdflang -O2 emits a single accumulator).  A wave owns 32 leaves and
+// streams them through LDS in chunks of R rows: the loads are whole 256-B
+// colour segments shared by 64 lanes (coalesced), the next chunk is in flight
+// while the lanes run their add chains out of LDS.
+template <int NC>
+__global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
+                                                  int n_leaves, double* __restrict__ out) {
+  constexpr int H = NC / 2, R = 4, SEG = R * H;   // doubles of one colour in a chunk
+  constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
+  constexpr int PER = 32 * CH2 / 64;              // double2 per lane per chunk
+  constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
+  constexpr int NCH = NC * NC / R;
+  __shared__ double lds[32 * P];
+  const int lane = threadIdx.x, b0 = blockIdx.x * 32;
+  const long long hv = L.hv;
+  const double* src[PER];
+  int dst[PER];
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const int t = lane + 64 * r, bb = t / CH2, w = t % CH2, seg = w / (SEG / 2), off = w % (SEG / 2);
+    const int q = min(b0 + bb, n_leaves - 1);
+    src[r] = boxp(L, iv, leaves[q]) + seg * hv + 2 * off;
+    dst[r] = bb * P + seg * SEG + 2 * off;
+  }
+  double2 v[PER];
+#pragma unroll
+  for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r]);
+  double acc = 0.0;
+  const double* my = lds + lane * P;
+  for (int c = 0; c < NCH; c++) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+      lds[dst[r]] = v[r].x;
+      lds[dst[r] + 1] = v[r].y;
+    }
+    __syncthreads();
+    const int k = c / (NC / R) + 1, j0 = (c % (NC / R)) * R + 1;
+    if (c + 1 < NCH) {
+      const int k1 = (c + 1) / (NC / R) + 1, j1 = ((c + 1) % (NC / R)) * R + 1;
+      const int r1 = H * ((j1 - 1) + NC * (k1 - 1));
+#pragma unroll
+      for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r] + r1);
+    }
+    if (lane < 32) {
+#pragma unroll
+      for (int rr = 0; rr < R; rr++) {
+        const int ca = (1 + j0 + rr + k) & 1;   // colour of the odd-i cells of row j0+rr
+        const double* A = my + ca * SEG + rr * H;
+        const double* B = my + (1 - ca) * SEG + rr * H;
+#pragma unroll
+        for (int m = 0; m < H; m++) {
+          acc += A[m];
+          acc += B[m];
+        }
+      }
+    }
+  }
+  if (lane < 32 && b0 + lane < n_leaves) out[b0 + lane] = acc;
+}
+
+// generic box size: one lane per leaf straight from HBM
+__global__ void __launch_bounds__(64) k_box_sums_any(LevelView L, int iv, const int* leaves, int n_leaves,
+                                                     double* out) {
   const int q = blockIdx.x * 64 + threadIdx.x;
   if (q >= n_leaves) return;
   const double* u = boxp(L, iv, leaves[q]);
   double acc = 0.0;
-  for (int k = 1; k <= nc; k++) {
-#pragma unroll 2
-    for (int j = 1; j <= nc; j++) {
-      const int r0 = h * ((j - 1) + nc * (k - 1));
-      const double2* A = reinterpret_cast<const double2*>(u + ((1 + j + k) & 1) * L.hv + r0);  // odd i
-      const double2* B = reinterpret_cast<const double2*>(u + ((j + k) & 1) * L.hv + r0);      // even i
-      for (int m = 0; m < h / 2; m++) {
-        const double2 a = A[m], bb = B[m];
-        acc += a.x;
-        acc += bb.x;
-        acc += a.y;
-        acc += bb.y;
-      }
-    }
-  }
+  for (int k = 1; k <= L.nc; k++)
+    for (int j = 1; j <= L.nc; j++)
+      for (int i = 1; i <= L.nc; i++) acc += u[off_int(L, i, j, k)];
   out[q] = acc;
 }
 
-// acc = acc + w*s_q in order (get_sum's loop); the products are formed off
-// the dependent add chain.
-__global__ void __launch_bounds__(256) k_seq_sum2(const double* box_sums, int n, double w, double* acc) {
-  __shared__ double stage[2048];
+// acc = acc + w*s_q in leaf order (get_sum's loop, m_multigrid.f90:284-291).
+// One wave: the box sums are staged through LDS 1024 at a time (the next
+// stage in flight in registers), every lane runs the same add chain reading
+// LDS a group ahead, and the products are formed off the chain.
+__global__ void __launch_bounds__(64) k_seq_sum3(const double* __restrict__ box_sums, int n, double w,
+                                                 double* __restrict__ acc) {
+  constexpr int CH = 1024, PL = CH / 128, G = 16;
+  __shared__ double st[CH];
+  const int lane = threadIdx.x;
   double a = *acc;
-  for (int base = 0; base < n; base += 2048) {
-    const int m = min(2048, n - base);
-    for (int q = threadIdx.x; q < m; q += blockDim.x) stage[q] = w * box_sums[base + q];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int q = 0;
-      for (; q + 8 <= m; q += 8) {
-        const double t0 = stage[q], t1 = stage[q + 1], t2 = stage[q + 2], t3 = stage[q + 3];
-        const double t4 = stage[q + 4], t5 = stage[q + 5], t6 = stage[q + 6], t7 = stage[q + 7];
-        a = a + t0; a = a + t1; a = a + t2; a = a + t3;
-        a = a + t4; a = a + t5; a = a + t6; a = a + t7;
-      }
-      for (; q < m; q++) a = a + stage[q];
+  double2 pre[PL];
+  auto fetch = [&](int base) {
+#pragma unroll
+    for (int r = 0; r < PL; r++) {
+      const int q = base + 2 * (lane + 64 * r);
+      pre[r].x = q < n ? box_sums[q] : 0.0;
+      pre[r].y = q + 1 < n ? box_sums[q + 1] : 0.0;
     }
+  };
+  fetch(0);
+  for (int base = 0; base < n; base += CH) {
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PL; r++) reinterpret_cast<double2*>(st)[lane + 64 * r] = pre[r];
+    __syncthreads();
+    if (base + CH < n) fetch(base + CH);
+    const int m = min(CH, n - base);
+    if (m == CH) {
+      double cur[G], nxt[G];
+#pragma unroll
+      for (int t = 0; t < G; t++) cur[t] = st[t];
+      for (int g = 0; g < CH / G; g++) {
+        const int gn = g + 1 < CH / G ? g + 1 : g;
+#pragma unroll
+        for (int t = 0; t < G; t++) nxt[t] = st[G * gn + t];
+        double p[G];
+#pragma unroll
+        for (int t = 0; t < G; t++) p[t] = w * cur[t];
+#pragma unroll
+        for (int t = 0; t < G; t++) a = a + p[t];
+#pragma unroll
+        for (int t = 0; t < G; t++) cur[t] = nxt[t];
+      }
+    } else {
+      for (int q = 0; q < m; q++) a = a + w * st[q];
+    }
   }
-  if (threadIdx.x == 0) *acc = a;
+  if (lane == 0) *acc = a;
 }
 
 bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }
@@ -239,12 +314,18 @@ void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const i
 
 void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
   if (n == 0) return;
-  k_box_sums2<<<(n + 63) / 64, 64, 0, st>>>(L, iv, leaves, n, out);
+  const dim3 g((n + 31) / 32);
+  switch (L.nc) {
+    case 16: k_box_sums3<16><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
+    case 8: k_box_sums3<8><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
+    case 4: k_box_sums3<4><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
+    default: k_box_sums_any<<<(n + 63) / 64, 64, 0, st>>>(L, iv, leaves, n, out); break;
+  }
 }
 
 void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
   if (n == 0) return;
-  k_seq_sum2<<<1, 256, 0, st>>>(box_sums, n, w, acc);
+  k_seq_sum3<<<1, 64, 0, st>>>(box_sums, n, w, acc);
 }
 
 }  // namespace omg
