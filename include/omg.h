@@ -48,8 +48,10 @@ const char *omg_last_error(void);
  * (replaces mg_comm_init's MPI set-up, src/m_communication.f90:14-35). */
 int omg_get_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
 
-/* Create a context on HIP device `device` for rank `rank` of `n_ranks`.
- * unique_id may be NULL when n_ranks == 1. */
+/* Create a context on HIP device `device` (device < 0: rank modulo the number
+ * of visible devices) for rank `rank` of `n_ranks`.  unique_id may be NULL
+ * when n_ranks == 1.  Replaces the device side of mg_comm_init
+ * (src/m_communication.f90:14-35). */
 int omg_ctx_create(omg_ctx **ctx, int device, int rank, int n_ranks, const void *unique_id);
 int omg_ctx_destroy(omg_ctx *ctx);
 

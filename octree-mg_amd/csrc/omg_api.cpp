@@ -768,6 +768,12 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
   return guarded([&] {
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw OmgError("bad rank / n_ranks");
     if (n_ranks > 1 && !unique_id) throw OmgError("unique_id required for n_ranks > 1");
+    if (device < 0) {   // one rank per GPU: rank modulo the visible devices
+      int n_dev = 0;
+      HIPCHK(hipGetDeviceCount(&n_dev));
+      if (n_dev < 1) throw OmgError("no HIP device visible");
+      device = rank % n_dev;
+    }
     omg_ctx* c = new omg_ctx();
     c->device = device;
     c->rank = rank;

@@ -1,0 +1,429 @@
+!> Drop-in m_multigrid for octree-mg, backed by the MI355X kernels of libomg.so.
+!>
+!> Same module name and public API as the reference's src/m_multigrid.f90
+!> (mg_fas_vcycle :150-243, mg_fas_fmg :84-147, mg_set_methods :27-60,
+!> mg_apply_op :439-456), so the reference's programs (tests/test_*.f90) and
+!> callers compile unchanged against it.  The tree (mg_t, m_build_tree,
+!> m_load_balance, m_allocate_storage) stays host Fortran; every per-level box
+!> loop of the cycle runs on the GPU through the C-ABI of include/omg.h
+!> (bindings in m_omg_capi.f90).
+!>
+!> Host/device coherence: mg%boxes(:)%cc stays the owner of the data.  Each
+!> call uploads every variable of every level this rank owns, runs the cycle on
+!> the device and copies phi, rhs, old and res back (interior and face ghosts;
+!> edge and corner ghosts are not device state: no reference operator reads
+!> them, src/m_ghost_cells.f90 never sets them).  The device context is built
+!> on first use and rebuilt when the tree changes.
+!>
+!> Boundary conditions: mg%bc(nb, iv)%bc_type/bc_value go over as they are; a
+!> boundary_cond callback is tabulated on every physical face of every box of
+!> this rank at each call (the reference evaluates it at each ghost fill, with
+!> the same arguments).  Custom refinement_bnd callbacks, non-Cartesian
+!> geometry and NDIM /= 3 are rejected with error stop.
+module m_multigrid
+  use iso_c_binding
+  use mpi
+  use m_data_structures
+  use m_prolong
+  use m_omg_capi
+
+  implicit none
+  private
+
+  type(c_ptr) :: ctx = c_null_ptr
+  integer     :: ctx_n_boxes = -1
+  integer     :: ctx_n_vars  = -1
+  integer     :: ctx_lowest  = huge(1)
+  integer     :: ctx_highest = -huge(1)
+
+  integer :: timer_device_vcycle = -1
+  integer :: timer_device_fmg    = -1
+  integer :: timer_host_to_dev   = -1
+  integer :: timer_dev_to_host   = -1
+
+  public :: mg_fas_vcycle
+  public :: mg_fas_fmg
+  public :: mg_set_methods
+  public :: mg_apply_op
+
+contains
+
+  !> Operator/smoother selection, unchanged semantics (m_multigrid.f90:27-60):
+  !> the host procedure pointers are still set (mg%box_op stays callable), and
+  !> the device picks the operator from mg%operator_type at the next call.
+  subroutine mg_set_methods(mg)
+    use m_laplacian
+    use m_vlaplacian
+    use m_helmholtz
+    use m_vhelmholtz
+    use m_ahelmholtz
+    type(mg_t), intent(inout) :: mg
+
+    mg%box_prolong => mg_prolong_sparse
+
+    select case (mg%operator_type)
+    case (mg_laplacian)
+       call laplacian_set_methods(mg)
+    case (mg_vlaplacian)
+       call vlaplacian_set_methods(mg)
+    case (mg_helmholtz)
+       call helmholtz_set_methods(mg)
+    case (mg_vhelmholtz)
+       call vhelmholtz_set_methods(mg)
+    case (mg_ahelmholtz)
+       call ahelmholtz_set_methods(mg)
+    case default
+       error stop "mg_set_methods: unknown operator"
+    end select
+
+    if (mg%smoother_type == mg_smoother_gsrb) then
+       mg%n_smoother_substeps = 2
+    else
+       mg%n_smoother_substeps = 1
+    end if
+  end subroutine mg_set_methods
+
+  subroutine check_methods(mg)
+    type(mg_t), intent(inout) :: mg
+    if (.not. associated(mg%box_op) .or. &
+         .not. associated(mg%box_smoother)) then
+       call mg_set_methods(mg)
+    end if
+  end subroutine check_methods
+
+  subroutine add_timers(mg)
+    type(mg_t), intent(inout) :: mg
+    timer_device_vcycle = mg_add_timer(mg, "omg V-cycle (GPU)")
+    timer_device_fmg    = mg_add_timer(mg, "omg FMG (GPU)")
+    timer_host_to_dev   = mg_add_timer(mg, "omg host->GPU")
+    timer_dev_to_host   = mg_add_timer(mg, "omg GPU->host")
+  end subroutine add_timers
+
+  subroutine omg_ok(ierr, what)
+    integer(c_int), intent(in)   :: ierr
+    character(len=*), intent(in) :: what
+    if (ierr /= 0) then
+       print *, "octree-mg GPU backend: ", what, ": ", omg_error_message()
+       error stop "octree-mg GPU backend error"
+    end if
+  end subroutine omg_ok
+
+  !> Perform FAS-FMG cycle (m_multigrid.f90:84-147) on the GPU.
+  subroutine mg_fas_fmg(mg, have_guess, max_res)
+    type(mg_t), intent(inout)       :: mg
+    logical, intent(in)             :: have_guess
+    real(dp), intent(out), optional :: max_res
+    real(c_double)                  :: res
+    integer(c_int)                  :: want
+
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call to_device(mg)
+    want = merge(1_c_int, 0_c_int, present(max_res))
+    call mg_timer_start(mg%timers(timer_device_fmg))
+    call omg_ok(omg_fas_fmg(ctx, merge(1_c_int, 0_c_int, have_guess), want, res), &
+         "mg_fas_fmg")
+    call omg_ok(omg_synchronize(ctx), "synchronize")
+    call mg_timer_end(mg%timers(timer_device_fmg))
+    call to_host(mg)
+    if (present(max_res)) max_res = res
+  end subroutine mg_fas_fmg
+
+  !> Perform FAS V-cycle (m_multigrid.f90:150-243) on the GPU.
+  subroutine mg_fas_vcycle(mg, highest_lvl, max_res, standalone)
+    type(mg_t), intent(inout)       :: mg
+    integer, intent(in), optional   :: highest_lvl
+    real(dp), intent(out), optional :: max_res
+    logical, intent(in), optional   :: standalone
+    real(c_double)                  :: res
+    integer(c_int)                  :: hl, sa, want
+
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call to_device(mg)
+    hl = mg%lowest_lvl - 1              ! "absent" for the C side
+    if (present(highest_lvl)) hl = highest_lvl
+    sa = 1
+    if (present(standalone)) sa = merge(1_c_int, 0_c_int, standalone)
+    want = merge(1_c_int, 0_c_int, present(max_res))
+    call mg_timer_start(mg%timers(timer_device_vcycle))
+    call omg_ok(omg_fas_vcycle(ctx, hl, want, res, sa), "mg_fas_vcycle")
+    call omg_ok(omg_synchronize(ctx), "synchronize")
+    call mg_timer_end(mg%timers(timer_device_vcycle))
+    call to_host(mg)
+    if (present(max_res)) max_res = res
+  end subroutine mg_fas_vcycle
+
+  !> Apply the operator on all levels (m_multigrid.f90:439-456).  A custom
+  !> per-box `op` is a host procedure: it runs on the host boxes as before.
+  subroutine mg_apply_op(mg, i_out, op)
+    type(mg_t), intent(inout)      :: mg
+    integer, intent(in)            :: i_out
+    procedure(mg_box_op), optional :: op
+    integer                        :: lvl, i, id, nc
+
+    if (present(op)) then
+       do lvl = mg%lowest_lvl, mg%highest_lvl
+          nc = mg%box_size_lvl(lvl)
+          do i = 1, size(mg%lvls(lvl)%my_ids)
+             id = mg%lvls(lvl)%my_ids(i)
+             call op(mg, id, nc, i_out)
+          end do
+       end do
+       return
+    end if
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call to_device(mg)
+    call omg_ok(omg_apply_op(ctx, int(i_out, c_int)), "mg_apply_op")
+    call copy_var_to_host(mg, i_out)
+  end subroutine mg_apply_op
+
+  ! ------------------------------------------------------------------------
+  ! Host <-> device
+
+  !> Build (or rebuild) the device context for the current tree.
+  subroutine attach(mg)
+    type(mg_t), intent(inout)    :: mg
+    integer(c_int8_t)            :: uid(omg_unique_id_bytes)
+    integer(c_int), allocatable  :: blvl(:), bpar(:), bch(:, :), bnb(:, :)
+    integer(c_int), allocatable  :: bix(:, :), brank(:), bsl(:), off(:), lists(:)
+    real(c_double), allocatable  :: dr(:, :)
+    integer                      :: n, id, lvl, nlev, t, pos, ierr, n_vars
+
+#if NDIM != 3
+    error stop "octree-mg GPU backend: only NDIM == 3 is supported"
+#endif
+    if (.not. mg%is_allocated) error stop "mg_fas_vcycle: storage not allocated"
+    if (mg%geometry_type /= mg_cartesian) &
+         error stop "octree-mg GPU backend: only Cartesian geometry is supported"
+
+    n_vars = mg_num_vars + mg%n_extra_vars
+    if (c_associated(ctx) .and. ctx_n_boxes == mg%n_boxes .and. &
+         ctx_n_vars == n_vars .and. ctx_lowest == mg%lowest_lvl .and. &
+         ctx_highest == mg%highest_lvl) return
+    if (c_associated(ctx)) call omg_ok(omg_ctx_destroy(ctx), "ctx_destroy")
+
+    uid = 0
+    if (mg%n_cpu > 1) then
+       if (mg%my_rank == 0) call omg_ok(omg_get_unique_id(uid), "get_unique_id")
+       call mpi_bcast(uid, omg_unique_id_bytes, MPI_BYTE, 0, mg%comm, ierr)
+    end if
+    call omg_ok(omg_ctx_create(ctx, -1_c_int, int(mg%my_rank, c_int), &
+         int(mg%n_cpu, c_int), uid), "ctx_create")
+
+    n = mg%n_boxes
+    allocate(blvl(n), bpar(n), bch(2**NDIM, n), bnb(2*NDIM, n), bix(NDIM, n), brank(n))
+    do id = 1, n
+       blvl(id)     = mg%boxes(id)%lvl
+       bpar(id)     = mg%boxes(id)%parent
+       bch(:, id)   = mg%boxes(id)%children
+       bnb(:, id)   = mg%boxes(id)%neighbors
+       bix(:, id)   = mg%boxes(id)%ix
+       brank(id)    = mg%boxes(id)%rank
+    end do
+
+    nlev = mg%highest_lvl - mg%lowest_lvl + 1
+    allocate(bsl(nlev), dr(NDIM, nlev), off(4*nlev+1))
+    pos = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       pos = pos + size(mg%lvls(lvl)%ids) + size(mg%lvls(lvl)%leaves) + &
+            size(mg%lvls(lvl)%parents) + size(mg%lvls(lvl)%ref_bnds)
+    end do
+    allocate(lists(max(pos, 1)))
+    pos = 0
+    off(1) = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       t = lvl - mg%lowest_lvl
+       bsl(t+1)   = mg%box_size_lvl(lvl)
+       dr(:, t+1) = mg%dr(:, lvl)
+       call put_list(mg%lvls(lvl)%ids, 4*t+2)
+       call put_list(mg%lvls(lvl)%leaves, 4*t+3)
+       call put_list(mg%lvls(lvl)%parents, 4*t+4)
+       call put_list(mg%lvls(lvl)%ref_bnds, 4*t+5)
+    end do
+
+    call omg_ok(omg_tree_setup(ctx, int(n, c_int), blvl, bpar, bch, bnb, bix, brank, &
+         int(mg%lowest_lvl, c_int), int(mg%highest_lvl, c_int), &
+         int(mg%first_normal_lvl, c_int), int(mg%box_size, c_int), bsl, dr, off, &
+         lists, int(n_vars, c_int)), "tree_setup")
+    ctx_n_boxes = mg%n_boxes
+    ctx_n_vars  = n_vars
+    ctx_lowest  = mg%lowest_lvl
+    ctx_highest = mg%highest_lvl
+
+  contains
+
+    subroutine put_list(ids, slot)
+      integer, intent(in) :: ids(:)
+      integer, intent(in) :: slot
+      integer             :: m
+      m = size(ids)
+      if (m > 0) lists(pos+1:pos+m) = ids
+      pos = pos + m
+      off(slot) = pos
+    end subroutine put_list
+  end subroutine attach
+
+  !> Methods, boundary conditions and all data of this rank onto the device.
+  subroutine to_device(mg)
+    use m_helmholtz, only: helmholtz_lambda
+    use m_ahelmholtz, only: ahelmholtz_lambda
+    type(mg_t), intent(inout) :: mg
+    real(c_double)            :: lambda
+    integer                   :: iv, nb, lvl, n_vars
+
+    call attach(mg)
+    call mg_timer_start(mg%timers(timer_host_to_dev))
+
+    select case (mg%operator_type)
+    case (mg_laplacian)
+       lambda = 0.0_dp
+    case (mg_helmholtz)
+       lambda = helmholtz_lambda
+    case (mg_ahelmholtz)
+       lambda = ahelmholtz_lambda
+    case default
+       error stop "octree-mg GPU backend: operator not supported on the GPU yet"
+    end select
+    call omg_ok(omg_set_operator(ctx, int(mg%operator_type, c_int), lambda), "set_operator")
+    call omg_ok(omg_set_smoother(ctx, int(mg%smoother_type, c_int), &
+         int(mg%n_cycle_down, c_int), int(mg%n_cycle_up, c_int), &
+         int(mg%max_coarse_cycles, c_int), real(mg%residual_coarse_abs, c_double), &
+         real(mg%residual_coarse_rel, c_double)), "set_smoother")
+    call omg_ok(omg_set_subtract_mean(ctx, merge(1_c_int, 0_c_int, mg%subtract_mean)), &
+         "set_subtract_mean")
+
+    n_vars = mg_num_vars + mg%n_extra_vars
+    do iv = 1, n_vars
+       do nb = 1, mg_num_neighbors
+          if (associated(mg%bc(nb, iv)%refinement_bnd)) &
+               error stop "octree-mg GPU backend: custom refinement_bnd not supported"
+          call omg_ok(omg_set_bc(ctx, int(iv, c_int), int(nb, c_int), &
+               int(mg%bc(nb, iv)%bc_type, c_int), real(mg%bc(nb, iv)%bc_value, c_double)), &
+               "set_bc")
+       end do
+       if (any([(associated(mg%bc(nb, iv)%boundary_cond), nb = 1, mg_num_neighbors)])) &
+            call tabulate_bc(mg, iv)
+    end do
+
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       do iv = 1, n_vars
+          call copy_level(mg, lvl, iv, .true.)
+       end do
+    end do
+    ! mg_phi_bc_store's data sits in the uploaded rhs ghost cells; the device
+    ! flag follows the host one (m_ghost_cells.f90:66-78, 266-270)
+    if (mg%phi_bc_data_stored) call omg_ok(omg_phi_bc_store(ctx), "phi_bc_store")
+    call mg_timer_end(mg%timers(timer_host_to_dev))
+  end subroutine to_device
+
+  !> phi, rhs, old and res of every level back into mg%boxes(:)%cc.
+  subroutine to_host(mg)
+    type(mg_t), intent(inout) :: mg
+    integer                   :: lvl, iv
+    call mg_timer_start(mg%timers(timer_dev_to_host))
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       do iv = 1, mg_num_vars
+          call copy_level(mg, lvl, iv, .false.)
+       end do
+    end do
+    call mg_timer_end(mg%timers(timer_dev_to_host))
+  end subroutine to_host
+
+  subroutine copy_var_to_host(mg, iv)
+    type(mg_t), intent(inout) :: mg
+    integer, intent(in)       :: iv
+    integer                   :: lvl
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       call copy_level(mg, lvl, iv, .false.)
+    end do
+  end subroutine copy_var_to_host
+
+  !> One variable of all my boxes at lvl, in my_ids order, (nc+2)^3 per box.
+  subroutine copy_level(mg, lvl, iv, up)
+    type(mg_t), intent(inout)   :: mg
+    integer, intent(in)         :: lvl, iv
+    logical, intent(in)         :: up
+    real(c_double), allocatable :: buf(:, :, :, :)
+    integer                     :: i, id, nc, n
+
+    n = size(mg%lvls(lvl)%my_ids)
+    if (n == 0) return
+    nc = mg%box_size_lvl(lvl)
+    allocate(buf(0:nc+1, 0:nc+1, 0:nc+1, n))
+    if (up) then
+       do i = 1, n
+          id = mg%lvls(lvl)%my_ids(i)
+          buf(:, :, :, i) = mg%boxes(id)%cc(:, :, :, iv)
+       end do
+       call omg_ok(omg_upload_level(ctx, int(lvl, c_int), int(iv, c_int), buf), "upload_level")
+    else
+       call omg_ok(omg_download_level(ctx, int(lvl, c_int), int(iv, c_int), buf), &
+            "download_level")
+       do i = 1, n
+          id = mg%lvls(lvl)%my_ids(i)
+          associate (cc => mg%boxes(id)%cc)
+            cc(1:nc, 1:nc, 1:nc, iv) = buf(1:nc, 1:nc, 1:nc, i)
+            cc(0, 1:nc, 1:nc, iv)    = buf(0, 1:nc, 1:nc, i)
+            cc(nc+1, 1:nc, 1:nc, iv) = buf(nc+1, 1:nc, 1:nc, i)
+            cc(1:nc, 0, 1:nc, iv)    = buf(1:nc, 0, 1:nc, i)
+            cc(1:nc, nc+1, 1:nc, iv) = buf(1:nc, nc+1, 1:nc, i)
+            cc(1:nc, 1:nc, 0, iv)    = buf(1:nc, 1:nc, 0, i)
+            cc(1:nc, 1:nc, nc+1, iv) = buf(1:nc, 1:nc, nc+1, i)
+          end associate
+       end do
+    end if
+  end subroutine copy_level
+
+  !> Evaluate the boundary_cond callbacks of variable iv on every physical
+  !> face of my boxes (set_ghost_cells' call, m_ghost_cells.f90:264-278).
+  subroutine tabulate_bc(mg, iv)
+    type(mg_t), intent(inout)         :: mg
+    integer, intent(in)               :: iv
+    integer(c_long_long), allocatable :: face_off(:)
+    integer(c_int), allocatable       :: face_type(:)
+    real(c_double), allocatable       :: data(:)
+    real(dp), allocatable             :: bc(:, :)
+    integer                           :: lvl, i, id, nb, nc, bc_type
+    integer(c_long_long)              :: n_data, m
+
+    allocate(face_off(6 * mg%n_boxes), face_type(6 * mg%n_boxes))
+    face_off  = -1
+    face_type = 0
+    n_data = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       nc = mg%box_size_lvl(lvl)
+       do i = 1, size(mg%lvls(lvl)%my_ids)
+          id = mg%lvls(lvl)%my_ids(i)
+          do nb = 1, mg_num_neighbors
+             if (mg%boxes(id)%neighbors(nb) < mg_no_box .and. &
+                  associated(mg%bc(nb, iv)%boundary_cond)) n_data = n_data + nc * nc
+          end do
+       end do
+    end do
+    allocate(data(max(n_data, 1_c_long_long)))
+    m = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       nc = mg%box_size_lvl(lvl)
+       allocate(bc(nc, nc))
+       do i = 1, size(mg%lvls(lvl)%my_ids)
+          id = mg%lvls(lvl)%my_ids(i)
+          do nb = 1, mg_num_neighbors
+             if (mg%boxes(id)%neighbors(nb) < mg_no_box .and. &
+                  associated(mg%bc(nb, iv)%boundary_cond)) then
+                call mg%bc(nb, iv)%boundary_cond(mg%boxes(id), nc, iv, nb, bc_type, bc)
+                face_off(6*(id-1) + nb) = m
+                face_type(6*(id-1) + nb) = bc_type
+                data(m+1:m+nc*nc) = reshape(bc, [nc*nc])
+                m = m + nc * nc
+             end if
+          end do
+       end do
+       deallocate(bc)
+    end do
+    call omg_ok(omg_set_bc_faces(ctx, int(iv, c_int), face_off, face_type, data, n_data), &
+         "set_bc_faces")
+  end subroutine tabulate_bc
+
+end module m_multigrid
