@@ -398,8 +398,10 @@ void update_coarse(omg_ctx* c, int lvl) {
 // correct_children (m_multigrid.f90:387-402)
 void correct_children(omg_ctx* c, int lvl) {
   Level* C = level_ptr(c, lvl);
-  if (C && !C->parents.empty())
+  if (C && !C->parents.empty()) {
+    Prof p(c, "sub_parents", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl);
     launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
+  }
   prolong(c, lvl, 4, 1, 1);
 }
 
@@ -411,8 +413,10 @@ void correct_and_fill(omg_ctx* c, int lvl) {
   Level* C = level_ptr(c, lvl);
   if (F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
       !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv))) {
-    if (!C->parents.empty())
+    if (!C->parents.empty()) {
+      Prof p(c, "sub_parents", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl);
       launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
+    }
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
@@ -479,7 +483,10 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts) {
   HIPCHK(hipMemcpyAsync(c->d_scalar + 3, c->h_scalar + 3, 8, hipMemcpyHostToDevice, c->stream));
   for (int l = c->lowest; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
-    if (L && L->n) launch_subtract(L->view(), iv, c->d_scalar + 3, ghosts, c->stream);
+    if (L && L->n) {
+      Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, l);
+      launch_subtract(L->view(), iv, c->d_scalar + 3, ghosts, c->stream);
+    }
   }
 }
 

@@ -3,7 +3,7 @@
 # kernel regex over tools/sweep_bench.py.   tools/pmc.sh <regex> <op> [reps]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-RE=${1:-gsrb_sweep}; OP=${2:-smooth}; REPS=${3:-5}
+RE=${1:-k_gsrb_tile}; OP=${2:-smooth}; REPS=${3:-5}
 OUT=$PWD/gpurun_out/pmc_$OP
 mkdir -p "$OUT"
 timeout -k 10 300 python3 tools/sweep_bench.py 20 512 $OP > "$OUT/time.log" 2>&1 || exit $?
