@@ -48,6 +48,12 @@ const char *omg_last_error(void);
  * (replaces mg_comm_init's MPI set-up, src/m_communication.f90:14-35). */
 int omg_get_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
 
+/* Loopback transport (testing the multi-rank path on ONE GPU): fills `out`
+ * with an id that makes omg_ctx_create join an in-process group `tag` of
+ * n_ranks contexts, one host thread each, exchanging halos by device copies
+ * instead of RCCL (same plans, kernels and reduction orders). */
+int omg_loopback_unique_id(long long tag, void *out /* OMG_UNIQUE_ID_BYTES */);
+
 /* Create a context on HIP device `device` (device < 0: rank modulo the number
  * of visible devices) for rank `rank` of `n_ranks`.  unique_id may be NULL
  * when n_ranks == 1.  Replaces the device side of mg_comm_init

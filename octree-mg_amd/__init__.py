@@ -7,7 +7,7 @@ host mirror of the reference's Fortran API (mg.py) and its tree bookkeeping
 (tree.py).  The Fortran drop-in m_multigrid lives in fortran/.
 """
 from . import device, problems, tree  # noqa: F401
-from .mg import (BC, MG, helmholtz_set_lambda, mg_add_children, mg_allocate_storage,  # noqa: F401
+from .mg import (BC, MG, Loopback, helmholtz_set_lambda, mg_add_children, mg_allocate_storage,  # noqa: F401
                  mg_apply_op, mg_build_rectangle, mg_comm_init, mg_deallocate_storage,
                  mg_fas_fmg, mg_fas_vcycle, mg_fill_ghost_cells, mg_fill_ghost_cells_lvl,
                  mg_load_balance, mg_load_balance_parents, mg_load_balance_simple,

@@ -10,6 +10,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <tuple>
 #include <climits>
 #include <cstdio>
 #include <cstring>
@@ -135,7 +139,7 @@ void finalize_transfer(Transfer& T) {
 struct Rec {
   int peer;
   long long key;
-  int a, b;
+  int a, b, c = 0;
 };
 std::vector<PeerList> group(std::vector<Rec>& recs, int ints_per_item) {
   std::sort(recs.begin(), recs.end(), [](const Rec& x, const Rec& y) {
@@ -148,9 +152,126 @@ std::vector<PeerList> group(std::vector<Rec>& recs, int ints_per_item) {
       out.back().peer = r.peer;
     }
     out.back().items.push_back(r.a);
-    if (ints_per_item == 2) out.back().items.push_back(r.b);
+    if (ints_per_item >= 2) out.back().items.push_back(r.b);
+    if (ints_per_item >= 3) out.back().items.push_back(r.c);
   }
   return out;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// In-process loopback transport.  n_ranks contexts of ONE process (one host
+// thread each, typically sharing one GPU) exchange their transfer segments by
+// device-to-device copies ordered with HIP events, instead of RCCL.  The plans,
+// the packing/unpacking kernels, the wire order and the reductions are those
+// of the RCCL path, so multi-rank parity can be checked on a single GPU.
+struct omg_loop {
+  struct Msg {
+    const double* src;
+    size_t n;
+    hipEvent_t ev;
+  };
+  using Key = std::tuple<int, int, long long>;   // (from, to, sequence of that pair)
+  int n_ranks = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<Key, Msg> box;
+  std::map<Key, hipEvent_t> acks;               // (receiver, sender, seq) -> copies done
+  std::map<long long, std::vector<double>> vals;
+  std::map<long long, int> n_in, n_out;
+};
+
+namespace {
+
+constexpr char kLoopMagic[16] = "OMG-LOOPBACK-v1";
+std::mutex g_loop_mu;
+std::map<long long, std::shared_ptr<omg_loop>> g_loops;
+
+template <typename Pred>
+void loop_wait(omg_ctx* c, std::unique_lock<std::mutex>& lk, Pred pred, const std::string& what) {
+  if (!c->loop->cv.wait_for(lk, std::chrono::seconds(60), pred))
+    throw OmgError(std::string("loopback transport: rank ") + std::to_string(c->rank) +
+                   " timed out waiting for " + what);
+}
+
+hipEvent_t loop_event(hipStream_t st) {
+  hipEvent_t e;
+  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e, st));
+  return e;
+}
+
+void loop_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf) {
+  omg_loop& G = *c->loop;
+  const size_t per = (size_t)T.item_doubles;
+  const int me = c->rank;
+  for (auto& p : T.send) {
+    const size_t n = p.items.size() / T.send_ints * per;
+    hipEvent_t ev = loop_event(c->stream);
+    std::lock_guard<std::mutex> lk(G.mu);
+    G.box[{me, p.peer, c->loop_seq_send[p.peer]}] = {sendbuf + (size_t)p.offset * per, n, ev};
+    G.cv.notify_all();
+  }
+  for (auto& p : T.recv) {
+    const size_t n = p.items.size() / T.recv_ints * per;
+    const omg_loop::Key k{p.peer, me, c->loop_seq_recv[p.peer]};
+    omg_loop::Msg m;
+    {
+      std::unique_lock<std::mutex> lk(G.mu);
+      loop_wait(c, lk, [&] { return G.box.count(k) > 0; },
+                "a message from rank " + std::to_string(p.peer) + " (pair sequence " +
+                    std::to_string(std::get<2>(k)) + ", " + std::to_string(n) + " doubles)");
+      m = G.box[k];
+      G.box.erase(k);
+    }
+    if (m.n != n) throw OmgError("loopback transport: message size mismatch");
+    HIPCHK(hipStreamWaitEvent(c->stream, m.ev, 0));
+    HIPCHK(hipMemcpyAsync(recvbuf + (size_t)p.offset * per, m.src, n * sizeof(double),
+                          hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipEventDestroy(m.ev));
+  }
+  for (auto& p : T.recv) {   // the sender may reuse its buffer once our copies ran
+    hipEvent_t ev = loop_event(c->stream);
+    std::lock_guard<std::mutex> lk(G.mu);
+    G.acks[{me, p.peer, c->loop_seq_recv[p.peer]++}] = ev;
+    G.cv.notify_all();
+  }
+  for (auto& p : T.send) {
+    const omg_loop::Key k{p.peer, me, c->loop_seq_send[p.peer]++};
+    hipEvent_t ev;
+    {
+      std::unique_lock<std::mutex> lk(G.mu);
+      loop_wait(c, lk, [&] { return G.acks.count(k) > 0; },
+                "the acknowledgement of rank " + std::to_string(p.peer) + " (pair sequence " +
+                    std::to_string(std::get<2>(k)) + ")");
+      ev = G.acks[k];
+      G.acks.erase(k);
+    }
+    HIPCHK(hipStreamWaitEvent(c->stream, ev, 0));
+    HIPCHK(hipEventDestroy(ev));
+  }
+}
+
+// every rank's value, in rank order (the loopback MPI_Allgather)
+std::vector<double> loop_allgather(omg_ctx* c, double v) {
+  omg_loop& G = *c->loop;
+  const long long s = c->loop_ar_seq++;
+  std::unique_lock<std::mutex> lk(G.mu);
+  auto& vals = G.vals[s];
+  vals.resize(G.n_ranks);
+  vals[c->rank] = v;
+  G.n_in[s]++;
+  G.cv.notify_all();
+  loop_wait(c, lk, [&] { return G.n_in[s] == G.n_ranks; },
+            "allreduce #" + std::to_string(s) + " (" + std::to_string(G.n_in[s]) + " ranks in)");
+  std::vector<double> all = G.vals[s];
+  if (++G.n_out[s] == G.n_ranks) {
+    G.vals.erase(s);
+    G.n_in.erase(s);
+    G.n_out.erase(s);
+  }
+  return all;
 }
 
 // One grouped RCCL round: send segment i to peer i, receive likewise
@@ -158,6 +279,10 @@ std::vector<PeerList> group(std::vector<Rec>& recs, int ints_per_item) {
 void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf) {
   if (c->n_ranks == 1) return;
   if (T.send.empty() && T.recv.empty()) return;
+  if (c->loop) {
+    loop_exchange(c, T, sendbuf, recvbuf);
+    return;
+  }
   ncclComm_t comm = (ncclComm_t)c->nccl;
   const size_t per = (size_t)T.item_doubles;
   NCCLCHK(ncclGroupStart());
@@ -241,9 +366,20 @@ void phi_dirty_all(omg_ctx* c) {
 // halo exchange of the faces packed by the last fill/substep kernel, then
 // fill_buffered_nb (m_ghost_cells.f90:163-174, 424-454)
 void finish_halo(omg_ctx* c, Level* L, int iv) {
-  if (c->n_ranks == 1 || !(L->halo.n_send || L->halo.n_recv)) return;
-  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
-  launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+  if (c->n_ranks == 1) return;
+  if (L->halo.n_send || L->halo.n_recv) {
+    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
+    launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+  }
+  // refinement boundaries across ranks (buffer_refinement_boundaries,
+  // m_ghost_cells.f90:157-162, 200-229): coarse faces go out interpolated,
+  // the fine side applies sides_rb once they arrive
+  if (L->rbx.n_send || L->rbx.n_recv) {
+    launch_rb_pack(view_of(c, L->lvl - 1), iv, L->rbx.d_send_items, L->rbx.n_send, L->nc, L->d_rbsend,
+                   c->stream);
+    exchange(c, L->rbx, L->d_rbsend, L->d_rbrecv);
+    launch_rb_unpack(L->view(), iv, L->rbx.d_recv_items, L->rbx.n_recv, L->d_rbrecv, c->stream);
+  }
 }
 
 // mg_fill_ghost_cells_lvl (m_ghost_cells.f90:131-175): same-GPU faces are
@@ -434,14 +570,22 @@ void correct_and_fill(omg_ctx* c, int lvl) {
 // pairwise order of MPICH for power-of-two communicators.
 double allreduce(omg_ctx* c, double v, bool is_max) {
   if (c->n_ranks == 1) return v;
-  double* d = c->d_scalar + 8;
-  c->h_scalar[1] = v;
-  HIPCHK(hipMemcpyAsync(d, &c->h_scalar[1], 8, hipMemcpyHostToDevice, c->stream));
-  NCCLCHK(ncclAllGather(d, d + 1, 1, ncclDouble, (ncclComm_t)c->nccl, c->stream));
   std::vector<double> all(c->n_ranks);
-  HIPCHK(hipMemcpyAsync(all.data(), d + 1, 8 * c->n_ranks, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->loop) {
+    all = loop_allgather(c, v);
+  } else {
+    double* d = c->d_scalar + 8;
+    c->h_scalar[1] = v;
+    HIPCHK(hipMemcpyAsync(d, &c->h_scalar[1], 8, hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclAllGather(d, d + 1, 1, ncclDouble, (ncclComm_t)c->nccl, c->stream));
+    HIPCHK(hipMemcpyAsync(all.data(), d + 1, 8 * c->n_ranks, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
   if (is_max) return *std::max_element(all.begin(), all.end());
+  // MPI_Allreduce(MPI_SUM) as MPICH 3.3.2 computes it on one node
+  // (m_multigrid.f90:255): a binomial-tree reduce to rank 0 in rank order,
+  // ((a0+a1)+(a2+a3))+a4 ..., then a broadcast.  Pinned by the golden runs
+  // of the reference at 1-6 and 8 ranks (per32_gsrb_v).
   for (int w = 1; w < c->n_ranks; w *= 2)
     for (int r = 0; r + w < c->n_ranks; r += 2 * w) all[r] = all[r] + all[r + w];
   return all[0];
@@ -565,7 +709,8 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch);
-    for (Transfer* T : {&L.halo, &L.restr, &L.prol}) {
+    dfree(L.d_rbsend); dfree(L.d_rbrecv);
+    for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
     }
@@ -609,7 +754,7 @@ void build_plan(omg_ctx* c) {
     // neighbour table + halo receive plan
     L.h_nbk.assign((size_t)L.n * 6, NB_LOCAL);
     L.h_nba.assign((size_t)L.n * 6, 0);
-    std::vector<Rec> hrecv, hsend;
+    std::vector<Rec> hrecv, hsend, rbrecv, rbsend;
     for (int b = 0; b < L.n; b++) {
       const int id = L.ids[b];
       for (int nb = 1; nb <= 6; nb++) {
@@ -630,8 +775,11 @@ void build_plan(omg_ctx* c) {
           const int p_id = T.parent(id);
           const int p_nb = p_id > 0 ? T.nbr(p_id, nb) : 0;
           if (p_nb <= 0) throw OmgError("refinement boundary without coarse neighbour");
-          if (T.rank(p_nb) != me)
-            throw OmgError("refinement boundary across ranks is not supported yet");
+          if (T.rank(p_nb) != me) {
+            L.h_nbk[f] = NB_RBREM;
+            rbrecv.push_back({T.rank(p_nb), (long long)id * 6 + nb, (int)f, 0});
+            continue;
+          }
           RBRec r;
           r.coarse_idx = c->local_index[p_nb];
           T.child_offset(id, r.dix);
@@ -644,6 +792,35 @@ void build_plan(omg_ctx* c) {
         }
       }
     }
+    // coarse side of the refinement boundaries toward other ranks: my
+    // ref_bnds at lvl-1 next to a refined box with children elsewhere
+    // (buffer_refinement_boundaries, m_ghost_cells.f90:200-229)
+    if (l > c->lowest)
+      for (int cid : c->ref_bnds[l - 1]) {
+        if (T.rank(cid) != me) continue;
+        for (int nb = 1; nb <= 6; nb++) {
+          const int nid = T.nbr(cid, nb);
+          if (nid <= 0 || T.child(nid, 1) <= 0) continue;
+          const int rev = kNeighbRev[nb - 1];
+          for (int s = 1; s <= 8; s++) {
+            const int ch = T.child(nid, s);
+            // children of nid on the face toward cid: child offset along the
+            // normal matches the low/high side rev points to
+            const int d = (nb + 1) >> 1, bit = ((s - 1) >> (d - 1)) & 1;
+            if (bit != ((rev & 1) ? 0 : 1)) continue;
+            if (ch <= 0 || T.rank(ch) == me) continue;
+            int dd[3];
+            T.child_offset(ch, dd);
+            rbsend.push_back({T.rank(ch), (long long)ch * 6 + rev, c->local_index[cid], nb, pack_dix(dd)});
+          }
+        }
+      }
+    L.rbx.recv = group(rbrecv, 1);
+    L.rbx.send = group(rbsend, 3);
+    L.rbx.send_ints = 3;
+    L.rbx.recv_ints = 1;
+    L.rbx.item_doubles = nc * nc;
+    finalize_transfer(L.rbx);
     L.halo.recv = group(hrecv, 1);
     L.halo.send = group(hsend, 1);
     L.halo.send_ints = L.halo.recv_ints = 1;
@@ -660,7 +837,7 @@ void build_plan(omg_ctx* c) {
         for (int f : p.items) sendpos[f] = pos++;
     }
     finalize_transfer(L.halo);
-    L.has_rb = !L.h_rb.empty();
+    L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
     L.d_phi = L.d_data;
@@ -751,6 +928,10 @@ void build_plan(omg_ctx* c) {
       L.recvbuf_doubles = recvn[l];
       if (sendn[l]) HIPCHK(hipMalloc(&L.d_sendbuf, sizeof(double) * sendn[l]));
       if (recvn[l]) HIPCHK(hipMalloc(&L.d_recvbuf, sizeof(double) * recvn[l]));
+      if (L.rbx.n_send)
+        HIPCHK(hipMalloc(&L.d_rbsend, sizeof(double) * (size_t)L.rbx.n_send * L.rbx.item_doubles));
+      if (L.rbx.n_recv)
+        HIPCHK(hipMalloc(&L.d_rbrecv, sizeof(double) * (size_t)L.rbx.n_recv * L.rbx.item_doubles));
     }
   }
 }
@@ -768,6 +949,14 @@ int omg_get_unique_id(void* out) {
     ncclUniqueId id;
     NCCLCHK(ncclGetUniqueId(&id));
     std::memcpy(out, &id, sizeof(id));
+  });
+}
+
+int omg_loopback_unique_id(long long tag, void* out) {
+  return guarded([&] {
+    std::memset(out, 0, OMG_UNIQUE_ID_BYTES);
+    std::memcpy(out, kLoopMagic, sizeof(kLoopMagic));
+    std::memcpy((char*)out + sizeof(kLoopMagic), &tag, sizeof(tag));
   });
 }
 
@@ -794,7 +983,18 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
         c->bc[iv].type[nb] = OMG_BC_DIRICHLET;
         c->bc[iv].value[nb] = 0.0;
       }
-    if (n_ranks > 1) {
+    if (n_ranks > 1 && std::memcmp(unique_id, kLoopMagic, sizeof(kLoopMagic)) == 0) {
+      long long tag;
+      std::memcpy(&tag, (const char*)unique_id + sizeof(kLoopMagic), sizeof(tag));
+      std::lock_guard<std::mutex> lk(g_loop_mu);
+      auto& g = g_loops[tag];
+      if (!g) {
+        g = std::make_shared<omg_loop>();
+        g->n_ranks = n_ranks;
+      }
+      if (g->n_ranks != n_ranks) throw OmgError("loopback group: n_ranks mismatch");
+      c->loop = g;
+    } else if (n_ranks > 1) {
       ncclUniqueId id;
       std::memcpy(&id, unique_id, sizeof(id));
       ncclComm_t comm;
@@ -815,6 +1015,15 @@ int omg_ctx_destroy(omg_ctx* c) {
     dfree(c->d_stage);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
+    if (c->loop) {   // the last context of a loopback group removes it
+      std::lock_guard<std::mutex> lk(g_loop_mu);
+      for (auto it = g_loops.begin(); it != g_loops.end(); ++it)
+        if (it->second == c->loop && it->second.use_count() == 2) {
+          g_loops.erase(it);
+          break;
+        }
+      c->loop.reset();
+    }
     (void)hipStreamDestroy(c->stream);
     delete c;
   });

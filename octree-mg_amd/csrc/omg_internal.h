@@ -14,12 +14,15 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
 namespace omg {
 
-enum NbKind : int8_t { NB_LOCAL = 0, NB_PHYS = 1, NB_RB = 2, NB_REMOTE = 3 };
+// NB_RBREM: refinement boundary whose coarse neighbour lives on another rank;
+// its interpolated coarse face arrives with the halo (buffer_for_fine_nb).
+enum NbKind : int8_t { NB_LOCAL = 0, NB_PHYS = 1, NB_RB = 2, NB_REMOTE = 3, NB_RBREM = 4 };
 
 enum Op : int { OP_LPL = 1, OP_VLPL = 2, OP_HELM = 3, OP_VHELM = 4, OP_AHELM = 5 };
 
@@ -114,6 +117,10 @@ struct Level {
   Transfer halo;        // ghost faces of this level (items: box*6+nb)
   Transfer restr;       // restriction this level -> lvl-1 (send: child idx; recv: parent*8+slot)
   Transfer prol;        // prolongation lvl-1 -> this level (send: child global → parent idx*8+slot; recv: my child idx)
+  Transfer rbx;         // refinement-boundary faces across ranks at this level (send: coarse idx at
+                        // lvl-1, coarse-side nb, child offset; recv: box*6+nb of my fine face)
+  double* d_rbsend = nullptr;
+  double* d_rbrecv = nullptr;
   double* d_sendbuf = nullptr;
   double* d_recvbuf = nullptr;
   size_t sendbuf_doubles = 0, recvbuf_doubles = 0;
@@ -156,10 +163,15 @@ struct KStat {
 
 }  // namespace omg
 
+struct omg_loop;   // in-process loopback transport (omg_api.cpp)
+
 struct omg_ctx {
   int device = 0, rank = 0, n_ranks = 1;
   hipStream_t stream = nullptr;
   void* nccl = nullptr;  // ncclComm_t
+  std::shared_ptr<omg_loop> loop;           // set instead of nccl in loopback mode
+  std::map<int, long long> loop_seq_send, loop_seq_recv;
+  long long loop_ar_seq = 0;
   // tree (global, host)
   int n_boxes = 0, lowest = 0, highest = 0, first_normal = 0, box_size = 0, n_vars = 4;
   std::vector<int> lvl, parent, children, neighbors, ix, rank_of;

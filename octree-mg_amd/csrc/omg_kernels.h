@@ -29,6 +29,8 @@ void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C,
                     const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, const double* recv,
                          hipStream_t st);
+void launch_rb_pack(const LevelView& C, int iv, const int* items, int n, int nc, double* buf, hipStream_t st);
+void launch_rb_unpack(const LevelView& L, int iv, const int* items, int n, const double* recv, hipStream_t st);
 void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* pairs, int n_pairs,
                      const int* parent_local, const int* dixp, hipStream_t st);
 void launch_restrict_pack(const LevelView& F, int iv, const int* items, int n, double* buf,

@@ -68,7 +68,7 @@ __device__ __forceinline__ void face_cell_fill(const LevelView& L, int iv, int b
       c0 = 0; c1 = 2; c2 = -1;
     }
     u[gi] = c0 * bv + c1 * u[off_face_cell(L, nb, x1, a, c)] + c2 * u[off_face_cell(L, nb, x2, a, c)];
-  } else {
+  } else if (kind == NB_RB) {
     // refinement boundary: box_gc_for_fine_neighbor + sides_rb
     // (m_ghost_cells.f90:287-328, 500-577, 769-861)
     const RBRec R = rb[arg];
@@ -106,6 +106,50 @@ __global__ void __launch_bounds__(256) k_unpack_faces(LevelView L, int iv, const
     const int q = (int)(t / nc2), cell = (int)(t % nc2);
     const int it = items[q], b = it / 6, nb = it % 6 + 1;
     boxp(L, iv, b)[off_gh(L, nb, cell % nc + 1, cell / nc + 1)] = recv[t];
+  }
+}
+
+// buffer_for_fine_nb (m_ghost_cells.f90:385-422) on the coarse rank: the
+// coarse face next to a fine neighbour on another rank, interpolated by
+// box_gc_for_fine_neighbor (:500-577).  Item = (coarse box, coarse-side nb,
+// packed child offset of the fine box).
+__global__ void __launch_bounds__(256) k_rb_pack(LevelView C, int iv, const int* items, int n_items, int nc,
+                                                 double* buf) {
+  const int nc2 = nc * nc;
+  GRID_STRIDE(t, (long long)n_items * nc2) {
+    const int q = (int)(t / nc2), cell = (int)(t % nc2);
+    const int cb = items[3 * q], nbc = items[3 * q + 1], dp = items[3 * q + 2];
+    const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
+    const int a = cell % nc + 1, c = cell / nc + 1;
+    const int d = (nbc + 1) >> 1;
+    const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;
+    const int clayer = (nbc & 1) ? 1 : C.nc;     // low side: cc(1,..), high: cc(nc,..)
+    const double* cu = boxp(C, iv, cb);
+    const int i = (a + 1) >> 1, j = (c + 1) >> 1;
+    auto T = [&](int p, int r) { return cu[off_face_cell(C, nbc, clayer, dix[t1] + p, dix[t2] + r)]; };
+    const double tc = T(i, j);
+    const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
+    const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
+    double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
+    gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
+    buf[t] = gv;
+  }
+}
+
+// fill_refinement_bnd with a remote coarse neighbour (m_ghost_cells.f90:
+// 305-311) + sides_rb (:769-861) on the fine rank.
+__global__ void __launch_bounds__(256) k_rb_unpack(LevelView L, int iv, const int* items, int n_items,
+                                                   const double* recv) {
+  const int nc = L.nc, nc2 = nc * nc;
+  GRID_STRIDE(t, (long long)n_items * nc2) {
+    const int q = (int)(t / nc2), cell = (int)(t % nc2);
+    const int it = items[q], b = it / 6, nb = it % 6 + 1;
+    const int a = cell % nc + 1, c = cell / nc + 1;
+    const bool low = nb & 1;
+    const int x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
+    double* u = boxp(L, iv, b);
+    u[off_gh(L, nb, a, c)] = 0.5 * recv[t] + 0.75 * u[off_face_cell(L, nb, x1, a, c)] -
+                             0.25 * u[off_face_cell(L, nb, x2, a, c)];
   }
 }
 
@@ -490,6 +534,18 @@ void launch_residual(const LevelView& L, int op, double lambda, unsigned long lo
   const long long work = 2LL * L.hv * L.n;
   if (work == 0) return;
   OP_SWITCH(op, k_residual, grid_for(work), 256, st, L, lambda, maxbits);
+}
+
+void launch_rb_pack(const LevelView& C, int iv, const int* items, int n, int nc, double* buf, hipStream_t st) {
+  if (n == 0) return;
+  const long long work = (long long)n * nc * nc;
+  k_rb_pack<<<grid_for(work), 256, 0, st>>>(C, iv, items, n, nc, buf);
+}
+
+void launch_rb_unpack(const LevelView& L, int iv, const int* items, int n, const double* recv, hipStream_t st) {
+  if (n == 0) return;
+  const long long work = (long long)n * L.nc * L.nc;
+  k_rb_unpack<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, recv);
 }
 
 void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C, const RBRec* rb,

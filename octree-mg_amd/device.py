@@ -22,6 +22,7 @@ _LP = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 SIGNATURES = {
     "omg_last_error": (C.c_char_p, []),
     "omg_get_unique_id": (_I, [C.c_char_p]),
+    "omg_loopback_unique_id": (_I, [C.c_longlong, C.c_char_p]),
     "omg_ctx_create": (_I, [C.POINTER(_P), _I, _I, _I, C.c_char_p]),
     "omg_ctx_destroy": (_I, [_P]),
     "omg_tree_setup": (_I, [_P, _I, _IP, _IP, _IP, _IP, _IP, _IP, _I, _I, _I, _I, _IP, _DP,
@@ -90,6 +91,14 @@ def check(rc: int):
 def unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     check(lib().omg_get_unique_id(buf))
+    return buf.raw
+
+
+def loopback_unique_id(tag: int) -> bytes:
+    """Id of an in-process loopback group (several ranks, one GPU, one thread
+    per rank): see omg_loopback_unique_id in include/omg.h."""
+    buf = C.create_string_buffer(128)
+    check(lib().omg_loopback_unique_id(int(tag), buf))
     return buf.raw
 
 

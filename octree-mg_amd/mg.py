@@ -122,9 +122,22 @@ class MG(MGTree):
 # ---------------------------------------------------------------------------
 # The public procedures (names as in the reference's m_octree_mg)
 
+class Loopback:
+    """Communicator of an in-process loopback group: n_ranks MG objects of one
+    process, one host thread each, sharing a GPU (include/omg.h,
+    omg_loopback_unique_id).  Used to run the multi-rank path on one GPU."""
+
+    def __init__(self, tag: int, rank: int, n_ranks: int):
+        self.tag, self.rank, self.n_ranks = int(tag), int(rank), int(n_ranks)
+
+
 def mg_comm_init(mg: MG, comm=None):
     """mg_comm_init (reference: src/m_communication.f90:14-35).  Ranks come
-    from torch.distributed when it is initialised, else a single rank."""
+    from torch.distributed when it is initialised (or from a Loopback
+    communicator), else a single rank."""
+    if isinstance(comm, Loopback):
+        mg.comm, mg.my_rank, mg.n_cpu = comm, comm.rank, comm.n_ranks
+        return
     try:
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized():
@@ -218,7 +231,10 @@ def mg_allocate_storage(mg: MG, device_index=None):
     if device_index is None:
         device_index = int(os.environ.get("LOCAL_RANK", mg.device_index if mg.n_cpu == 1 else 0))
     uid = None
-    if mg.n_cpu > 1:
+    if isinstance(mg.comm, Loopback):
+        uid = device.loopback_unique_id(mg.comm.tag) if mg.comm.n_ranks > 1 else None
+        device_index = 0
+    elif mg.n_cpu > 1:
         import torch.distributed as dist
         obj = [device.unique_id() if mg.my_rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)

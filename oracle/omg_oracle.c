@@ -686,9 +686,10 @@ static double get_sum_rank(orc_mg *mg, int iv, int r) {
     return s;
 }
 
-/* MPI_Allreduce(sum) of one double over a power-of-two communicator is a
- * recursive-doubling pairwise tree in rank order (MPICH 3.3.2 small-message
- * path); for 1 rank it is the value itself. */
+/* MPI_Allreduce(sum) of one double over n ranks is a
+ * binomial tree in rank order, ((a0+a1)+(a2+a3))+a4 ...: MPICH 3.3.2 on one node
+ * reduces to rank 0 along a binomial tree before the broadcast (pinned by the
+ * golden runs at 1-6 and 8 ranks); for 1 rank it is the value itself. */
 static double allreduce_sum(const double *v, int n) {
     double *t = malloc(sizeof(double) * n);
     memcpy(t, v, sizeof(double) * n);

@@ -35,17 +35,19 @@ CONFIGS = {
     "odd48_gsrb": ("8 48 48 48 4 v gsrb lpl 0 d0 sol 1 lb 0", True, [1]),
     "odd48_gs": ("8 48 48 48 4 v gs lpl 0 d0 sol 1 lb 0", True, [1]),
     # C3-like periodic GSRB (subtract_mean), rank counts pin the allreduce order
-    "per32_gsrb_v": ("8 32 32 32 10 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
+    "per32_gsrb_v": ("8 32 32 32 10 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 3, 4, 5, 6, 8]),
     "per32_gs_f": ("8 32 32 32 5 f gs lpl 0 per sol 1 lb 1", True, [1]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1]),
     "helm32_gs_c0": ("8 32 32 32 5 v gs helm 10 c0 sol 1 lb 0", True, [1]),
     # C4-like: tests/test_refinement (centre-refined AMR tree)
-    "ref2_gs_v": ("8 32 32 32 6 v gs lpl 0 sol sol 2 lb 0", True, [1, 4]),
-    "ref3_gs_f": ("8 32 32 32 5 f gs lpl 0 sol sol 3 lb 1", True, [1]),
-    "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1]),
-    "c4_ref2_box16": ("16 128 128 128 4 v gs lpl 0 sol sol 2 lb 0", False, [1]),
+    # ranks 3 put refinement boundaries across ranks (power-of-two rank counts
+    # cut these trees along the octree and never do)
+    "ref2_gs_v": ("8 32 32 32 6 v gs lpl 0 sol sol 2 lb 0", True, [1, 3, 4]),
+    "ref3_gs_f": ("8 32 32 32 5 f gs lpl 0 sol sol 3 lb 1", True, [1, 3]),
+    "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1, 3]),
+    "c4_ref2_box16": ("16 128 128 128 4 v gs lpl 0 sol sol 2 lb 0", False, [1, 3, 4]),
 }
 
 

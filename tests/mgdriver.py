@@ -127,7 +127,7 @@ class OracleBackend:
 
 
 class DeviceBackend:
-    def __init__(self, cfg, n_ranks=1, my_rank=0):
+    def __init__(self, cfg, comm=None):
         self.cfg = cfg
         mg = omg.MG()
         mg.n_extra_vars = 1
@@ -135,7 +135,7 @@ class DeviceBackend:
         mg.helmholtz_lambda = cfg["lam"]
         mg.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
         omg.mg_set_methods(mg)
-        omg.mg_comm_init(mg)
+        omg.mg_comm_init(mg, comm)
         build_tree(cfg, mg, mg.n_cpu, mg.my_rank)
         omg.mg_set_methods(mg)
 
@@ -259,15 +259,7 @@ def phi_digest(be):
     return h.hexdigest()
 
 
-def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None):
-    """Run one omg_golden configuration; returns {'history': [...], 'phi_sha256'}.
-
-    reduce(err, res) -> (err, res) combines per-rank maxima for multi-rank runs."""
-    cfg = parse(args)
-    if n_its is not None:
-        cfg["n_its"] = n_its
-    be = OracleBackend(cfg, n_ranks) if backend == "oracle" else DeviceBackend(cfg)
-    setup_problem(be)
+def _cycles(be, cfg, reduce=None):
     hist = []
 
     def record(it, mres):
@@ -283,4 +275,66 @@ def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None)
         else:
             m = be.vcycle(cfg["maxres"])
         record(n, m if cfg["maxres"] else 0.0)
+    return hist
+
+
+def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None):
+    """Run one omg_golden configuration; returns {'history': [...], 'phi_sha256'}.
+
+    reduce(err, res) -> (err, res) combines per-rank maxima for multi-rank runs."""
+    cfg = parse(args)
+    if n_its is not None:
+        cfg["n_its"] = n_its
+    be = OracleBackend(cfg, n_ranks) if backend == "oracle" else DeviceBackend(cfg)
+    setup_problem(be)
+    hist = _cycles(be, cfg, reduce)
     return {"history": hist, "phi_sha256": phi_digest(be), "backend": be}
+
+
+def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600):
+    """The same configuration on n_ranks device contexts of this process (one
+    thread per rank, all on GPU 0), exchanging through the loopback transport
+    (omg_loopback_unique_id): the multi-rank path of libomg.so (plans, packing,
+    MPICH-order reductions) on a single GPU.  Returns the history with err /
+    res reduced by max over ranks, as omg_golden's MPI_Reduce(MAX)."""
+    import threading
+    cfg = parse(args)
+    if n_its is not None:
+        cfg["n_its"] = n_its
+    tag = int.from_bytes(os.urandom(6), "little")
+    bar = threading.Barrier(n_ranks)
+    slots = [None] * n_ranks
+    out = [None] * n_ranks
+    errors = []
+
+    def worker(rank):
+        def reduce(e, r):
+            slots[rank] = (e, r)
+            bar.wait()
+            E = max(x[0] for x in slots)
+            R = max(x[1] for x in slots)
+            bar.wait()
+            return E, R
+        try:
+            be = DeviceBackend(cfg, omg.Loopback(tag, rank, n_ranks))
+            setup_problem(be)
+            out[rank] = _cycles(be, cfg, reduce)
+            be.mg.ctx.call("synchronize")
+            omg.mg_deallocate_storage(be.mg)
+        except BaseException as ex:  # noqa: BLE001  (re-raised in the caller)
+            errors.append((rank, ex))
+            bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n_ranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    if errors:
+        msg = "; ".join(f"rank {r}: {type(e).__name__}: {e}" for r, e in sorted(errors, key=lambda x: x[0])
+                        if not isinstance(e, threading.BrokenBarrierError))
+        raise RuntimeError(msg or str(errors[0][1]))
+    if any(t.is_alive() for t in th):
+        raise TimeoutError("loopback run did not finish")
+    assert all(h == out[0] for h in out)
+    return {"history": out[0]}
