@@ -34,6 +34,7 @@ extern "C" {
 typedef struct omg_ctx omg_ctx;
 
 #define OMG_UNIQUE_ID_BYTES 128
+#define OMG_DEVICE_NONE (-2)
 
 /* Operators / smoothers / bc codes: same values as the reference
  * (src/m_data_structures.f90:14-37, 73-79). */
@@ -55,7 +56,9 @@ int omg_get_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
 int omg_loopback_unique_id(long long tag, void *out /* OMG_UNIQUE_ID_BYTES */);
 
 /* Create a context on HIP device `device` (device < 0: rank modulo the number
- * of visible devices) for rank `rank` of `n_ranks`.  unique_id may be NULL
+ * of visible devices; OMG_DEVICE_NONE: a plan-only context that builds the
+ * host tables of omg_tree_setup and touches no device, for inspecting the
+ * communication plans with omg_plan_transfer) for rank `rank` of `n_ranks`.  unique_id may be NULL
  * when n_ranks == 1.  Replaces the device side of mg_comm_init
  * (src/m_communication.f90:14-35). */
 int omg_ctx_create(omg_ctx **ctx, int device, int rank, int n_ranks, const void *unique_id);
@@ -119,6 +122,15 @@ int omg_max_residual_lvl(omg_ctx *ctx, int lvl, double *out);    /* max_residual
 int omg_get_sum(omg_ctx *ctx, int iv, double *out);              /* get_sum + allreduce */
 int omg_subtract_mean(omg_ctx *ctx, int iv, int include_ghostcells); /* subtract_mean */
 int omg_phi_bc_store(omg_ctx *ctx);                              /* mg_phi_bc_store */
+
+/* The communication plan of level lvl as built by omg_tree_setup: transfer
+ * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,
+ * 3 refinement-boundary faces), direction dir (0 send, 1 receive); fills
+ * min(cap, n) (peer, key) pairs in wire order.  Keys are the ordering keys of
+ * sort_and_transfer_buffers (src/m_communication.f90:37-66): 6*id+nb for
+ * faces, 8*parent+child slot for restriction, child id for prolongation. */
+int omg_plan_transfer(omg_ctx *ctx, int lvl, int which, int dir, int cap, int *peers,
+                      long long *keys, int *n_items, int *item_doubles);
 
 /* Stream / timing helpers for benchmarks. */
 int omg_synchronize(omg_ctx *ctx);

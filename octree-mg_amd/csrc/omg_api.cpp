@@ -60,9 +60,21 @@ int guarded(F&& f) {
   }
 }
 
+// Plan-only contexts (omg_ctx_create with OMG_DEVICE_NONE) build every host
+// table of omg_tree_setup but allocate nothing on a device.
+thread_local bool g_host_only = false;
+
+template <typename T>
+void dmalloc(T** p, size_t bytes, bool zero = false) {
+  *p = nullptr;
+  if (g_host_only || bytes == 0) return;
+  HIPCHK(hipMalloc((void**)p, bytes));
+  if (zero) HIPCHK(hipMemset(*p, 0, bytes));
+}
+
 template <typename T>
 T* to_device(const std::vector<T>& v) {
-  if (v.empty()) return nullptr;
+  if (v.empty() || g_host_only) return nullptr;
   T* d = nullptr;
   HIPCHK(hipMalloc(&d, sizeof(T) * v.size()));
   HIPCHK(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
@@ -151,6 +163,7 @@ std::vector<PeerList> group(std::vector<Rec>& recs, int ints_per_item) {
       out.push_back(PeerList());
       out.back().peer = r.peer;
     }
+    out.back().keys.push_back(r.key);
     out.back().items.push_back(r.a);
     if (ints_per_item >= 2) out.back().items.push_back(r.b);
     if (ints_per_item >= 3) out.back().items.push_back(r.c);
@@ -748,8 +761,7 @@ void build_plan(omg_ctx* c) {
     // arena
     if (L.n) {
       const size_t bytes = sizeof(double) * (size_t)c->n_vars * L.n * L.stride;
-      HIPCHK(hipMalloc(&L.d_data, bytes));
-      HIPCHK(hipMemset(L.d_data, 0, bytes));
+      dmalloc(&L.d_data, bytes, true);
     }
     // neighbour table + halo receive plan
     L.h_nbk.assign((size_t)L.n * 6, NB_LOCAL);
@@ -852,7 +864,7 @@ void build_plan(omg_ctx* c) {
       if (T.rank(id) == me) L.leaves.push_back(c->local_index[id]);
     L.d_parents = to_device(L.parents);
     L.d_leaves = to_device(L.leaves);
-    if (!L.leaves.empty()) HIPCHK(hipMalloc(&L.d_scratch, sizeof(double) * L.leaves.size()));
+    dmalloc(&L.d_scratch, sizeof(double) * L.leaves.size());
   }
   // grid transfers between lvl-1 (coarse) and lvl (fine)
   for (int l = c->lowest + 1; l <= c->highest; l++) {
@@ -926,12 +938,10 @@ void build_plan(omg_ctx* c) {
       Level& L = c->levels[l];
       L.sendbuf_doubles = sendn[l];
       L.recvbuf_doubles = recvn[l];
-      if (sendn[l]) HIPCHK(hipMalloc(&L.d_sendbuf, sizeof(double) * sendn[l]));
-      if (recvn[l]) HIPCHK(hipMalloc(&L.d_recvbuf, sizeof(double) * recvn[l]));
-      if (L.rbx.n_send)
-        HIPCHK(hipMalloc(&L.d_rbsend, sizeof(double) * (size_t)L.rbx.n_send * L.rbx.item_doubles));
-      if (L.rbx.n_recv)
-        HIPCHK(hipMalloc(&L.d_rbrecv, sizeof(double) * (size_t)L.rbx.n_recv * L.rbx.item_doubles));
+      dmalloc(&L.d_sendbuf, sizeof(double) * sendn[l]);
+      dmalloc(&L.d_recvbuf, sizeof(double) * recvn[l]);
+      dmalloc(&L.d_rbsend, sizeof(double) * (size_t)L.rbx.n_send * L.rbx.item_doubles);
+      dmalloc(&L.d_rbrecv, sizeof(double) * (size_t)L.rbx.n_recv * L.rbx.item_doubles);
     }
   }
 }
@@ -963,7 +973,17 @@ int omg_loopback_unique_id(long long tag, void* out) {
 int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void* unique_id) {
   return guarded([&] {
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw OmgError("bad rank / n_ranks");
-    if (n_ranks > 1 && !unique_id) throw OmgError("unique_id required for n_ranks > 1");
+    if (n_ranks > 1 && !unique_id && device != OMG_DEVICE_NONE)
+      throw OmgError("unique_id required for n_ranks > 1");
+    if (device == OMG_DEVICE_NONE) {   // plan-only context: no HIP, no RCCL
+      omg_ctx* c = new omg_ctx();
+      c->device = device;
+      c->rank = rank;
+      c->n_ranks = n_ranks;
+      c->host_only = true;
+      *out = c;
+      return;
+    }
     if (device < 0) {   // one rank per GPU: rank modulo the visible devices
       int n_dev = 0;
       HIPCHK(hipGetDeviceCount(&n_dev));
@@ -1008,6 +1028,13 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
 int omg_ctx_destroy(omg_ctx* c) {
   return guarded([&] {
     if (!c) return;
+    if (c->host_only) {
+      g_host_only = true;
+      free_levels(c);
+      g_host_only = false;
+      delete c;
+      return;
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     free_levels(c);
@@ -1035,7 +1062,11 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
                    const double* dr, const int* list_off, const int* lists, int n_vars) {
   return guarded([&] {
     if (n_vars < 4 || n_vars > kMaxVars) throw OmgError("n_vars out of range");
-    (void)hipSetDevice(c->device);
+    struct HostOnly {
+      explicit HostOnly(bool on) { g_host_only = on; }
+      ~HostOnly() { g_host_only = false; }
+    } host_only_scope(c->host_only);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     free_levels(c);
     c->n_boxes = n_boxes;
     c->lvl.assign(lvl, lvl + n_boxes);
@@ -1063,7 +1094,29 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
       }
     }
     build_plan(c);
-    HIPCHK(hipDeviceSynchronize());
+    if (!c->host_only) HIPCHK(hipDeviceSynchronize());
+  });
+}
+
+int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* peers, long long* keys,
+                      int* n_items, int* item_doubles) {
+  return guarded([&] {
+    Level* L = level_ptr(c, lvl);
+    if (!L) throw OmgError("no such level");
+    if (which < 0 || which > 3) throw OmgError("omg_plan_transfer: bad transfer");
+    const Transfer* T[4] = {&L->halo, &L->restr, &L->prol, &L->rbx};
+    const auto& lists = dir ? T[which]->recv : T[which]->send;
+    int n = 0;
+    for (auto& p : lists)
+      for (long long k : p.keys) {
+        if (n < cap) {
+          peers[n] = p.peer;
+          keys[n] = k;
+        }
+        n++;
+      }
+    *n_items = n;
+    *item_doubles = T[which]->item_doubles;
   });
 }
 

@@ -68,6 +68,7 @@ struct RBRec {             // refinement boundary: coarse neighbour + child offs
 
 struct PeerList {          // one peer's part of a transfer, in wire order
   int peer;
+  std::vector<long long> keys;   // ordering keys (sort_and_transfer_buffers' ix)
   std::vector<int> items;  // meaning depends on the transfer type
   int offset = 0;          // first item in the device list / buffer
 };
@@ -167,6 +168,7 @@ struct omg_loop;   // in-process loopback transport (omg_api.cpp)
 
 struct omg_ctx {
   int device = 0, rank = 0, n_ranks = 1;
+  bool host_only = false;                   // plan-only context (OMG_DEVICE_NONE)
   hipStream_t stream = nullptr;
   void* nccl = nullptr;  // ncclComm_t
   std::shared_ptr<omg_loop> loop;           // set instead of nccl in loopback mode

@@ -23,6 +23,8 @@ SIGNATURES = {
     "omg_last_error": (C.c_char_p, []),
     "omg_get_unique_id": (_I, [C.c_char_p]),
     "omg_loopback_unique_id": (_I, [C.c_longlong, C.c_char_p]),
+    "omg_plan_transfer": (_I, [_P, _I, _I, _I, _I, _IP, C.POINTER(C.c_longlong), C.POINTER(_I),
+                               C.POINTER(_I)]),
     "omg_ctx_create": (_I, [C.POINTER(_P), _I, _I, _I, C.c_char_p]),
     "omg_ctx_destroy": (_I, [_P]),
     "omg_tree_setup": (_I, [_P, _I, _IP, _IP, _IP, _IP, _IP, _IP, _I, _I, _I, _I, _IP, _DP,
@@ -124,6 +126,18 @@ class Context:
 
     def call(self, name, *args):
         check(getattr(self.L, "omg_" + name)(self.h, *args))
+
+    def plan_transfer(self, lvl, which, direction):
+        """[(peer, key), ...] in wire order and the doubles per item of one
+        transfer of the communication plan (omg_plan_transfer)."""
+        n, per = _I(), _I()
+        self.call("plan_transfer", lvl, which, direction, 0, np.zeros(1, np.int32),
+                  np.zeros(1, np.int64).ctypes.data_as(C.POINTER(C.c_longlong)), C.byref(n), C.byref(per))
+        peers = np.zeros(max(n.value, 1), np.int32)
+        keys = np.zeros(max(n.value, 1), np.int64)
+        self.call("plan_transfer", lvl, which, direction, n.value, peers,
+                  keys.ctypes.data_as(C.POINTER(C.c_longlong)), C.byref(n), C.byref(per))
+        return [(int(p), int(k)) for p, k in zip(peers[:n.value], keys[:n.value])], per.value
 
     def stream(self) -> int:
         return self.L.omg_stream(self.h) or 0

@@ -1,0 +1,135 @@
+"""Multi-rank communication plans on CPU: world_size 2 and 3 gloo process
+groups, each rank building its own plan-only context (OMG_DEVICE_NONE) of
+libomg.so from its own copy of the tree, exactly as mg_allocate_storage does on
+a GPU rank.  The plans are exchanged over gloo and checked pairwise:
+
+* what rank a sends to rank b in a transfer (ghost faces, restriction,
+  prolongation, refinement-boundary faces) is, key for key and in wire order,
+  what b expects from a — the property sort_and_transfer_buffers relies on
+  (src/m_communication.f90:37-66);
+* every face of a box whose neighbour lives on another rank is received
+  exactly once (6*id+nb), and every refinement-boundary face whose coarse
+  neighbour lives elsewhere arrives in the refinement-boundary transfer.
+
+The data path over those plans is checked bit for bit against the reference
+at 2-8 ranks on the GPU (tests/test_gpu_multirank.py)."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.mgdriver import T, build_tree, omg, parse
+
+CASES = [
+    ("8 32 32 32 1 v gsrb lpl 0 per sol 1 lb 0", 2),     # periodic halo
+    ("8 64 32 32 1 v gs lpl 0 d0 sol 1 lbp 0", 2),       # non-cube, parents balanced
+    ("8 32 32 32 1 v gs lpl 0 sol sol 3 lb 0", 2),       # 3-level refined tree
+    ("8 32 32 32 1 v gs lpl 0 sol sol 2 lb 0", 3),       # refinement boundaries across ranks
+    ("8 32 32 32 1 v gsrb lpl 0 d0 sol 3 lb 0", 3),
+]
+WHICH = {0: "halo", 1: "restrict", 2: "prolong", 3: "refinement-boundary"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _plans(args, rank, world):
+    cfg = parse(args)
+    tree = build_tree(cfg, T.MGTree(), world, rank)
+    ctx = omg.device.Context(-2, rank, world)   # OMG_DEVICE_NONE
+    arrs = omg.mg._tree_arrays(tree)
+    ctx.call("tree_setup", tree.n_boxes, *arrs[:6], tree.lowest_lvl, tree.highest_lvl,
+             tree.first_normal_lvl, tree.box_size, arrs[6], arrs[7], arrs[8], arrs[9], 5)
+    out = {}
+    for lvl in range(tree.lowest_lvl, tree.highest_lvl + 1):
+        for w in WHICH:
+            for d in (0, 1):
+                out[(lvl, w, d)] = ctx.plan_transfer(lvl, w, d)
+    ctx.close()
+    return out
+
+
+def _expected_remote(args, rank, world):
+    """Faces of my boxes that need data from another rank, from the tree alone."""
+    cfg = parse(args)
+    t = build_tree(cfg, T.MGTree(), world, rank)
+    halo, rb = {}, {}
+    for lvl in range(t.lowest_lvl, t.highest_lvl + 1):
+        h, r = set(), set()
+        for id_ in t.lvls[lvl].ids:
+            if t.rank[id_] != rank:
+                continue
+            for nb in range(1, 7):
+                nid = t.neighbors[id_][nb - 1]
+                if nid > 0 and t.rank[nid] != rank:
+                    h.add(6 * int(id_) + nb)
+                elif nid == 0:
+                    pn = t.neighbors[t.parent[id_]][nb - 1]
+                    if t.rank[pn] != rank:
+                        r.add(6 * int(id_) + nb)
+        halo[lvl], rb[lvl] = h, r
+    return halo, rb
+
+
+def _worker(rank, world, port, args, q):
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        mine = _plans(args, rank, world)
+        allp = [None] * world
+        dist.all_gather_object(allp, mine)
+        problems = []
+        for (lvl, w, d), (items, per) in mine.items():
+            if d != 0:
+                continue
+            for b in range(world):
+                if b == rank:
+                    if any(p == rank for p, _ in items):
+                        problems.append(f"lvl {lvl} {WHICH[w]}: send to self")
+                    continue
+                sent = [k for p, k in items if p == b]
+                got, per_b = allp[b][(lvl, w, 1)]
+                expected = [k for p, k in got if p == rank]
+                if sent != expected:
+                    problems.append(f"lvl {lvl} {WHICH[w]}: {rank}->{b} sends {len(sent)} keys, "
+                                    f"{b} expects {len(expected)}")
+                if sent and per != per_b:
+                    problems.append(f"lvl {lvl} {WHICH[w]}: item size {per} vs {per_b}")
+        halo, rb = _expected_remote(args, rank, world)
+        for lvl in halo:
+            got_h = [k for _, k in mine[(lvl, 0, 1)][0]]
+            got_r = [k for _, k in mine[(lvl, 3, 1)][0]]
+            if sorted(got_h) != sorted(halo[lvl]) or len(set(got_h)) != len(got_h):
+                problems.append(f"lvl {lvl}: halo receives {len(got_h)} faces, tree needs {len(halo[lvl])}")
+            if sorted(got_r) != sorted(rb[lvl]):
+                problems.append(f"lvl {lvl}: rb receives {len(got_r)} faces, tree needs {len(rb[lvl])}")
+        n_rb = sum(len(v) for v in rb.values())
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, problems, n_rb))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, [f"{type(e).__name__}: {e}"], 0))
+
+
+@pytest.mark.parametrize("args,world", CASES)
+def test_plans_pair_up_across_ranks(args, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(60)
+    problems = [f"rank {r}: {m}" for r, ms, _ in res for m in ms]
+    assert not problems, "\n".join(problems)
+    if world == 3 and " 2 lb" in args:
+        assert sum(n for _, _, n in res) > 0, "case meant to cross refinement boundaries has none"
