@@ -24,11 +24,13 @@
 
 namespace omg {
 
-template <int NC, int OP>
-__global__ void __launch_bounds__(256) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
-                                                   double* __restrict__ sendbuf) {
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+template <int NC, int OP, int BS, int NT>
+__global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
+                                                  double* __restrict__ sendbuf) {
   constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
-  constexpr int NP2 = (HV / 2 + 255) / 256;    // double2 cell pairs per thread
+  constexpr int NP2 = (HV / 2 + BS - 1) / BS;  // double2 cell pairs per thread
   __shared__ double so[HV];                    // colour 1-e of the interior
   __shared__ double se[HV];                    // colour e, updated
   __shared__ double sg[6 * FH];                // colour 1-e halves of the ghost faces
@@ -40,52 +42,99 @@ __global__ void __launch_bounds__(256) k_gsrb_tile(LevelView L, double lambda, i
 
   // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
   {
-    const double2* src = reinterpret_cast<const double2*>(u + o * HV);
-    double2* dst = reinterpret_cast<double2*>(so);
-    for (int q = tid; q < HV / 2; q += 256) dst[q] = src[q];
-    for (int q = tid; q < 3 * FH; q += 256) {   // 6 faces x FH/2 double2
+    const v2d* src = reinterpret_cast<const v2d*>(u + o * HV);
+    v2d* dst = reinterpret_cast<v2d*>(so);
+    for (int q = tid; q < HV / 2; q += BS) dst[q] = NT >= 2 ? __builtin_nontemporal_load(src + q) : src[q];
+    for (int q = tid; q < 3 * FH; q += BS) {   // 6 faces x FH/2 double2
       const int nb = q / (FH / 2), r = q % (FH / 2);
-      reinterpret_cast<double2*>(sg + nb * FH)[r] =
-          reinterpret_cast<const double2*>(u + 2 * HV + nb * FS + o * FH)[r];
+      const v2d* gp = reinterpret_cast<const v2d*>(u + 2 * HV + nb * FS + o * FH) + r;
+      reinterpret_cast<v2d*>(sg + nb * FH)[r] = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
     }
   }
   double2 fr[NP2];
 #pragma unroll
   for (int r = 0; r < NP2; r++) {
-    const int q2 = tid + 256 * r;
-    if (q2 < HV / 2) fr[r] = reinterpret_cast<const double2*>(f + e * HV)[q2];
+    const int q2 = tid + BS * r;
+    if (q2 < HV / 2) {
+      const double2* fp = reinterpret_cast<const double2*>(f + e * HV) + q2;
+      if (NT) {
+        const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(fp));
+        fr[r] = make_double2(t.x, t.y);
+      } else {
+        fr[r] = *fp;
+      }
+    }
   }
   __syncthreads();
 
   // ---- colour e update ----------------------------------------------------
+  // Each thread updates two neighbouring cells of one row (colour indices ih,
+  // ih+1 with ih even; NC >= 4).  Their y/z neighbours are aligned
+  // colour-(1-e) pairs and their x neighbours one aligned pair plus one single
+  // value: five 16-B and one 8-B LDS read per two cells, the lanes of a wave
+  // on consecutive 16-B slots.
 #pragma unroll
   for (int r = 0; r < NP2; r++) {
-    const int q2 = tid + 256 * r;
+    const int q2 = tid + BS * r;
     if (q2 >= HV / 2) continue;
-    double nv[2];
+    double2 nv;
+    if constexpr (H % 2 == 0) {
+      const int q = 2 * q2, ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+      const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
+      const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
+      const int xgi = ((j - 1) >> 1) + H * (k - 1);   // x ghosts of this row
+      const double* xs_ptr = p ? (ih + 2 == H ? sg + FH + xgi : so + ih + 2 + H * row)
+                               : (ih == 0 ? sg + xgi : so + ih - 1 + H * row);
+      const double xs = *xs_ptr;
+      const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
+                                                               : sg + 2 * FH + ih + H * (k - 1));
+      const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
+                                                                : sg + 3 * FH + ih + H * (k - 1));
+      const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
+                                                               : sg + 4 * FH + ih + H * (j - 1));
+      const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
+                                                                : sg + 5 * FH + ih + H * (j - 1));
+      Nbr7 s0, s1;
+      s0.xm = p ? xc.x : xs;
+      s0.xp = p ? xc.y : xc.x;
+      s1.xm = p ? xc.y : xc.x;
+      s1.xp = p ? xs : xc.y;
+      s0.ym = ym.x; s1.ym = ym.y;
+      s0.yp = yp.x; s1.yp = yp.y;
+      s0.zm = zm.x; s1.zm = zm.y;
+      s0.zp = zp.x; s1.zp = zp.y;
+      nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));
+    } else {   // NC == 2: one cell per row
+      double v[2];
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const int q = 2 * q2 + s;
-      const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
-      const int i = 2 * ih + 1 + ((1 + j + k + e) & 1);
-      const int tj = (i - 1) >> 1;                      // colour-1-e index of (i, j, k)
-      Nbr7 st;
-      st.xm = i > 1 ? so[((i - 2) >> 1) + H * row] : sg[0 * FH + ((j - 1) >> 1) + H * (k - 1)];
-      st.xp = i < NC ? so[(i >> 1) + H * row] : sg[1 * FH + ((j - 1) >> 1) + H * (k - 1)];
-      st.ym = j > 1 ? so[tj + H * (row - 1)] : sg[2 * FH + tj + H * (k - 1)];
-      st.yp = j < NC ? so[tj + H * (row + 1)] : sg[3 * FH + tj + H * (k - 1)];
-      st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
-      st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
-      const double fv = s ? fr[r].y : fr[r].x;
-      nv[s] = gs_value<OP>(K, st, fv);
-      se[q] = nv[s];
+      for (int s = 0; s < 2; s++) {
+        const int q = 2 * q2 + s;
+        const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+        const int i = 2 * ih + 1 + ((1 + j + k + e) & 1);
+        const int tj = (i - 1) >> 1;
+        Nbr7 st;
+        st.xm = i > 1 ? so[((i - 2) >> 1) + H * row] : sg[0 * FH + ((j - 1) >> 1) + H * (k - 1)];
+        st.xp = i < NC ? so[(i >> 1) + H * row] : sg[1 * FH + ((j - 1) >> 1) + H * (k - 1)];
+        st.ym = j > 1 ? so[tj + H * (row - 1)] : sg[2 * FH + tj + H * (k - 1)];
+        st.yp = j < NC ? so[tj + H * (row + 1)] : sg[3 * FH + tj + H * (k - 1)];
+        st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
+        st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
+        v[s] = gs_value<OP>(K, st, s ? fr[r].y : fr[r].x);
+      }
+      nv = make_double2(v[0], v[1]);
     }
-    reinterpret_cast<double2*>(u + e * HV)[q2] = make_double2(nv[0], nv[1]);
+    reinterpret_cast<double2*>(se)[q2] = nv;
+    double2* up = reinterpret_cast<double2*>(u + e * HV) + q2;
+    if (NT) {
+      v2d t = {nv.x, nv.y};
+      __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(up));
+    } else
+      *up = nv;
   }
   __syncthreads();
 
   // ---- ghost fill after the substep ---------------------------------------
-  for (int p = tid; p < 6 * NC * NC; p += 256) {
+  for (int p = tid; p < 6 * NC * NC; p += BS) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
     const int a = cell % NC + 1, c = cell / NC + 1;
     const long long fidx = (long long)b * 6 + nb - 1;
@@ -102,8 +151,13 @@ __global__ void __launch_bounds__(256) k_gsrb_tile(LevelView L, double lambda, i
     const int idx1 = ((i1 - 1) >> 1) + H * ((j1 - 1) + NC * (k1 - 1));
     const double v1 = c1 == e ? se[idx1] : so[idx1];
     if (kind == NB_LOCAL) {
-      if ((colours >> c1) & 1)
-        L.phi[(long long)arg * L.stride + off_gh(L, low ? nb + 1 : nb - 1, a, c)] = v1;
+      if ((colours >> c1) & 1) {
+        double* gp = L.phi + (long long)arg * L.stride + off_gh(L, low ? nb + 1 : nb - 1, a, c);
+        if (NT >= 2)
+          __builtin_nontemporal_store(v1, gp);
+        else
+          *gp = v1;
+      }
     } else if (kind == NB_REMOTE) {
       sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
     } else {  // NB_PHYS (refinement boundaries take the generic kernel)
@@ -127,17 +181,21 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   }
   GcBC b2 = bc;
   b2.phi_stored = bc.phi_stored;  // iv == 1 here
-  const dim3 g(L.n), blk(256);
-#define OMG_TILE(NC)                                                                          \
-  if (op == OP_HELM)                                                                          \
-    k_gsrb_tile<NC, OP_HELM><<<g, blk, 0, st>>>(L, lambda, e, colours, b2, sendbuf);          \
-  else                                                                                        \
-    k_gsrb_tile<NC, OP_LPL><<<g, blk, 0, st>>>(L, lambda, e, colours, b2, sendbuf);
+  // 16^3 boxes: 8 waves per box (4 boxes = 32 waves per CU, the LDS of 4
+  // boxes fits); streaming loads/stores are non-temporal: nothing a substep
+  // reads or writes is touched again before the next substep has swept the
+  // level, far beyond L2 / MALL at the sizes that matter.
+  const dim3 g(L.n);
+#define OMG_TILE(NC, BS)                                                                   \
+  if (op == OP_HELM)                                                                       \
+    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf); \
+  else                                                                                     \
+    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf);
   switch (L.nc) {
-    case 16: OMG_TILE(16) break;
-    case 8: OMG_TILE(8) break;
-    case 4: OMG_TILE(4) break;
-    default: OMG_TILE(2) break;
+    case 16: OMG_TILE(16, 512) break;
+    case 8: OMG_TILE(8, 256) break;
+    case 4: OMG_TILE(4, 256) break;
+    default: OMG_TILE(2, 256) break;
   }
 #undef OMG_TILE
 }

@@ -15,55 +15,100 @@
 
 namespace omg {
 
-template <int NC, int OP>
-__global__ void __launch_bounds__(256) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
-                                                        unsigned long long* maxbits, int restrict_on,
-                                                        const int* parent_local, const int* dixp) {
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2d ld_nt(const double* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+}
+__device__ __forceinline__ void st_nt(double* p, double x, double y) {
+  v2d t = {x, y};
+  __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(p));
+}
+
+// The seven stencil values of two neighbouring same-colour cells of one row
+// (colour indices ih, ih+1, ih even) of colour e, from a stored box in LDS:
+// `so` = the other colour's interior, `gb` = the other colour's half of ghost
+// face 1, consecutive faces `fstride` apart.  Five 16-B and one 8-B LDS read.
+template <int NC>
+__device__ __forceinline__ void pair_stencil(const double* so, const double* gb, int fstride, int e, int q,
+                                             Nbr7& s0, Nbr7& s1) {
+  constexpr int H = NC / 2;
+  const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+  const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
+  const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
+  const int xgi = ((j - 1) >> 1) + H * (k - 1);
+  const double xs = *(p ? (ih + 2 == H ? gb + fstride + xgi : so + ih + 2 + H * row)
+                        : (ih == 0 ? gb + xgi : so + ih - 1 + H * row));
+  const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
+                                                           : gb + 2 * fstride + ih + H * (k - 1));
+  const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
+                                                            : gb + 3 * fstride + ih + H * (k - 1));
+  const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
+                                                           : gb + 4 * fstride + ih + H * (j - 1));
+  const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
+                                                            : gb + 5 * fstride + ih + H * (j - 1));
+  s0.xm = p ? xc.x : xs;
+  s0.xp = p ? xc.y : xc.x;
+  s1.xm = p ? xc.y : xc.x;
+  s1.xp = p ? xs : xc.y;
+  s0.ym = ym.x; s1.ym = ym.y;
+  s0.yp = yp.x; s1.yp = yp.y;
+  s0.zm = zm.x; s1.zm = zm.y;
+  s0.zp = zp.x; s1.zp = zp.y;
+}
+
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
+                                                       unsigned long long* maxbits, int restrict_on,
+                                                       const int* parent_local, const int* dixp) {
   using TL = Tl<NC>;
-  constexpr int NST = TL::NST, HV = TL::HV, NR = (HV + 255) / 256, HN = NC / 2;
+  constexpr int NST = TL::NST, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, HN = NC / 2;
   __shared__ double sb[NST];
   const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
   const long long boff = (long long)b * F.stride;
   const double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
   double* __restrict__ res = F.data + 3 * F.vstride + boff;
-  for (int q = tid; q < NST / 2; q += 256)
-    reinterpret_cast<double2*>(sb)[q] = reinterpret_cast<const double2*>(u)[q];
-  double2 fr[NR];
+  for (int q = tid; q < NST / 2; q += BS) reinterpret_cast<v2d*>(sb)[q] = ld_nt(u + 2 * q);
+  v2d fr[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q2 = tid + 256 * r;
-    if (q2 < HV) fr[r] = reinterpret_cast<const double2*>(f)[q2];
+    const int q2 = tid + BS * r;
+    if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
   }
   __syncthreads();
 
-  // residual_box (m_multigrid.f90:426-436) with box_lpl / box_helmh
+  // residual_box (m_multigrid.f90:426-436) with box_lpl / box_helmh, two
+  // same-colour cells per thread and step (pair q2: colour q2 / (HV/2))
   const OpCoef<OP> K(F, lambda);
   double mx = 0.0;
   double2 rv[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q2 = tid + 256 * r;
+    const int q2 = tid + BS * r;
     if (q2 >= HV) continue;
-    double out[2];
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const int q = 2 * q2 + s;
+    const int e = q2 >= HV / 2, o = 1 - e;
+    Nbr7 s0, s1;
+    if constexpr (HN % 2 == 0) {
+      pair_stencil<NC>(sb + o * HV, sb + 2 * HV + o * FH, FS, e, 2 * q2 - e * HV, s0, s1);
+    } else {   // NC == 2: one cell per row
       int i, j, k;
-      TL::decode(q, i, j, k);
-      Nbr7 st;
-      st.c = sb[q];
-      st.xm = sb[TL::ocell(i - 1, j, k)];
-      st.xp = sb[TL::ocell(i + 1, j, k)];
-      st.ym = sb[TL::ocell(i, j - 1, k)];
-      st.yp = sb[TL::ocell(i, j + 1, k)];
-      st.zm = sb[TL::ocell(i, j, k - 1)];
-      st.zp = sb[TL::ocell(i, j, k + 1)];
-      out[s] = (s ? fr[r].y : fr[r].x) - op_value<OP>(K, st);
-      mx = fmax(mx, fabs(out[s]));
+      TL::decode(2 * q2, i, j, k);
+      s0.xm = sb[TL::ocell(i - 1, j, k)]; s0.xp = sb[TL::ocell(i + 1, j, k)];
+      s0.ym = sb[TL::ocell(i, j - 1, k)]; s0.yp = sb[TL::ocell(i, j + 1, k)];
+      s0.zm = sb[TL::ocell(i, j, k - 1)]; s0.zp = sb[TL::ocell(i, j, k + 1)];
+      TL::decode(2 * q2 + 1, i, j, k);
+      s1.xm = sb[TL::ocell(i - 1, j, k)]; s1.xp = sb[TL::ocell(i + 1, j, k)];
+      s1.ym = sb[TL::ocell(i, j - 1, k)]; s1.yp = sb[TL::ocell(i, j + 1, k)];
+      s1.zm = sb[TL::ocell(i, j, k - 1)]; s1.zp = sb[TL::ocell(i, j, k + 1)];
     }
-    rv[r] = make_double2(out[0], out[1]);
-    reinterpret_cast<double2*>(res)[q2] = rv[r];
+    const double2 cc = reinterpret_cast<const double2*>(sb)[q2];
+    s0.c = cc.x;
+    s1.c = cc.y;
+    const double r0 = fr[r].x - op_value<OP>(K, s0), r1 = fr[r].y - op_value<OP>(K, s1);
+    mx = fmax(mx, fmax(fabs(r0), fabs(r1)));
+    rv[r] = make_double2(r0, r1);
+    st_nt(res + 2 * q2, r0, r1);
   }
   if (maxbits) {
     for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
@@ -78,7 +123,7 @@ __global__ void __launch_bounds__(256) k_resid_restrict(LevelView F, LevelView C
   const long long poff = (long long)pb * Cv.stride;
   for (int pass = 0; pass < 2; pass++) {
     double* __restrict__ dst = pass == 0 ? Cv.phi + poff : Cv.data + 3 * Cv.vstride + poff;
-    for (int q = tid; q < HN * HN * HN; q += 256) {
+    for (int q = tid; q < HN * HN * HN; q += BS) {
       const int i = q % HN + 1, j = (q / HN) % HN + 1, k = q / (HN * HN) + 1;
       double acc = 0.0;
 #pragma unroll
@@ -93,7 +138,7 @@ __global__ void __launch_bounds__(256) k_resid_restrict(LevelView F, LevelView C
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < NR; r++) {
-        const int q2 = tid + 256 * r;
+        const int q2 = tid + BS * r;
         if (q2 < HV) reinterpret_cast<double2*>(sb)[q2] = rv[r];
       }
       __syncthreads();
@@ -101,34 +146,34 @@ __global__ void __launch_bounds__(256) k_resid_restrict(LevelView F, LevelView C
   }
 }
 
-template <int NC>
-__global__ void __launch_bounds__(256) k_prolong_fill(LevelView Cv, LevelView F, int iv,
-                                                      const int* parent_local, const int* dixp, GcBC bc,
-                                                      double* sendbuf) {
+template <int NC, int BS>
+__global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
+                                                     const int* parent_local, const int* dixp, GcBC bc,
+                                                     double* sendbuf) {
   using TL = Tl<NC>;
-  constexpr int HV = TL::HV, NR = (HV + 255) / 256, HN = NC / 2, CB = HN + 2;
+  constexpr int HV = TL::HV, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
   __shared__ double cb[CB * CB * CB];   // the parent's octant + one face layer around it
   __shared__ double sb[2 * HV];         // the corrected fine interior
   const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
   const int pb = parent_local[b], dp = dixp[b];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
   const double* __restrict__ cu = boxp(Cv, iv, pb);
-  for (int q = tid; q < CB * CB * CB; q += 256) {
+  for (int q = tid; q < CB * CB * CB; q += BS) {
     const int p = q % CB, s = (q / CB) % CB, t = q / (CB * CB);
     const int nbnd = (p == 0 || p == CB - 1) + (s == 0 || s == CB - 1) + (t == 0 || t == CB - 1);
     if (nbnd < 2) cb[q] = cu[off_cell(Cv, dx + p, dy + s, dz + t)];
   }
   double* __restrict__ u = F.phi + (long long)b * F.stride;
-  double2 old[NR];
+  v2d old[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q2 = tid + 256 * r;
-    if (q2 < HV) old[r] = reinterpret_cast<const double2*>(u)[q2];
+    const int q2 = tid + BS * r;
+    if (q2 < HV) old[r] = ld_nt(u + 2 * q2);
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q2 = tid + 256 * r;
+    const int q2 = tid + BS * r;
     if (q2 >= HV) continue;
     double nv[2];
 #pragma unroll
@@ -146,7 +191,7 @@ __global__ void __launch_bounds__(256) k_prolong_fill(LevelView Cv, LevelView F,
       nv[s] = o + (f0 + fx + fy + fz);
       sb[q] = nv[s];
     }
-    reinterpret_cast<double2*>(u)[q2] = make_double2(nv[0], nv[1]);
+    st_nt(u + 2 * q2, nv[0], nv[1]);
   }
   __syncthreads();
   tile_face_fill<NC>(F, b, sb, 3, bc, sendbuf);
@@ -284,18 +329,19 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st) {
   if (F.n == 0) return;
-  const dim3 g(F.n), blk(256);
-#define OMG_RR(NC)                                                                                     \
+  const dim3 g(F.n);
+#define OMG_RR(NC, BS)                                                                                 \
   if (op == OP_HELM)                                                                                   \
-    k_resid_restrict<NC, OP_HELM><<<g, blk, 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, \
-                                                      dixp);                                           \
+    k_resid_restrict<NC, OP_HELM, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on,      \
+                                                              parent_local, dixp);                     \
   else                                                                                                 \
-    k_resid_restrict<NC, OP_LPL><<<g, blk, 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, dixp);
+    k_resid_restrict<NC, OP_LPL, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on,       \
+                                                             parent_local, dixp);
   switch (F.nc) {
-    case 16: OMG_RR(16) break;
-    case 8: OMG_RR(8) break;
-    case 4: OMG_RR(4) break;
-    default: OMG_RR(2) break;
+    case 16: OMG_RR(16, 512) break;
+    case 8: OMG_RR(8, 256) break;
+    case 4: OMG_RR(4, 256) break;
+    default: OMG_RR(2, 256) break;
   }
 #undef OMG_RR
 }
@@ -303,12 +349,12 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st) {
   if (F.n == 0) return;
-  const dim3 g(F.n), blk(256);
+  const dim3 g(F.n);
   switch (F.nc) {
-    case 16: k_prolong_fill<16><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    case 8: k_prolong_fill<8><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    case 4: k_prolong_fill<4><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    default: k_prolong_fill<2><<<g, blk, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 16: k_prolong_fill<16, 512><<<g, 512, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 8: k_prolong_fill<8, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 4: k_prolong_fill<4, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    default: k_prolong_fill<2, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
   }
 }
 
