@@ -412,11 +412,20 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   finish_halo(c, L, iv);
 }
 
+void materialize_level(omg_ctx* c, Level* L);
+double* red_mean(omg_ctx* c, int ch);
+double allreduce(omg_ctx* c, double v, bool is_max);
+
 // smooth_boxes (m_multigrid.f90:404-424)
 void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps;
   if (!L) return;
+  // a pending phi shift is subtracted by the first tiled substep while it
+  // loads (the values it reads are dead afterwards); otherwise applied now
+  const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 2 && L->phi_gc_ok &&
+                      gs_tiled(L->nc, c->op, L->has_rb);
+  if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
@@ -436,10 +445,12 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
     // substep and a full fill follows it.
     const int e = n & 1;
     const bool odd = L->nc & 1;
+    const double* shift = (n == 1 && absorb) ? red_mean(c, 0) : nullptr;
+    if (n == 1) L->shift_pending = false;
     if (L->n) {
       Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc, lvl);
       launch_gs_substep(L->view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
-                        L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, c->stream);
+                        L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream);
     }
     finish_halo(c, L, 1);
     if (odd || !L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
@@ -521,6 +532,12 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
 // update_coarse (m_multigrid.f90:347-384)
 void update_coarse(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl);
+  if (Level* Cl = level_ptr(c, lvl - 1)) {
+    // restriction overwrites every box of an all-parents level (interior), and
+    // the fill below every ghost face: a pending shift there is dead
+    if (Cl->all_parents) Cl->shift_pending = false;
+    else materialize_level(c, Cl);
+  }
   if (F && F->n && tiled_level(c, F)) {
     // residual + restriction of phi and res in one pass (omg_tiles.hip)
     phi_dirty(c, lvl - 1);
@@ -604,45 +621,157 @@ double allreduce(omg_ctx* c, double v, bool is_max) {
   return all[0];
 }
 
-// get_sum (m_multigrid.f90:278-294) + MPI_Allreduce(sum) (:255)
-double get_sum(omg_ctx* c, int iv) {
-  double* acc = c->d_scalar + 2;
-  HIPCHK(hipMemsetAsync(acc, 0, 8, c->stream));
+// ---------------------------------------------------------------------------
+// get_sum / subtract_mean on the device.  d_red slots: kAcc (this rank's sum,
+// per channel phi / rhs), kMean (the mean), kAll (the gathered per-rank sums).
+enum { kChPhi = 0, kChRhs = 1 };
+double* red_acc(omg_ctx* c, int ch) { return c->d_red + ch; }
+double* red_mean(omg_ctx* c, int ch) { return c->d_red + 2 + ch; }
+double* red_all(omg_ctx* c, int ch) { return c->d_red + 8 + (size_t)ch * c->n_ranks; }
+
+// get_sum's loop (m_multigrid.f90:278-294) for this rank: acc = 0, then per
+// level 1..highest the leaf sums and the sequential chain, on stream st.
+void leaf_sum_device(omg_ctx* c, int iv, double* acc, hipStream_t st) {
+  HIPCHK(hipMemsetAsync(acc, 0, 8, st));
   for (int l = 1; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     const double w = L->dr[0] * L->dr[1] * L->dr[2];
     {
       Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
-      launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, c->stream);
+      launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, st);
     }
     Prof p(c, "seq_sum", (double)L->leaves.size(), l);
-    launch_seq_sum2(L->d_scratch, (int)L->leaves.size(), w, acc, c->stream);
+    launch_seq_sum2(L->d_scratch, (int)L->leaves.size(), w, acc, st);
   }
-  HIPCHK(hipMemcpyAsync(c->h_scalar + 2, acc, 8, hipMemcpyDeviceToHost, c->stream));
+}
+
+double subtract_volume(omg_ctx* c) {
+  const int nc = c->box_size;
+  const auto& d1 = c->drl[1];
+  return (double)(nc * nc * nc) * (d1[0] * d1[1] * d1[2]) * (double)c->ids[1].size();
+}
+
+// MPI_Allreduce(acc) / volume into red_mean(ch), without leaving the stream
+// (RCCL all-gather + k_mean); the loopback transport gathers on the host.
+void mean_device(omg_ctx* c, int ch) {
+  const int n = c->n_ranks;
+  if (n > 64) throw OmgError("subtract_mean: more than 64 ranks");
+  double* all = red_all(c, ch);
+  if (n == 1) {
+    all = red_acc(c, ch);
+  } else if (c->loop) {
+    HIPCHK(hipMemcpyAsync(c->h_scalar + 4, red_acc(c, ch), 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<double> v = loop_allgather(c, c->h_scalar[4]);
+    for (int r = 0; r < n; r++) c->h_scalar[8 + r] = v[r];
+    HIPCHK(hipMemcpyAsync(all, c->h_scalar + 8, 8 * n, hipMemcpyHostToDevice, c->stream));
+  } else {
+    NCCLCHK(ncclAllGather(red_acc(c, ch), all, 1, ncclDouble, (ncclComm_t)c->nccl, c->stream));
+  }
+  launch_mean(all, n, subtract_volume(c), red_mean(c, ch), c->stream);
+}
+
+// get_sum + MPI_Allreduce(sum) as one value on the host (omg_get_sum)
+double get_sum(omg_ctx* c, int iv) {
+  leaf_sum_device(c, iv, red_acc(c, kChPhi), c->stream);
+  HIPCHK(hipMemcpyAsync(c->h_scalar + 2, red_acc(c, kChPhi), 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return allreduce(c, c->h_scalar[2], false);
 }
 
-// subtract_mean (m_multigrid.f90:245-276)
-void subtract_mean(omg_ctx* c, int iv, int ghosts) {
-  const int nc = c->box_size;
+// A pending phi -= mean (left by a standalone V-cycle, see subtract_mean) is
+// applied before anything else reads phi.
+void materialize_level(omg_ctx* c, Level* L) {
+  if (!L->shift_pending) return;
+  L->shift_pending = false;
+  if (L->n) {
+    Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, L->lvl);
+    launch_subtract(L->view(), 1, red_mean(c, kChPhi), 1, c->stream);
+  }
+}
+void materialize_phi(omg_ctx* c) {
+  if (!c->phi_shift_pending) return;
+  for (auto& kv : c->levels) materialize_level(c, &kv.second);
+  c->phi_shift_pending = false;
+}
+void drop_rhs_cache(omg_ctx* c) { c->rhs_cache_valid = false; }
+// entry points other than the cycles: apply pending phi work first; `writes`
+// = the call may change rhs (the cached rhs sum is dropped)
+void enter(omg_ctx* c, bool writes = true) {
+  materialize_phi(c);
+  if (writes) drop_rhs_cache(c);
+}
+
+// subtract_mean (m_multigrid.f90:245-276), mean computed on the device.
+// mode kInCycle: the standalone V-cycle's calls, where the next reads are
+// known: rhs of levels whose boxes are all parents is overwritten by
+// update_coarse before it is read (skipped), and phi -= mean is left pending:
+// the first red-black substep of the next cycle subtracts it while loading
+// (bit-identical), levels that restriction overwrites drop it, anything else
+// applies it first (materialize_phi).
+enum { kPlain = 0, kInCycle = 1 };
+void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
   // subtracting from interior and ghosts keeps same-GPU / remote face ghosts
   // equal to a fill; physical and refinement-boundary ghosts are not.
-  if (iv == 1)
+  if (iv == 1) {
+    materialize_phi(c);
     for (auto& kv : c->levels)
       if (!ghosts || kv.second.has_phys || kv.second.has_rb) kv.second.phi_gc_ok = false;
-  double mean = get_sum(c, iv);
-  const auto& d1 = c->drl[1];
-  const double volume = (double)(nc * nc * nc) * (d1[0] * d1[1] * d1[2]) * (double)c->ids[1].size();
-  mean = mean / volume;
-  c->h_scalar[3] = mean;
-  HIPCHK(hipMemcpyAsync(c->d_scalar + 3, c->h_scalar + 3, 8, hipMemcpyHostToDevice, c->stream));
+  }
+  if (iv == 2 && !ghosts) {
+    // rhs: the sums may already be running on the side stream (see below)
+    if (c->rhs_cache_valid) {
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_side, 0));
+    } else {
+      leaf_sum_device(c, 2, red_acc(c, kChRhs), c->stream);
+    }
+    c->rhs_cache_valid = false;
+    mean_device(c, kChRhs);
+    bool all_fused = true;
+    for (int l = c->lowest; l <= c->highest; l++) {
+      Level* L = level_ptr(c, l);
+      if (!L || !L->n) continue;
+      if (mode == kInCycle && L->all_parents) continue;
+      Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, l);
+      if (l >= 1 && (int)L->leaves.size() == L->n && subtract_sums_nc(L->nc))
+        launch_subtract_sums(L->view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
+      else {
+        launch_subtract(L->view(), 2, red_mean(c, kChRhs), 0, c->stream);
+        if (l >= 1 && !L->leaves.empty()) all_fused = false;
+      }
+    }
+    if (all_fused) {
+      // the next get_sum(rhs): its leaf sums were produced by the fused
+      // kernels; its sequential chain runs now on the side stream
+      HIPCHK(hipEventRecord(c->ev_main, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_main, 0));
+      double* acc = red_acc(c, kChRhs);
+      HIPCHK(hipMemsetAsync(acc, 0, 8, c->stream2));
+      for (int l = 1; l <= c->highest; l++) {
+        Level* L = level_ptr(c, l);
+        if (!L || L->leaves.empty()) continue;
+        launch_seq_sum2(L->d_scratch_rhs, (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, c->stream2);
+      }
+      HIPCHK(hipEventRecord(c->ev_side, c->stream2));
+      c->rhs_cache_valid = true;
+    }
+    return;
+  }
+  if (iv == 2) drop_rhs_cache(c);
+  const int ch = iv == 2 ? kChRhs : kChPhi;
+  leaf_sum_device(c, iv, red_acc(c, ch), c->stream);
+  mean_device(c, ch);
+  if (iv == 1 && ghosts && mode == kInCycle) {
+    for (auto& kv : c->levels) kv.second.shift_pending = kv.second.n > 0;
+    c->phi_shift_pending = true;
+    return;
+  }
   for (int l = c->lowest; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (L && L->n) {
       Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, l);
-      launch_subtract(L->view(), iv, c->d_scalar + 3, ghosts, c->stream);
+      launch_subtract(L->view(), iv, red_mean(c, ch), ghosts, c->stream);
     }
   }
 }
@@ -650,12 +779,30 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts) {
 // mg_fas_vcycle (m_multigrid.f90:150-243)
 double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalone) {
   const bool has_highest = highest_lvl >= c->lowest;
-  if (c->subtract_mean && !has_highest) subtract_mean(c, 2, 0);
   const int min_lvl = c->lowest, max_lvl = has_highest ? highest_lvl : c->highest;
+  const bool full = standalone && !has_highest;   // a stand-alone cycle over the whole tree
+  // a pending phi shift (previous stand-alone cycle) is absorbed by the first
+  // substep on max_lvl or dropped where restriction overwrites a level
+  if (c->phi_shift_pending) {
+    if (!full) {
+      materialize_phi(c);
+    } else {
+      for (auto& kv : c->levels) {
+        Level& L = kv.second;
+        if (L.shift_pending && L.lvl != max_lvl && !L.all_parents) materialize_level(c, &L);
+      }
+    }
+  }
+  if (c->subtract_mean && !has_highest) subtract_mean(c, 2, 0, full ? kInCycle : kPlain);
   if (standalone) {
     // the fill is idempotent: skip it when the ghosts already equal its result
     Level* L = level_ptr(c, max_lvl);
-    if (!(L && L->phi_gc_ok && !L->has_rb && !L->has_remote)) fill_gc_lvl(c, max_lvl, 1);
+    bool need = !(L && L->phi_gc_ok && !L->has_rb);
+    if (c->n_ranks > 1) need = allreduce(c, need ? 1.0 : 0.0, true) > 0.5;   // fills exchange: agree
+    if (need) {
+      if (L) materialize_level(c, L);
+      fill_gc_lvl(c, max_lvl, 1);
+    }
   }
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     smooth_boxes(c, l, c->n_cycle_down);
@@ -684,12 +831,19 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     for (int l = min_lvl; l <= max_lvl; l++) m = std::max(max_residual_lvl(c, l), m);
     max_res = allreduce(c, m, true);
   }
-  if (c->subtract_mean) subtract_mean(c, 1, 1);
+  materialize_phi(c);   // nothing left pending after a cycle (defensive: all consumed)
+  if (c->subtract_mean) subtract_mean(c, 1, 1, full ? kInCycle : kPlain);
   return max_res;
 }
 
 // mg_fas_fmg (m_multigrid.f90:84-147)
 double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
+  if (have_guess) {
+    materialize_phi(c);
+  } else {
+    for (auto& kv : c->levels) kv.second.shift_pending = false;   // phi = 0 below
+    c->phi_shift_pending = false;
+  }
   if (!have_guess) phi_dirty_all(c);
   if (!have_guess)
     for (int l = c->highest; l >= c->lowest; l--) {
@@ -721,7 +875,7 @@ void free_levels(omg_ctx* c) {
     Level& L = kv.second;
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
-    dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch);
+    dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rbsend); dfree(L.d_rbrecv);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx}) {
       dfree(T->d_send_items);
@@ -865,6 +1019,8 @@ void build_plan(omg_ctx* c) {
     L.d_parents = to_device(L.parents);
     L.d_leaves = to_device(L.leaves);
     dmalloc(&L.d_scratch, sizeof(double) * L.leaves.size());
+    dmalloc(&L.d_scratch_rhs, sizeof(double) * L.leaves.size());
+    L.all_parents = L.n > 0 && (int)L.parents.size() == L.n;
   }
   // grid transfers between lvl-1 (coarse) and lvl (fine)
   for (int l = c->lowest + 1; l <= c->highest; l++) {
@@ -997,7 +1153,12 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
-    HIPCHK(hipHostMalloc(&c->h_scalar, sizeof(double) * 64));
+    HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
+    HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+    HIPCHK(hipHostMalloc(&c->h_scalar, sizeof(double) * (16 + (size_t)n_ranks)));
     for (int iv = 0; iv < kMaxVars; iv++)
       for (int nb = 0; nb < 6; nb++) {
         c->bc[iv].type[nb] = OMG_BC_DIRICHLET;
@@ -1037,9 +1198,14 @@ int omg_ctx_destroy(omg_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream2);
     free_levels(c);
     dfree(c->d_scalar);
+    dfree(c->d_red);
     dfree(c->d_stage);
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+    if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
     if (c->loop) {   // the last context of a loopback group removes it
@@ -1093,6 +1259,8 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
         (*dst[t])[l] = std::vector<int>(lists + a, lists + b);
       }
     }
+    c->rhs_cache_valid = false;
+    c->phi_shift_pending = false;
     build_plan(c);
     if (!c->host_only) HIPCHK(hipDeviceSynchronize());
   });
@@ -1217,6 +1385,7 @@ double* stage(omg_ctx* c, size_t n) {
 
 int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
   return guarded([&] {
+    enter(c);
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
@@ -1232,6 +1401,7 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
 
 int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
   return guarded([&] {
+    enter(c, false);
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
@@ -1260,6 +1430,7 @@ int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
 
 int omg_apply_op(omg_ctx* c, int i_out) {
   return guarded([&] {
+    enter(c);
     if (i_out == 1) phi_dirty_all(c);
     for (int l = c->lowest; l <= c->highest; l++) {
       Level* L = level_ptr(c, l);
@@ -1270,40 +1441,69 @@ int omg_apply_op(omg_ctx* c, int i_out) {
 
 int omg_restrict(omg_ctx* c, int iv) {
   return guarded([&] {
+    enter(c);
     for (int l = c->highest; l >= c->lowest + 1; l--) restrict_lvl(c, iv, l);
   });
 }
 int omg_restrict_lvl(omg_ctx* c, int iv, int lvl) {
-  return guarded([&] { restrict_lvl(c, iv, lvl); });
+  return guarded([&] {
+    enter(c);
+    restrict_lvl(c, iv, lvl);
+  });
 }
 int omg_fill_ghost_cells(omg_ctx* c, int iv) {
   return guarded([&] {
+    enter(c);
     for (int l = c->lowest; l <= c->highest; l++) fill_gc_lvl(c, l, iv);
   });
 }
 int omg_fill_ghost_cells_lvl(omg_ctx* c, int lvl, int iv) {
-  return guarded([&] { fill_gc_lvl(c, lvl, iv); });
+  return guarded([&] {
+    enter(c);
+    fill_gc_lvl(c, lvl, iv);
+  });
 }
 int omg_prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
-  return guarded([&] { prolong(c, lvl, iv, iv_to, add); });
+  return guarded([&] {
+    enter(c);
+    prolong(c, lvl, iv, iv_to, add);
+  });
 }
 int omg_smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
-  return guarded([&] { smooth_boxes(c, lvl, n_cycle); });
+  return guarded([&] {
+    enter(c);
+    smooth_boxes(c, lvl, n_cycle);
+  });
 }
 int omg_update_coarse(omg_ctx* c, int lvl) {
-  return guarded([&] { update_coarse(c, lvl); });
+  return guarded([&] {
+    enter(c);
+    update_coarse(c, lvl);
+  });
 }
 int omg_correct_children(omg_ctx* c, int lvl) {
-  return guarded([&] { correct_children(c, lvl); });
+  return guarded([&] {
+    enter(c);
+    correct_children(c, lvl);
+  });
 }
 int omg_residual_lvl(omg_ctx* c, int lvl) {
-  return guarded([&] { residual_lvl(c, lvl, nullptr); });
+  return guarded([&] {
+    enter(c);
+    residual_lvl(c, lvl, nullptr);
+  });
 }
 int omg_max_residual_lvl(omg_ctx* c, int lvl, double* out) {
-  return guarded([&] { *out = max_residual_lvl(c, lvl); });
+  return guarded([&] {
+    enter(c);
+    *out = max_residual_lvl(c, lvl);
+  });
 }
 int omg_get_sum(omg_ctx* c, int iv, double* out) {
-  return guarded([&] { *out = get_sum(c, iv); });
+  return guarded([&] {
+    enter(c, false);
+    *out = get_sum(c, iv);
+  });
 }
 int omg_subtract_mean(omg_ctx* c, int iv, int include_ghostcells) {
   return guarded([&] { subtract_mean(c, iv, include_ghostcells); });
@@ -1313,6 +1513,7 @@ int omg_subtract_mean(omg_ctx* c, int iv, int include_ghostcells) {
 // the rhs ghost cells and the bc type into the neighbour slot.
 int omg_phi_bc_store(omg_ctx* c) {
   return guarded([&] {
+    enter(c);
     phi_dirty_all(c);
     for (auto& kv : c->levels) {
       Level& L = kv.second;
@@ -1333,7 +1534,10 @@ int omg_phi_bc_store(omg_ctx* c) {
 }
 
 int omg_synchronize(omg_ctx* c) {
-  return guarded([&] { HIPCHK(hipStreamSynchronize(c->stream)); });
+  return guarded([&] {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream2));
+  });
 }
 
 void* omg_stream(omg_ctx* c) { return (void*)c->stream; }

@@ -91,6 +91,8 @@ struct Level {
   double* d_phi = nullptr;              // phi (d_data's var 1)
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
   bool has_rb = false, has_remote = false, has_phys = false;
+  bool all_parents = false;      // every box of this rank at this level is a parent
+  bool shift_pending = false;    // phi -= mean still to apply (see subtract_mean)
   int8_t* d_nbk = nullptr;
   int* d_nba = nullptr;
   int* d_sendpos = nullptr;
@@ -120,6 +122,7 @@ struct Level {
   Transfer prol;        // prolongation lvl-1 -> this level (send: child global → parent idx*8+slot; recv: my child idx)
   Transfer rbx;         // refinement-boundary faces across ranks at this level (send: coarse idx at
                         // lvl-1, coarse-side nb, child offset; recv: box*6+nb of my fine face)
+  double* d_scratch_rhs = nullptr;   // leaf sums of rhs for the next get_sum
   double* d_rbsend = nullptr;
   double* d_rbrecv = nullptr;
   double* d_sendbuf = nullptr;
@@ -194,6 +197,11 @@ struct omg_ctx {
   std::map<int, long long*> d_face_off_lvl[omg::kMaxVars];
   std::map<int, int*> d_face_type_lvl[omg::kMaxVars];
   // scalars
+  double* d_red = nullptr;             // device reductions (get_sum / subtract_mean)
+  hipStream_t stream2 = nullptr;       // side stream (rhs sum chain)
+  hipEvent_t ev_main = nullptr, ev_side = nullptr;
+  bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
+  bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch
   double* h_scalar = nullptr;          // pinned host scratch
   double* d_stage = nullptr;           // upload/download staging (reference layout)

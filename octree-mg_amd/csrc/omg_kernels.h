@@ -17,8 +17,15 @@ struct GcBC {
 
 // red-black substep (colour e) + the ghost fill after it; picks the LDS-tiled
 // kernel (omg_sweep.hip) when the level allows, else the generic one
+// shift (device scalar or null): subtract it from every value the substep
+// loads (a pending subtract_mean of phi, bit-identical to applying it first)
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
-                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, hipStream_t st);
+                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
+                       hipStream_t st);
+// whether launch_gs_substep takes the LDS-tiled kernel (which alone takes a shift)
+inline bool gs_tiled(int nc, int op, bool has_rb) {
+  return !has_rb && (op == OP_LPL || op == OP_HELM) && (nc == 16 || nc == 8 || nc == 4 || nc == 2);
+}
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st);
@@ -62,6 +69,10 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
+bool subtract_sums_nc(int nc);
+void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
+                          hipStream_t st);
+void launch_mean(const double* all, int n, double volume, double* mean, hipStream_t st);
 void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st);
 
 }  // namespace omg

@@ -439,6 +439,21 @@ __global__ void __launch_bounds__(256) k_subtract(LevelView L, int iv, const dou
   }
 }
 
+// Even box sizes: every slot of the stored range is a cell, so the variable
+// streams as contiguous double2 per box.
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256) k_subtract_even(LevelView L, int iv, const double* mean, int per2) {
+  const double m = *mean;
+  GRID_STRIDE(t, (long long)per2 * L.n) {
+    const int b = (int)(t / per2), o = (int)(t % per2);
+    v2d_t* u = reinterpret_cast<v2d_t*>(boxp(L, iv, b)) + o;
+    v2d_t x = __builtin_nontemporal_load(u);
+    x.x = x.x - m;
+    x.y = x.y - m;
+    __builtin_nontemporal_store(x, u);
+  }
+}
+
 // Whole-box copy / zero of one variable (FMG's old = phi and phi = 0).
 __global__ void __launch_bounds__(256) k_copy_var(LevelView L, int src, int dst) {
   GRID_STRIDE(t, (long long)L.n * L.stride) {
@@ -631,6 +646,11 @@ void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStr
 void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts, hipStream_t st) {
   const long long work = (2LL * L.hv + 6LL * L.fs) * L.n;
   if (work == 0) return;
+  if ((L.nc & 1) == 0) {
+    const int per2 = (int)((ghosts ? 2LL * L.hv + 6LL * L.fs : 2LL * L.hv) / 2);
+    k_subtract_even<<<grid_for((long long)per2 * L.n), 256, 0, st>>>(L, iv, mean, per2);
+    return;
+  }
   k_subtract<<<grid_for(work), 256, 0, st>>>(L, iv, mean, ghosts);
 }
 

@@ -28,7 +28,7 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 
 template <int NC, int OP, int BS, int NT>
 __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
-                                                  double* __restrict__ sendbuf) {
+                                                  double* __restrict__ sendbuf, const double* __restrict__ shift) {
   constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
   constexpr int NP2 = (HV / 2 + BS - 1) / BS;  // double2 cell pairs per thread
   __shared__ double so[HV];                    // colour 1-e of the interior
@@ -44,11 +44,24 @@ __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, in
   {
     const v2d* src = reinterpret_cast<const v2d*>(u + o * HV);
     v2d* dst = reinterpret_cast<v2d*>(so);
-    for (int q = tid; q < HV / 2; q += BS) dst[q] = NT >= 2 ? __builtin_nontemporal_load(src + q) : src[q];
+    const double m = shift ? *shift : 0.0;
+    for (int q = tid; q < HV / 2; q += BS) {
+      v2d x = NT >= 2 ? __builtin_nontemporal_load(src + q) : src[q];
+      if (shift) {
+        x.x = x.x - m;
+        x.y = x.y - m;
+      }
+      dst[q] = x;
+    }
     for (int q = tid; q < 3 * FH; q += BS) {   // 6 faces x FH/2 double2
       const int nb = q / (FH / 2), r = q % (FH / 2);
       const v2d* gp = reinterpret_cast<const v2d*>(u + 2 * HV + nb * FS + o * FH) + r;
-      reinterpret_cast<v2d*>(sg + nb * FH)[r] = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
+      v2d x = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
+      if (shift) {
+        x.x = x.x - m;
+        x.y = x.y - m;
+      }
+      reinterpret_cast<v2d*>(sg + nb * FH)[r] = x;
     }
   }
   double2 fr[NP2];
@@ -171,11 +184,10 @@ __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, in
 }
 
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
-                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, hipStream_t st) {
+                       const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
+                       hipStream_t st) {
   if (L.n == 0) return;
-  const bool tiled = !has_rb && (op == OP_LPL || op == OP_HELM) &&
-                     (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2);
-  if (!tiled) {
+  if (!gs_tiled(L.nc, op, has_rb)) {
     launch_gs_sub(L, op, lambda, e, colours, C, rb, bc, sendbuf, st);
     return;
   }
@@ -188,9 +200,9 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   const dim3 g(L.n);
 #define OMG_TILE(NC, BS)                                                                   \
   if (op == OP_HELM)                                                                       \
-    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf); \
+    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift); \
   else                                                                                     \
-    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf);
+    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift);
   switch (L.nc) {
     case 16: OMG_TILE(16, 512) break;
     case 8: OMG_TILE(8, 256) break;

@@ -203,9 +203,13 @@ __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, 
 // streams them through LDS in chunks of R rows: the loads are whole 256-B
 // colour segments shared by 64 lanes (coalesced), the next chunk is in flight
 // while the lanes run their add chains out of LDS.
-template <int NC>
+// SUB: subtract_mean fused in front (m_multigrid.f90:268-272, no ghosts): every
+// value is replaced by v - mean in HBM and the box sums are those of the new
+// values (what the next get_sum of this variable will need).
+template <int NC, bool SUB>
 __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
-                                                  int n_leaves, double* __restrict__ out) {
+                                                  int n_leaves, double* __restrict__ out,
+                                                  const double* __restrict__ mean) {
   constexpr int H = NC / 2, R = 4, SEG = R * H;   // doubles of one colour in a chunk
   constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
   constexpr int PER = 32 * CH2 / 64;              // double2 per lane per chunk
@@ -214,15 +218,18 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
   __shared__ double lds[32 * P];
   const int lane = threadIdx.x, b0 = blockIdx.x * 32;
   const long long hv = L.hv;
-  const double* src[PER];
+  double* src[PER];
   int dst[PER];
+  bool own[PER];   // lanes past the last leaf load a duplicate and never store
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const int t = lane + 64 * r, bb = t / CH2, w = t % CH2, seg = w / (SEG / 2), off = w % (SEG / 2);
     const int q = min(b0 + bb, n_leaves - 1);
+    own[r] = b0 + bb < n_leaves;
     src[r] = boxp(L, iv, leaves[q]) + seg * hv + 2 * off;
     dst[r] = bb * P + seg * SEG + 2 * off;
   }
+  const double m = SUB ? *mean : 0.0;
   double2 v[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r]);
@@ -230,8 +237,14 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
   const double* my = lds + lane * P;
   for (int c = 0; c < NCH; c++) {
     __syncthreads();
+    const int rc = H * (((c % (NC / R)) * R) + NC * (c / (NC / R)));   // chunk offset
 #pragma unroll
     for (int r = 0; r < PER; r++) {
+      if (SUB) {
+        v[r].x = v[r].x - m;
+        v[r].y = v[r].y - m;
+        if (own[r]) *reinterpret_cast<double2*>(src[r] + rc) = v[r];
+      }
       lds[dst[r]] = v[r].x;
       lds[dst[r] + 1] = v[r].y;
     }
@@ -362,11 +375,41 @@ void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, doub
   if (n == 0) return;
   const dim3 g((n + 31) / 32);
   switch (L.nc) {
-    case 16: k_box_sums3<16><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
-    case 8: k_box_sums3<8><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
-    case 4: k_box_sums3<4><<<g, 64, 0, st>>>(L, iv, leaves, n, out); break;
+    case 16: k_box_sums3<16, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
+    case 8: k_box_sums3<8, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
+    case 4: k_box_sums3<4, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
     default: k_box_sums_any<<<(n + 63) / 64, 64, 0, st>>>(L, iv, leaves, n, out); break;
   }
+}
+
+bool subtract_sums_nc(int nc) { return nc == 16 || nc == 8 || nc == 4; }
+
+void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
+                          hipStream_t st) {
+  if (n == 0) return;
+  const dim3 g((n + 31) / 32);
+  switch (L.nc) {
+    case 16: k_box_sums3<16, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
+    case 8: k_box_sums3<8, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
+    case 4: k_box_sums3<4, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
+    default: break;
+  }
+}
+
+// mean = MPI_Allreduce(sum) / volume on the device (subtract_mean,
+// m_multigrid.f90:255-262): the per-rank sums combined in MPICH's one-node
+// binomial order, ((a0+a1)+(a2+a3))+..., then the division.
+__global__ void k_mean(const double* all, int n, double volume, double* mean) {
+  if (threadIdx.x || blockIdx.x) return;
+  double t[64];
+  for (int r = 0; r < n; r++) t[r] = all[r];
+  for (int w = 1; w < n; w *= 2)
+    for (int r = 0; r + w < n; r += 2 * w) t[r] = t[r] + t[r + w];
+  *mean = t[0] / volume;
+}
+
+void launch_mean(const double* all, int n, double volume, double* mean, hipStream_t st) {
+  k_mean<<<1, 64, 0, st>>>(all, n, volume, mean);
 }
 
 void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
