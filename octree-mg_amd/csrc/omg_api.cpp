@@ -413,6 +413,7 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
 }
 
 void materialize_level(omg_ctx* c, Level* L);
+void phi_mean_ready(omg_ctx* c);
 double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
 
@@ -445,6 +446,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
     // substep and a full fill follows it.
     const int e = n & 1;
     const bool odd = L->nc & 1;
+    if (n == 1 && absorb) phi_mean_ready(c);
     const double* shift = (n == 1 && absorb) ? red_mean(c, 0) : nullptr;
     if (n == 1) L->shift_pending = false;
     if (L->n) {
@@ -557,7 +559,8 @@ void update_coarse(omg_ctx* c, int lvl) {
   Level* C = level_ptr(c, lvl - 1);
   if (C && !C->parents.empty()) {
     Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl - 1);
-    launch_coarse_rhs(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream);
+    if (!launch_coarse_rhs_tile(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream))
+      launch_coarse_rhs(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream);
   }
 }
 
@@ -579,14 +582,17 @@ void correct_and_fill(omg_ctx* c, int lvl) {
   Level* C = level_ptr(c, lvl);
   if (F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
       !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv))) {
-    if (!C->parents.empty()) {
+    // every parent here has all its children on this GPU (no prolongation
+    // traffic, every fine box has a local parent): the children form res
+    const bool sub = (size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc;
+    if (!sub && !C->parents.empty()) {
       Prof p(c, "sub_parents", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl);
       launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
     }
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
-                          F->d_sendbuf, c->stream);
+                          F->d_sendbuf, sub, c->stream);
     }
     finish_halo(c, F, 1);
     F->phi_gc_ok = true;
@@ -629,21 +635,41 @@ double* red_acc(omg_ctx* c, int ch) { return c->d_red + ch; }
 double* red_mean(omg_ctx* c, int ch) { return c->d_red + 2 + ch; }
 double* red_all(omg_ctx* c, int ch) { return c->d_red + 8 + (size_t)ch * c->n_ranks; }
 
-// get_sum's loop (m_multigrid.f90:278-294) for this rank: acc = 0, then per
-// level 1..highest the leaf sums and the sequential chain, on stream st.
-void leaf_sum_device(omg_ctx* c, int iv, double* acc, hipStream_t st) {
+// get_sum's loop (m_multigrid.f90:278-294) for this rank, in two parts: the
+// per-leaf sums of every level (into the channel's scratch), then acc = 0 and
+// the sequential chains level by level.  Scratch and acc of a channel may be
+// in use by a chain on the side stream: writers wait for it first.
+double* leaf_scratch(Level* L, int ch) { return ch == kChRhs ? L->d_scratch_rhs : L->d_scratch; }
+
+void side_done(omg_ctx* c) {
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_side, 0));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_phi, 0));
+}
+
+void leaf_box_sums(omg_ctx* c, int iv, int ch, hipStream_t st) {
+  for (int l = 1; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->leaves.empty()) continue;
+    Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
+    launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
+  }
+}
+
+void leaf_chain(omg_ctx* c, int ch, hipStream_t st) {
+  double* acc = red_acc(c, ch);
   HIPCHK(hipMemsetAsync(acc, 0, 8, st));
   for (int l = 1; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
-    const double w = L->dr[0] * L->dr[1] * L->dr[2];
-    {
-      Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
-      launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), L->d_scratch, st);
-    }
     Prof p(c, "seq_sum", (double)L->leaves.size(), l);
-    launch_seq_sum2(L->d_scratch, (int)L->leaves.size(), w, acc, st);
+    launch_seq_sum2(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, st);
   }
+}
+
+void leaf_sum_device(omg_ctx* c, int iv, int ch) {
+  side_done(c);
+  leaf_box_sums(c, iv, ch, c->stream);
+  leaf_chain(c, ch, c->stream);
 }
 
 double subtract_volume(omg_ctx* c) {
@@ -674,16 +700,26 @@ void mean_device(omg_ctx* c, int ch) {
 
 // get_sum + MPI_Allreduce(sum) as one value on the host (omg_get_sum)
 double get_sum(omg_ctx* c, int iv) {
-  leaf_sum_device(c, iv, red_acc(c, kChPhi), c->stream);
+  leaf_sum_device(c, iv, kChPhi);
   HIPCHK(hipMemcpyAsync(c->h_scalar + 2, red_acc(c, kChPhi), 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return allreduce(c, c->h_scalar[2], false);
+}
+
+// The phi mean of a stand-alone cycle's subtract_mean is finished on the side
+// stream (its chain overlaps the next cycle's rhs work); consumers wait here.
+void phi_mean_ready(omg_ctx* c) {
+  if (!c->phi_mean_on_side) return;
+  c->phi_mean_on_side = false;
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_phi, 0));
+  if (c->n_ranks > 1) mean_device(c, kChPhi);
 }
 
 // A pending phi -= mean (left by a standalone V-cycle, see subtract_mean) is
 // applied before anything else reads phi.
 void materialize_level(omg_ctx* c, Level* L) {
   if (!L->shift_pending) return;
+  phi_mean_ready(c);
   L->shift_pending = false;
   if (L->n) {
     Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, L->lvl);
@@ -724,7 +760,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
     if (c->rhs_cache_valid) {
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_side, 0));
     } else {
-      leaf_sum_device(c, 2, red_acc(c, kChRhs), c->stream);
+      leaf_sum_device(c, 2, kChRhs);
     }
     c->rhs_cache_valid = false;
     mean_device(c, kChRhs);
@@ -746,13 +782,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       // kernels; its sequential chain runs now on the side stream
       HIPCHK(hipEventRecord(c->ev_main, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_main, 0));
-      double* acc = red_acc(c, kChRhs);
-      HIPCHK(hipMemsetAsync(acc, 0, 8, c->stream2));
-      for (int l = 1; l <= c->highest; l++) {
-        Level* L = level_ptr(c, l);
-        if (!L || L->leaves.empty()) continue;
-        launch_seq_sum2(L->d_scratch_rhs, (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, c->stream2);
-      }
+      leaf_chain(c, kChRhs, c->stream2);
       HIPCHK(hipEventRecord(c->ev_side, c->stream2));
       c->rhs_cache_valid = true;
     }
@@ -760,13 +790,23 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
   }
   if (iv == 2) drop_rhs_cache(c);
   const int ch = iv == 2 ? kChRhs : kChPhi;
-  leaf_sum_device(c, iv, red_acc(c, ch), c->stream);
-  mean_device(c, ch);
   if (iv == 1 && ghosts && mode == kInCycle) {
+    // leaf sums now, chain (+ mean on one rank) on the side stream; the next
+    // cycle's rhs work overlaps it and phi_mean_ready() joins before use
+    side_done(c);
+    leaf_box_sums(c, 1, kChPhi, c->stream);
+    HIPCHK(hipEventRecord(c->ev_main, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_main, 0));
+    leaf_chain(c, kChPhi, c->stream2);
+    if (c->n_ranks == 1) launch_mean(red_acc(c, kChPhi), 1, subtract_volume(c), red_mean(c, kChPhi), c->stream2);
+    HIPCHK(hipEventRecord(c->ev_phi, c->stream2));
+    c->phi_mean_on_side = true;
     for (auto& kv : c->levels) kv.second.shift_pending = kv.second.n > 0;
     c->phi_shift_pending = true;
     return;
   }
+  leaf_sum_device(c, iv, ch);
+  mean_device(c, ch);
   for (int l = c->lowest; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (L && L->n) {
@@ -1158,6 +1198,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_phi, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(&c->h_scalar, sizeof(double) * (16 + (size_t)n_ranks)));
     for (int iv = 0; iv < kMaxVars; iv++)
       for (int nb = 0; nb < 6; nb++) {
@@ -1205,6 +1246,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     dfree(c->d_stage);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    if (c->ev_phi) (void)hipEventDestroy(c->ev_phi);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
@@ -1259,8 +1301,13 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
         (*dst[t])[l] = std::vector<int>(lists + a, lists + b);
       }
     }
+    if (!c->host_only) {
+      HIPCHK(hipStreamSynchronize(c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream2));
+    }
     c->rhs_cache_valid = false;
     c->phi_shift_pending = false;
+    c->phi_mean_on_side = false;
     build_plan(c);
     if (!c->host_only) HIPCHK(hipDeviceSynchronize());
   });

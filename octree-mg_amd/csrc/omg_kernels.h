@@ -66,8 +66,14 @@ bool tiled_nc(int nc);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st);
+// sub: form the parent's res = phi - old on the fly (and store it) instead of
+// reading it (correct_children's parent loop fused in)
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
-                         const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st);
+                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, hipStream_t st);
+// update_coarse's parent loop, LDS-tiled; false when the box size / operator
+// has no tiled kernel (caller falls back to launch_coarse_rhs)
+bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
+                            hipStream_t st);
 void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
 bool subtract_sums_nc(int nc);
 void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,

@@ -146,7 +146,11 @@ __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv
   }
 }
 
-template <int NC, int BS>
+// SUB: correct_children's `res = phi - old` on the parent (m_multigrid.f90:
+// 392-399) is formed here while the parent data is loaded; each child writes
+// the res cells of its own octant and of the parent ghost faces next to it
+// (every stored cell of the parent exactly once over its 8 children).
+template <int NC, int BS, bool SUB>
 __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
                                                      const int* parent_local, const int* dixp, GcBC bc,
                                                      double* sendbuf) {
@@ -161,7 +165,17 @@ __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, 
   for (int q = tid; q < CB * CB * CB; q += BS) {
     const int p = q % CB, s = (q / CB) % CB, t = q / (CB * CB);
     const int nbnd = (p == 0 || p == CB - 1) + (s == 0 || s == CB - 1) + (t == 0 || t == CB - 1);
-    if (nbnd < 2) cb[q] = cu[off_cell(Cv, dx + p, dy + s, dz + t)];
+    if (nbnd >= 2) continue;
+    const int x = dx + p, y = dy + s, z = dz + t, o = off_cell(Cv, x, y, z);
+    if (SUB) {
+      const double r = boxp(Cv, 1, pb)[o] - boxp(Cv, 3, pb)[o];
+      cb[q] = r;
+      const int n1 = Cv.nc + 1;
+      const bool ghost = x == 0 || x == n1 || y == 0 || y == n1 || z == 0 || z == n1;
+      if (nbnd == 0 || ghost) boxp(Cv, 4, pb)[o] = r;
+    } else {
+      cb[q] = cu[o];
+    }
   }
   double* __restrict__ u = F.phi + (long long)b * F.stride;
   v2d old[NR];
@@ -360,15 +374,97 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 }
 
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
-                         const int* dixp, const GcBC& bc, double* sendbuf, hipStream_t st) {
+                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, hipStream_t st) {
   if (F.n == 0) return;
   const dim3 g(F.n);
+#define OMG_PF(NC, BS)                                                                                \
+  if (sub)                                                                                            \
+    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf);        \
+  else                                                                                                \
+    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf);
   switch (F.nc) {
-    case 16: k_prolong_fill<16, 512><<<g, 512, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    case 8: k_prolong_fill<8, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    case 4: k_prolong_fill<4, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
-    default: k_prolong_fill<2, 256><<<g, 256, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf); break;
+    case 16: OMG_PF(16, 512) break;
+    case 8: OMG_PF(8, 256) break;
+    case 4: OMG_PF(4, 256) break;
+    default: OMG_PF(2, 256) break;
   }
+#undef OMG_PF
+}
+
+// update_coarse's parent loop (m_multigrid.f90:364-383) for one parent box
+// per workgroup: rhs = L(phi) + res over the interior (box_op, then the sum),
+// old = phi over the whole stored box.
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
+  using TL = Tl<NC>;
+  constexpr int NST = TL::NST, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, H = NC / 2;
+  __shared__ double sb[NST];
+  const int b = parents[xcd_box(blockIdx.x, gridDim.x)], tid = threadIdx.x;
+  const long long boff = (long long)b * Cv.stride;
+  const double* __restrict__ u = Cv.phi + boff;
+  double* __restrict__ rhs = Cv.data + Cv.vstride + boff;
+  double* __restrict__ old = Cv.data + 2 * Cv.vstride + boff;
+  const double* __restrict__ res = Cv.data + 3 * Cv.vstride + boff;
+  for (int q = tid; q < NST / 2; q += BS) {
+    const v2d x = reinterpret_cast<const v2d*>(u)[q];
+    reinterpret_cast<v2d*>(sb)[q] = x;
+    reinterpret_cast<v2d*>(old)[q] = x;
+  }
+  v2d rr[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 < HV) rr[r] = reinterpret_cast<const v2d*>(res)[q2];
+  }
+  __syncthreads();
+  const OpCoef<OP> K(Cv, lambda);
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 >= HV) continue;
+    const int e = q2 >= HV / 2, o = 1 - e;
+    Nbr7 s0, s1;
+    if constexpr (H % 2 == 0) {
+      pair_stencil<NC>(sb + o * HV, sb + 2 * HV + o * FH, FS, e, 2 * q2 - e * HV, s0, s1);
+    } else {
+      int i, j, k;
+      TL::decode(2 * q2, i, j, k);
+      s0.xm = sb[TL::ocell(i - 1, j, k)]; s0.xp = sb[TL::ocell(i + 1, j, k)];
+      s0.ym = sb[TL::ocell(i, j - 1, k)]; s0.yp = sb[TL::ocell(i, j + 1, k)];
+      s0.zm = sb[TL::ocell(i, j, k - 1)]; s0.zp = sb[TL::ocell(i, j, k + 1)];
+      TL::decode(2 * q2 + 1, i, j, k);
+      s1.xm = sb[TL::ocell(i - 1, j, k)]; s1.xp = sb[TL::ocell(i + 1, j, k)];
+      s1.ym = sb[TL::ocell(i, j - 1, k)]; s1.yp = sb[TL::ocell(i, j + 1, k)];
+      s1.zm = sb[TL::ocell(i, j, k - 1)]; s1.zp = sb[TL::ocell(i, j, k + 1)];
+    }
+    const double2 cc = reinterpret_cast<const double2*>(sb)[q2];
+    s0.c = cc.x;
+    s1.c = cc.y;
+    v2d out;
+    out.x = op_value<OP>(K, s0) + rr[r].x;
+    out.y = op_value<OP>(K, s1) + rr[r].y;
+    reinterpret_cast<v2d*>(rhs)[q2] = out;
+  }
+}
+
+bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
+                            hipStream_t st) {
+  if (!tiled_nc(C.nc) || (op != OP_LPL && op != OP_HELM)) return false;
+  if (n_par == 0) return true;
+  const dim3 g(n_par);
+#define OMG_CR(NC, BS)                                                                                  \
+  if (op == OP_HELM)                                                                                    \
+    k_coarse_rhs_tile<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, lambda, parents);                          \
+  else                                                                                                  \
+    k_coarse_rhs_tile<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, lambda, parents);
+  switch (C.nc) {
+    case 16: OMG_CR(16, 512) break;
+    case 8: OMG_CR(8, 256) break;
+    case 4: OMG_CR(4, 256) break;
+    default: OMG_CR(2, 256) break;
+  }
+#undef OMG_CR
+  return true;
 }
 
 void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
