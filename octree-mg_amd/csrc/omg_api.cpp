@@ -16,6 +16,7 @@
 #include <tuple>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
@@ -816,6 +817,62 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
   }
 }
 
+// The highest level `top` such that every level lowest..top can run inside
+// the single-workgroup coarse program (launch_coarse_tail): a few boxes, all
+// on this GPU, LDS-tiled box size, no refinement boundary, and every parent
+// with all its children here.  INT_MIN when not even the lowest level can.
+int tail_top(omg_ctx* c, int max_lvl) {
+  if (c->smoother != OMG_SMOOTHER_GSRB || (c->op != OP_LPL && c->op != OP_HELM)) return INT_MIN;
+  if (max_lvl - c->lowest + 1 > kTailMaxLevels) max_lvl = c->lowest + kTailMaxLevels - 1;
+  int top = INT_MIN;
+  for (int l = c->lowest; l <= max_lvl; l++) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->n < 1 || L->n > kTailMaxBoxes || L->n != (int)c->ids[l].size() || L->has_rb ||
+        !tiled_nc(L->nc))
+      break;
+    if (l > c->lowest) {
+      Level* C = level_ptr(c, l - 1);
+      if (L->n_pairs != L->n || !((size_t)L->n == 8 * C->parents.size() || C->nc * 2 == L->nc)) break;
+    }
+    top = l;
+  }
+  return top;
+}
+
+// Levels lowest..top of the V-cycle (down-smoothing of top .. up-smoothing of
+// top) in one launch, bit-identical to the level-by-level path.
+void run_tail(omg_ctx* c, int top) {
+  TailArgs A{};
+  A.n_lvls = top - c->lowest + 1;
+  for (int l = c->lowest; l <= top; l++) {
+    Level* L = level_ptr(c, l);
+    if (L->shift_pending) {
+      if (L->all_parents && l < top) L->shift_pending = false;   // overwritten by the restriction
+      else materialize_level(c, L);
+    }
+    TailLevel& T = A.lv[l - c->lowest];
+    T.L = L->view();
+    T.bc = bc_for(c, l, 1);
+    T.parents = L->d_parents;
+    T.n_par = (int)L->parents.size();
+    T.parent_local = L->d_parent_local;
+    T.dixp = L->d_dix;
+  }
+  A.lambda = c->lambda;
+  A.n_down = c->n_cycle_down;
+  A.n_up = c->n_cycle_up;
+  A.max_coarse = c->max_coarse_cycles;
+  A.res_abs = c->res_abs;
+  A.res_rel = c->res_rel;
+  A.maxbits = (unsigned long long*)c->d_scalar;
+  A.coarse_its = (int*)(c->d_scalar + 1);
+  {
+    Prof p(c, "coarse_tail", 0.0, top);
+    launch_coarse_tail(A, c->op, c->stream);
+  }
+  for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
+}
+
 // mg_fas_vcycle (m_multigrid.f90:150-243)
 double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalone) {
   const bool has_highest = highest_lvl >= c->lowest;
@@ -844,12 +901,17 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
       fill_gc_lvl(c, max_lvl, 1);
     }
   }
+  const int top = tail_top(c, max_lvl);
+  const bool tail = top >= min_lvl && !c->no_tail;
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
+    if (tail && l <= top) break;
     smooth_boxes(c, l, c->n_cycle_down);
     update_coarse(c, l);
   }
-  // coarse grid: all its boxes live on one rank (error stop otherwise, :197-200)
-  {
+  if (tail) {
+    run_tail(c, top);
+  } else {
+    // coarse grid: all its boxes live on one rank (error stop otherwise, :197-200)
     const auto& ids = c->ids[min_lvl];
     for (int id : ids)
       if (c->rank_of[id - 1] != c->rank_of[ids[0] - 1])
@@ -861,7 +923,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
       if (res < c->res_rel * init_res || res < c->res_abs) break;
     }
   }
-  for (int l = min_lvl + 1; l <= max_lvl; l++) {
+  for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
     correct_and_fill(c, l - 1);
     smooth_boxes(c, l, c->n_cycle_up);
   }
@@ -1190,6 +1252,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->device = device;
     c->rank = rank;
     c->n_ranks = n_ranks;
+    c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));

@@ -6,6 +6,49 @@
 
 namespace omg {
 
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2d ld_nt(const double* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+}
+__device__ __forceinline__ void st_nt(double* p, double x, double y) {
+  v2d t = {x, y};
+  __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(p));
+}
+
+// The seven stencil values of two neighbouring same-colour cells of one row
+// (colour indices ih, ih+1, ih even) of colour e, from a stored box in LDS:
+// `so` = the other colour's interior, `gb` = the other colour's half of ghost
+// face 1, consecutive faces `fstride` apart.  Five 16-B and one 8-B LDS read.
+template <int NC>
+__device__ __forceinline__ void pair_stencil(const double* so, const double* gb, int fstride, int e, int q,
+                                             Nbr7& s0, Nbr7& s1) {
+  constexpr int H = NC / 2;
+  const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+  const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
+  const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
+  const int xgi = ((j - 1) >> 1) + H * (k - 1);
+  const double xs = *(p ? (ih + 2 == H ? gb + fstride + xgi : so + ih + 2 + H * row)
+                        : (ih == 0 ? gb + xgi : so + ih - 1 + H * row));
+  const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
+                                                           : gb + 2 * fstride + ih + H * (k - 1));
+  const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
+                                                            : gb + 3 * fstride + ih + H * (k - 1));
+  const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
+                                                           : gb + 4 * fstride + ih + H * (j - 1));
+  const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
+                                                            : gb + 5 * fstride + ih + H * (j - 1));
+  s0.xm = p ? xc.x : xs;
+  s0.xp = p ? xc.y : xc.x;
+  s1.xm = p ? xc.y : xc.x;
+  s1.xp = p ? xs : xc.y;
+  s0.ym = ym.x; s1.ym = ym.y;
+  s0.yp = yp.x; s1.yp = yp.y;
+  s0.zm = zm.x; s1.zm = zm.y;
+  s0.zp = zp.x; s1.zp = zp.y;
+}
+
+
 // Bijective blockIdx -> box map giving each XCD one contiguous run of boxes
 // (workgroups are dealt round-robin over the 8 XCDs), so Morton-close
 // neighbour boxes share an L2.  Speed only, never correctness.
@@ -71,6 +114,72 @@ __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const 
       const int gi = TL::ogh(nb, a, c);
       u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, sb[TL::oint(i2, j2, k2)]);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Face work shared by the ghost fill and the smoother epilogue: everything the
+// reference's mg_fill_ghost_cells_lvl does for face nb of box b at (a, c)
+// (m_ghost_cells.f90:131-175, 232-285).  `colours`: bit e set = the cells of
+// colour e changed since the last fill (same-GPU neighbours receive those).
+__device__ __forceinline__ void face_cell_fill(const LevelView& L, int iv, int b, int nb, int a, int c,
+                                               int colours, const LevelView& C, const RBRec* rb,
+                                               const GcBC& bc, double* sendbuf) {
+  const int nc = L.nc;
+  const long long f = (long long)b * 6 + nb - 1;
+  const int kind = L.nbk[f], arg = L.nba[f];
+  const bool low = nb & 1;
+  const int x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
+  double* u = boxp(L, iv, b);
+  if (kind == NB_LOCAL) {
+    // copy_from_nb, done by the box that owns the data (push)
+    if (!((colours >> ((x1 + a + c) & 1)) & 1)) return;
+    boxp(L, iv, arg)[off_gh(L, low ? nb + 1 : nb - 1, a, c)] = u[off_face_cell(L, nb, x1, a, c)];
+  } else if (kind == NB_REMOTE) {
+    // buffer_for_nb (m_ghost_cells.f90:348-383): the whole face travels
+    sendbuf[(long long)L.sendpos[f] * nc * nc + (a - 1) + (long long)nc * (c - 1)] =
+        u[off_face_cell(L, nb, x1, a, c)];
+  } else if (kind == NB_PHYS) {
+    // box_set_gc + bc_to_gc (m_ghost_cells.f90:264-283, 665-766)
+    const int gi = off_gh(L, nb, a, c);
+    double bv;
+    int type;
+    if (bc.phi_stored && iv == 1) {
+      bv = boxp(L, 2, b)[gi];
+      type = arg;
+    } else if (bc.face_off && bc.face_off[f] >= 0) {
+      bv = bc.face_data[bc.face_off[f] + (a - 1) + (long long)nc * (c - 1)];
+      type = bc.face_type[f];
+    } else {
+      bv = bc.value[nb - 1];
+      type = bc.type[nb - 1];
+    }
+    double c0, c1, c2;
+    if (type == -10) {
+      c0 = 2; c1 = -1; c2 = 0;
+    } else if (type == -11) {
+      c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
+    } else {
+      c0 = 0; c1 = 2; c2 = -1;
+    }
+    u[gi] = c0 * bv + c1 * u[off_face_cell(L, nb, x1, a, c)] + c2 * u[off_face_cell(L, nb, x2, a, c)];
+  } else if (kind == NB_RB) {
+    // refinement boundary: box_gc_for_fine_neighbor + sides_rb
+    // (m_ghost_cells.f90:287-328, 500-577, 769-861)
+    const RBRec R = rb[arg];
+    const double* cu = boxp(C, iv, R.coarse_idx);
+    const int d = (nb + 1) >> 1;
+    const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;  // tangential dims (0-based)
+    const int clayer = low ? nc : 1;                          // coarse face toward us
+    const int i = (a + 1) >> 1, j = (c + 1) >> 1;
+    auto T = [&](int p, int q) { return cu[off_face_cell(C, nb, clayer, R.dix[t1] + p, R.dix[t2] + q)]; };
+    const double tc = T(i, j);
+    const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
+    const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
+    double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
+    gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
+    u[off_gh(L, nb, a, c)] = 0.5 * gv + 0.75 * u[off_face_cell(L, nb, x1, a, c)] -
+                             0.25 * u[off_face_cell(L, nb, x2, a, c)];
   }
 }
 

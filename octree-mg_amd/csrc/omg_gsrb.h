@@ -1,0 +1,173 @@
+// omg_gsrb.h — the red-black substep of one 16^3 (or 8, 4, 2) box, as a device
+// function of a workgroup: used by k_gsrb_tile (omg_sweep.hip) and by the
+// single-workgroup coarse-level program (omg_tiles.hip).
+#pragma once
+
+#include "omg_face.h"
+
+namespace omg {
+
+// LDS doubles gsrb_box<NC> needs
+template <int NC>
+constexpr int gsrb_lds() { return 2 * (NC / 2) * NC * NC + 6 * (NC / 2) * NC; }
+
+// One substep on box b (the workgroup's BS threads), LDS at `lds`.
+template <int NC, int OP, int BS, int NT>
+__device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int e, int colours, const GcBC& bc,
+                                         double* __restrict__ sendbuf, const double* __restrict__ shift, int b,
+                                         double* lds) {
+  constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
+  constexpr int NP2 = (HV / 2 + BS - 1) / BS;  // double2 cell pairs per thread
+  double* so = lds;                            // colour 1-e of the interior
+  double* se = lds + HV;                       // colour e, updated
+  double* sg = lds + 2 * HV;                   // colour 1-e halves of the ghost faces
+  const int tid = threadIdx.x, o = 1 - e;
+  const long long boff = (long long)b * L.stride;
+  double* __restrict__ u = L.phi + boff;
+  const double* __restrict__ f = L.data + L.vstride + boff;
+  const OpCoef<OP> K(L, lambda);
+
+  // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
+  {
+    const v2d* src = reinterpret_cast<const v2d*>(u + o * HV);
+    v2d* dst = reinterpret_cast<v2d*>(so);
+    const double m = shift ? *shift : 0.0;
+    for (int q = tid; q < HV / 2; q += BS) {
+      v2d x = NT >= 2 ? __builtin_nontemporal_load(src + q) : src[q];
+      if (shift) {
+        x.x = x.x - m;
+        x.y = x.y - m;
+      }
+      dst[q] = x;
+    }
+    for (int q = tid; q < 3 * FH; q += BS) {   // 6 faces x FH/2 double2
+      const int nb = q / (FH / 2), r = q % (FH / 2);
+      const v2d* gp = reinterpret_cast<const v2d*>(u + 2 * HV + nb * FS + o * FH) + r;
+      v2d x = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
+      if (shift) {
+        x.x = x.x - m;
+        x.y = x.y - m;
+      }
+      reinterpret_cast<v2d*>(sg + nb * FH)[r] = x;
+    }
+  }
+  double2 fr[NP2];
+#pragma unroll
+  for (int r = 0; r < NP2; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 < HV / 2) {
+      const double2* fp = reinterpret_cast<const double2*>(f + e * HV) + q2;
+      if (NT) {
+        const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(fp));
+        fr[r] = make_double2(t.x, t.y);
+      } else {
+        fr[r] = *fp;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- colour e update ----------------------------------------------------
+  // Each thread updates two neighbouring cells of one row (colour indices ih,
+  // ih+1 with ih even; NC >= 4).  Their y/z neighbours are aligned
+  // colour-(1-e) pairs and their x neighbours one aligned pair plus one single
+  // value: five 16-B and one 8-B LDS read per two cells, the lanes of a wave
+  // on consecutive 16-B slots.
+#pragma unroll
+  for (int r = 0; r < NP2; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 >= HV / 2) continue;
+    double2 nv;
+    if constexpr (H % 2 == 0) {
+      const int q = 2 * q2, ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+      const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
+      const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
+      const int xgi = ((j - 1) >> 1) + H * (k - 1);   // x ghosts of this row
+      const double* xs_ptr = p ? (ih + 2 == H ? sg + FH + xgi : so + ih + 2 + H * row)
+                               : (ih == 0 ? sg + xgi : so + ih - 1 + H * row);
+      const double xs = *xs_ptr;
+      const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
+                                                               : sg + 2 * FH + ih + H * (k - 1));
+      const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
+                                                                : sg + 3 * FH + ih + H * (k - 1));
+      const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
+                                                               : sg + 4 * FH + ih + H * (j - 1));
+      const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
+                                                                : sg + 5 * FH + ih + H * (j - 1));
+      Nbr7 s0, s1;
+      s0.xm = p ? xc.x : xs;
+      s0.xp = p ? xc.y : xc.x;
+      s1.xm = p ? xc.y : xc.x;
+      s1.xp = p ? xs : xc.y;
+      s0.ym = ym.x; s1.ym = ym.y;
+      s0.yp = yp.x; s1.yp = yp.y;
+      s0.zm = zm.x; s1.zm = zm.y;
+      s0.zp = zp.x; s1.zp = zp.y;
+      nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));
+    } else {   // NC == 2: one cell per row
+      double v[2];
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const int q = 2 * q2 + s;
+        const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+        const int i = 2 * ih + 1 + ((1 + j + k + e) & 1);
+        const int tj = (i - 1) >> 1;
+        Nbr7 st;
+        st.xm = i > 1 ? so[((i - 2) >> 1) + H * row] : sg[0 * FH + ((j - 1) >> 1) + H * (k - 1)];
+        st.xp = i < NC ? so[(i >> 1) + H * row] : sg[1 * FH + ((j - 1) >> 1) + H * (k - 1)];
+        st.ym = j > 1 ? so[tj + H * (row - 1)] : sg[2 * FH + tj + H * (k - 1)];
+        st.yp = j < NC ? so[tj + H * (row + 1)] : sg[3 * FH + tj + H * (k - 1)];
+        st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
+        st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
+        v[s] = gs_value<OP>(K, st, s ? fr[r].y : fr[r].x);
+      }
+      nv = make_double2(v[0], v[1]);
+    }
+    reinterpret_cast<double2*>(se)[q2] = nv;
+    double2* up = reinterpret_cast<double2*>(u + e * HV) + q2;
+    if (NT) {
+      v2d t = {nv.x, nv.y};
+      __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(up));
+    } else
+      *up = nv;
+  }
+  __syncthreads();
+
+  // ---- ghost fill after the substep ---------------------------------------
+  for (int p = tid; p < 6 * NC * NC; p += BS) {
+    const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
+    const int a = cell % NC + 1, c = cell / NC + 1;
+    const long long fidx = (long long)b * 6 + nb - 1;
+    const int kind = L.nbk[fidx], arg = L.nba[fidx];
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1;
+    // boundary cell x1 (and x2) of this face: colour and index
+    const int x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
+    int i1, j1, k1;
+    if (d == 1) { i1 = x1; j1 = a; k1 = c; }
+    else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
+    else { i1 = a; j1 = c; k1 = x1; }
+    const int c1 = (i1 + j1 + k1) & 1;
+    const int idx1 = ((i1 - 1) >> 1) + H * ((j1 - 1) + NC * (k1 - 1));
+    const double v1 = c1 == e ? se[idx1] : so[idx1];
+    if (kind == NB_LOCAL) {
+      if ((colours >> c1) & 1) {
+        double* gp = L.phi + (long long)arg * L.stride + off_gh(L, low ? nb + 1 : nb - 1, a, c);
+        if (NT >= 2)
+          __builtin_nontemporal_store(v1, gp);
+        else
+          *gp = v1;
+      }
+    } else if (kind == NB_REMOTE) {
+      sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
+    } else {  // NB_PHYS (refinement boundaries take the generic kernel)
+      const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
+      const int idx2 = ((i2 - 1) >> 1) + H * ((j2 - 1) + NC * (k2 - 1));
+      const double v2 = c1 == e ? so[idx2] : se[idx2];   // x2 has the other colour
+      const int gi = off_gh(L, nb, a, c);
+      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, v2);
+    }
+  }
+}
+
+}  // namespace omg

@@ -200,7 +200,8 @@ struct omg_ctx {
   double* d_red = nullptr;             // device reductions (get_sum / subtract_mean)
   hipStream_t stream2 = nullptr;       // side stream (rhs sum chain)
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_phi = nullptr;
-  bool phi_mean_on_side = false;       // the pending phi mean is still being finished on stream2
+  bool phi_mean_on_side = false;
+  bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)       // the pending phi mean is still being finished on stream2
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

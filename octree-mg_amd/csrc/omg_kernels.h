@@ -61,6 +61,32 @@ void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t 
 void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st);
 void launch_phi_bc_store(const LevelView& L, const GcBC& bc, int* nba, hipStream_t st);
 
+// The coarse end of the V-cycle in ONE single-workgroup launch (omg_tiles.hip):
+// levels lowest..top (each a handful of boxes, all on this GPU), from the
+// down-smoothing of `top` through the coarse solve to the up-smoothing of
+// `top`, with every level step separated by a workgroup barrier instead of a
+// kernel boundary and the coarse-solve convergence test on the device.
+constexpr int kTailMaxLevels = 12;
+constexpr int kTailMaxBoxes = 1;
+struct TailLevel {
+  LevelView L;
+  GcBC bc;
+  const int* parents;      // my_parents (local indices)
+  int n_par;
+  const int* parent_local; // per box: parent's local index at lvl-1
+  const int* dixp;         // per box: packed child offset
+};
+struct TailArgs {
+  int n_lvls;              // lv[0] = lowest .. lv[n_lvls-1] = top
+  TailLevel lv[kTailMaxLevels];
+  double lambda;
+  int n_down, n_up, max_coarse;
+  double res_abs, res_rel;
+  unsigned long long* maxbits;   // device scratch
+  int* coarse_its;               // device: sweeps the coarse solve took
+};
+void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st);
+
 // LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16
 bool tiled_nc(int nc);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,

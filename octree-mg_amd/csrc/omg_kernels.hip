@@ -7,6 +7,7 @@
 // every result bit-identical to the reference CPU solver.  Reference routines
 // are cited as path:line of FermiQ/octree-mg.
 #include "omg_device.h"
+#include "omg_face.h"
 #include "omg_kernels.h"
 
 namespace omg {
@@ -21,72 +22,6 @@ static inline unsigned grid_for(long long work, int block = 256) {
 #define GRID_STRIDE(t, total)                                                       \
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < (total); \
        t += (long long)gridDim.x * blockDim.x)
-
-// ---------------------------------------------------------------------------
-// Face work shared by the ghost fill and the smoother epilogue: everything the
-// reference's mg_fill_ghost_cells_lvl does for face nb of box b at (a, c)
-// (m_ghost_cells.f90:131-175, 232-285).  `colours`: bit e set = the cells of
-// colour e changed since the last fill (same-GPU neighbours receive those).
-__device__ __forceinline__ void face_cell_fill(const LevelView& L, int iv, int b, int nb, int a, int c,
-                                               int colours, const LevelView& C, const RBRec* rb,
-                                               const GcBC& bc, double* sendbuf) {
-  const int nc = L.nc;
-  const long long f = (long long)b * 6 + nb - 1;
-  const int kind = L.nbk[f], arg = L.nba[f];
-  const bool low = nb & 1;
-  const int x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
-  double* u = boxp(L, iv, b);
-  if (kind == NB_LOCAL) {
-    // copy_from_nb, done by the box that owns the data (push)
-    if (!((colours >> ((x1 + a + c) & 1)) & 1)) return;
-    boxp(L, iv, arg)[off_gh(L, low ? nb + 1 : nb - 1, a, c)] = u[off_face_cell(L, nb, x1, a, c)];
-  } else if (kind == NB_REMOTE) {
-    // buffer_for_nb (m_ghost_cells.f90:348-383): the whole face travels
-    sendbuf[(long long)L.sendpos[f] * nc * nc + (a - 1) + (long long)nc * (c - 1)] =
-        u[off_face_cell(L, nb, x1, a, c)];
-  } else if (kind == NB_PHYS) {
-    // box_set_gc + bc_to_gc (m_ghost_cells.f90:264-283, 665-766)
-    const int gi = off_gh(L, nb, a, c);
-    double bv;
-    int type;
-    if (bc.phi_stored && iv == 1) {
-      bv = boxp(L, 2, b)[gi];
-      type = arg;
-    } else if (bc.face_off && bc.face_off[f] >= 0) {
-      bv = bc.face_data[bc.face_off[f] + (a - 1) + (long long)nc * (c - 1)];
-      type = bc.face_type[f];
-    } else {
-      bv = bc.value[nb - 1];
-      type = bc.type[nb - 1];
-    }
-    double c0, c1, c2;
-    if (type == -10) {
-      c0 = 2; c1 = -1; c2 = 0;
-    } else if (type == -11) {
-      c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
-    } else {
-      c0 = 0; c1 = 2; c2 = -1;
-    }
-    u[gi] = c0 * bv + c1 * u[off_face_cell(L, nb, x1, a, c)] + c2 * u[off_face_cell(L, nb, x2, a, c)];
-  } else if (kind == NB_RB) {
-    // refinement boundary: box_gc_for_fine_neighbor + sides_rb
-    // (m_ghost_cells.f90:287-328, 500-577, 769-861)
-    const RBRec R = rb[arg];
-    const double* cu = boxp(C, iv, R.coarse_idx);
-    const int d = (nb + 1) >> 1;
-    const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;  // tangential dims (0-based)
-    const int clayer = low ? nc : 1;                          // coarse face toward us
-    const int i = (a + 1) >> 1, j = (c + 1) >> 1;
-    auto T = [&](int p, int q) { return cu[off_face_cell(C, nb, clayer, R.dix[t1] + p, R.dix[t2] + q)]; };
-    const double tc = T(i, j);
-    const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
-    const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
-    double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
-    gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
-    u[off_gh(L, nb, a, c)] = 0.5 * gv + 0.75 * u[off_face_cell(L, nb, x1, a, c)] -
-                             0.25 * u[off_face_cell(L, nb, x2, a, c)];
-  }
-}
 
 // Ghost fill of a level: one thread per (box, face, face cell).
 __global__ void __launch_bounds__(256) k_fill_gc(LevelView L, int iv, int colours, LevelView C,

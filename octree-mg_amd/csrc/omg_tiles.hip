@@ -11,60 +11,18 @@
 //  k_box_sums3 / k_seq_sum3: get_sum (:278-294) in the reference's exact
 //    sequential order, with wide loads and the products off the add chain.
 #include "omg_face.h"
+#include "omg_gsrb.h"
 #include "omg_kernels.h"
 
 namespace omg {
 
-typedef double v2d __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ v2d ld_nt(const double* p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
-}
-__device__ __forceinline__ void st_nt(double* p, double x, double y) {
-  v2d t = {x, y};
-  __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(p));
-}
-
-// The seven stencil values of two neighbouring same-colour cells of one row
-// (colour indices ih, ih+1, ih even) of colour e, from a stored box in LDS:
-// `so` = the other colour's interior, `gb` = the other colour's half of ghost
-// face 1, consecutive faces `fstride` apart.  Five 16-B and one 8-B LDS read.
-template <int NC>
-__device__ __forceinline__ void pair_stencil(const double* so, const double* gb, int fstride, int e, int q,
-                                             Nbr7& s0, Nbr7& s1) {
-  constexpr int H = NC / 2;
-  const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
-  const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
-  const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
-  const int xgi = ((j - 1) >> 1) + H * (k - 1);
-  const double xs = *(p ? (ih + 2 == H ? gb + fstride + xgi : so + ih + 2 + H * row)
-                        : (ih == 0 ? gb + xgi : so + ih - 1 + H * row));
-  const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
-                                                           : gb + 2 * fstride + ih + H * (k - 1));
-  const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
-                                                            : gb + 3 * fstride + ih + H * (k - 1));
-  const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
-                                                           : gb + 4 * fstride + ih + H * (j - 1));
-  const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
-                                                            : gb + 5 * fstride + ih + H * (j - 1));
-  s0.xm = p ? xc.x : xs;
-  s0.xp = p ? xc.y : xc.x;
-  s1.xm = p ? xc.y : xc.x;
-  s1.xp = p ? xs : xc.y;
-  s0.ym = ym.x; s1.ym = ym.y;
-  s0.yp = yp.x; s1.yp = yp.y;
-  s0.zm = zm.x; s1.zm = zm.y;
-  s0.zp = zp.x; s1.zp = zp.y;
-}
-
 template <int NC, int OP, int BS>
-__global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
-                                                       unsigned long long* maxbits, int restrict_on,
-                                                       const int* parent_local, const int* dixp) {
+__device__ __forceinline__ void resid_restrict_box(const LevelView& F, const LevelView& Cv, double lambda,
+                                                   unsigned long long* maxbits, int restrict_on,
+                                                   const int* parent_local, const int* dixp, int b, double* sb) {
   using TL = Tl<NC>;
   constexpr int NST = TL::NST, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, HN = NC / 2;
-  __shared__ double sb[NST];
-  const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const long long boff = (long long)b * F.stride;
   const double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
@@ -146,19 +104,31 @@ __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv
   }
 }
 
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
+                                                       unsigned long long* maxbits, int restrict_on,
+                                                       const int* parent_local, const int* dixp) {
+  __shared__ double sb[Tl<NC>::NST];
+  resid_restrict_box<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp,
+                                 xcd_box(blockIdx.x, gridDim.x), sb);
+}
+
 // SUB: correct_children's `res = phi - old` on the parent (m_multigrid.f90:
 // 392-399) is formed here while the parent data is loaded; each child writes
 // the res cells of its own octant and of the parent ghost faces next to it
 // (every stored cell of the parent exactly once over its 8 children).
+template <int NC>
+constexpr int prolong_cb() { return ((NC / 2 + 2) * (NC / 2 + 2) * (NC / 2 + 2) + 1) & ~1; }
+
 template <int NC, int BS, bool SUB>
-__global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
-                                                     const int* parent_local, const int* dixp, GcBC bc,
-                                                     double* sendbuf) {
+__device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
+                                                 const int* parent_local, const int* dixp, const GcBC& bc,
+                                                 double* sendbuf, int b, double* lds) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
-  __shared__ double cb[CB * CB * CB];   // the parent's octant + one face layer around it
-  __shared__ double sb[2 * HV];         // the corrected fine interior
-  const int b = xcd_box(blockIdx.x, gridDim.x), tid = threadIdx.x;
+  double* cb = lds;                     // the parent's octant + one face layer around it
+  double* sb = lds + prolong_cb<NC>();  // the corrected fine interior
+  const int tid = threadIdx.x;
   const int pb = parent_local[b], dp = dixp[b];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
   const double* __restrict__ cu = boxp(Cv, iv, pb);
@@ -209,6 +179,14 @@ __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, 
   }
   __syncthreads();
   tile_face_fill<NC>(F, b, sb, 3, bc, sendbuf);
+}
+
+template <int NC, int BS, bool SUB>
+__global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
+                                                     const int* parent_local, const int* dixp, GcBC bc,
+                                                     double* sendbuf) {
+  __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
+  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, xcd_box(blockIdx.x, gridDim.x), lds);
 }
 
 // get_sum's per-leaf interior sums (m_multigrid.f90:286-290): one lane per
@@ -395,11 +373,11 @@ void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const i
 // per workgroup: rhs = L(phi) + res over the interior (box_op, then the sum),
 // old = phi over the whole stored box.
 template <int NC, int OP, int BS>
-__global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
+__device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambda, int b, double* sb) {
   using TL = Tl<NC>;
-  constexpr int NST = TL::NST, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, H = NC / 2;
-  __shared__ double sb[NST];
-  const int b = parents[xcd_box(blockIdx.x, gridDim.x)], tid = threadIdx.x;
+  constexpr int HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, H = NC / 2;
+  constexpr int NST = TL::NST;
+  const int tid = threadIdx.x;
   const long long boff = (long long)b * Cv.stride;
   const double* __restrict__ u = Cv.phi + boff;
   double* __restrict__ rhs = Cv.data + Cv.vstride + boff;
@@ -445,6 +423,12 @@ __global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lam
     out.y = op_value<OP>(K, s1) + rr[r].y;
     reinterpret_cast<v2d*>(rhs)[q2] = out;
   }
+}
+
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
+  __shared__ double sb[Tl<NC>::NST];
+  coarse_rhs_box<NC, OP, BS>(Cv, lambda, parents[xcd_box(blockIdx.x, gridDim.x)], sb);
 }
 
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
@@ -511,6 +495,131 @@ void launch_mean(const double* all, int n, double volume, double* mean, hipStrea
 void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
   if (n == 0) return;
   k_seq_sum3<<<1, 64, 0, st>>>(box_sums, n, w, acc);
+}
+
+// ---------------------------------------------------------------------------
+// The coarse end of mg_fas_vcycle (m_multigrid.f90:185-229) in one workgroup.
+constexpr int kTailBS = 512;
+constexpr int kTailLds = Tl<16>::NST;   // the largest box program (16^3 residual / coarse rhs)
+
+template <int OP>
+__device__ void tail_smooth(const TailArgs& A, int li, int n_cycle, double* lds) {
+  const TailLevel& T = A.lv[li];
+  for (int n = 1; n <= 2 * n_cycle; n++) {
+    const int e = n & 1;
+    for (int b = 0; b < T.L.n; b++) {
+      switch (T.L.nc) {
+        case 16: gsrb_box<16, OP, kTailBS, 0>(T.L, A.lambda, e, 1 << e, T.bc, nullptr, nullptr, b, lds); break;
+        case 8: gsrb_box<8, OP, kTailBS, 0>(T.L, A.lambda, e, 1 << e, T.bc, nullptr, nullptr, b, lds); break;
+        case 4: gsrb_box<4, OP, kTailBS, 0>(T.L, A.lambda, e, 1 << e, T.bc, nullptr, nullptr, b, lds); break;
+        default: gsrb_box<2, OP, kTailBS, 0>(T.L, A.lambda, e, 1 << e, T.bc, nullptr, nullptr, b, lds); break;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// residual over level li (+ restriction onto li-1 when restrict_on); with
+// maxbits: max |res| returned to every thread
+template <int OP>
+__device__ double tail_residual(const TailArgs& A, int li, int restrict_on, bool want_max, double* lds) {
+  const TailLevel& T = A.lv[li];
+  const LevelView C = restrict_on ? A.lv[li - 1].L : T.L;
+  unsigned long long* mb = want_max ? A.maxbits : nullptr;
+  if (want_max) {
+    if (threadIdx.x == 0) *mb = 0ull;
+    __syncthreads();
+  }
+  for (int b = 0; b < T.L.n; b++) {
+    switch (T.L.nc) {
+      case 16: resid_restrict_box<16, OP, kTailBS>(T.L, C, A.lambda, mb, restrict_on, T.parent_local, T.dixp, b, lds); break;
+      case 8: resid_restrict_box<8, OP, kTailBS>(T.L, C, A.lambda, mb, restrict_on, T.parent_local, T.dixp, b, lds); break;
+      case 4: resid_restrict_box<4, OP, kTailBS>(T.L, C, A.lambda, mb, restrict_on, T.parent_local, T.dixp, b, lds); break;
+      default: resid_restrict_box<2, OP, kTailBS>(T.L, C, A.lambda, mb, restrict_on, T.parent_local, T.dixp, b, lds); break;
+    }
+    __syncthreads();
+  }
+  if (!want_max) return 0.0;
+  const unsigned long long bits = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  return __longlong_as_double((long long)bits);
+}
+
+// mg_fill_ghost_cells_lvl of phi on level li (same-GPU faces and physical
+// boundaries only, which is all a tail level has)
+__device__ void tail_fill(const TailArgs& A, int li) {
+  const TailLevel& T = A.lv[li];
+  const int nc = T.L.nc, nc2 = nc * nc;
+  const LevelView none{};
+  for (int t = threadIdx.x; t < T.L.n * 6 * nc2; t += blockDim.x) {
+    const int cell = t % nc2, f = t / nc2;
+    face_cell_fill(T.L, 1, f / 6, f % 6 + 1, cell % nc + 1, cell / nc + 1, 3, none, nullptr, T.bc, nullptr);
+  }
+  __syncthreads();
+}
+
+template <int OP>
+__device__ void tail_coarse_rhs(const TailArgs& A, int li, double* lds) {
+  const TailLevel& T = A.lv[li];
+  for (int p = 0; p < T.n_par; p++) {
+    const int b = T.parents[p];
+    switch (T.L.nc) {
+      case 16: coarse_rhs_box<16, OP, kTailBS>(T.L, A.lambda, b, lds); break;
+      case 8: coarse_rhs_box<8, OP, kTailBS>(T.L, A.lambda, b, lds); break;
+      case 4: coarse_rhs_box<4, OP, kTailBS>(T.L, A.lambda, b, lds); break;
+      default: coarse_rhs_box<2, OP, kTailBS>(T.L, A.lambda, b, lds); break;
+    }
+    __syncthreads();
+  }
+}
+
+// correct_children(li-1) + mg_fill_ghost_cells_lvl(li): every parent's
+// children are here, so each child forms its parent's res = phi - old
+__device__ void tail_correct(const TailArgs& A, int li, double* lds) {
+  const TailLevel& T = A.lv[li];
+  const LevelView C = A.lv[li - 1].L;
+  for (int b = 0; b < T.L.n; b++) {
+    switch (T.L.nc) {
+      case 16: prolong_fill_box<16, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
+      case 8: prolong_fill_box<8, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
+      case 4: prolong_fill_box<4, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
+      default: prolong_fill_box<2, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
+    }
+    __syncthreads();
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(kTailBS) k_coarse_tail(TailArgs A) {
+  __shared__ double lds[kTailLds];
+  const int top = A.n_lvls - 1;
+  for (int li = top; li >= 1; li--) {
+    tail_smooth<OP>(A, li, A.n_down, lds);
+    tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
+    tail_fill(A, li - 1);
+    tail_coarse_rhs<OP>(A, li - 1, lds);
+  }
+  // coarse solve (m_multigrid.f90:197-208)
+  const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
+  int its = 0;
+  for (int i = 1; i <= A.max_coarse; i++) {
+    tail_smooth<OP>(A, 0, A.n_up + A.n_down, lds);
+    its = i;
+    const double res = tail_residual<OP>(A, 0, 0, true, lds);
+    if (res < A.res_rel * init_res || res < A.res_abs) break;
+  }
+  for (int li = 1; li <= top; li++) {
+    tail_correct(A, li, lds);
+    tail_smooth<OP>(A, li, A.n_up, lds);
+  }
+  if (threadIdx.x == 0) *A.coarse_its = its;
+}
+
+void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st) {
+  if (op == OP_HELM)
+    k_coarse_tail<OP_HELM><<<1, kTailBS, 0, st>>>(A);
+  else
+    k_coarse_tail<OP_LPL><<<1, kTailBS, 0, st>>>(A);
 }
 
 }  // namespace omg
