@@ -1400,11 +1400,13 @@ int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* pee
 
 int omg_set_operator(omg_ctx* c, int op, double lambda) {
   return guarded([&] {
-    if (op != OMG_LAPLACIAN && op != OMG_HELMHOLTZ && op != OMG_AHELMHOLTZ)
-      throw OmgError("mg_set_methods: unsupported operator");
+    if (op < OMG_LAPLACIAN || op > OMG_AHELMHOLTZ) throw OmgError("mg_set_methods: unknown operator");
     if (lambda < 0) throw OmgError("helmholtz_set_lambda: lambda < 0 not allowed");
     if (op == OMG_AHELMHOLTZ && c->n_vars < 7 && c->n_boxes > 0)
       throw OmgError("ahelmholtz_set_methods: needs 3 extra variables");
+    if ((op == OMG_VLAPLACIAN || op == OMG_VHELMHOLTZ) && c->n_vars < 5 && c->n_boxes > 0)
+      throw OmgError("vlaplacian/vhelmholtz_set_methods: mg%n_extra_vars == 0");
+    if (op == OMG_VLAPLACIAN) lambda = 0.0;
     c->op = op;
     c->lambda = lambda;
   });

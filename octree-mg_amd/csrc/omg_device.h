@@ -162,15 +162,21 @@ __device__ __forceinline__ double gs_value(const OpCoef<OP>& K, const Nbr7& s, d
   return K.fac * (K.ix * (s.xp + s.xm) + K.iy * (s.yp + s.ym) + K.iz * (s.zp + s.zm) - f);
 }
 
+// Operators with a cell coefficient: harmonic face means of eps.
 // box_ahelmh (m_ahelmholtz.f90:215-234) and box_gs_ahelmh with the 3D a0(5:6)
-// index fixed (:143-156): harmonic face means of eps1..3 (vars 5..7)
+// index fixed (:143-156) use eps1..3 (vars 5..7, one per direction);
+// box_vlpl / box_gs_vlpl (m_vlaplacian.f90:51-189) and box_vhelmh /
+// box_gs_vhelmh (m_vhelmholtz.f90:61-205) one eps (var 5) for all.
+constexpr bool is_varop(int OP) { return OP == OP_AHELM || OP == OP_VLPL || OP == OP_VHELM; }
+
 struct AEps {
   double a0[3], a[6];
 };
+template <int OP>
 __device__ __forceinline__ AEps load_eps(const LevelView& L, int b, int i, int j, int k) {
   const double* e1 = boxp(L, 5, b);
-  const double* e2 = boxp(L, 6, b);
-  const double* e3 = boxp(L, 7, b);
+  const double* e2 = boxp(L, OP == OP_AHELM ? 6 : 5, b);
+  const double* e3 = boxp(L, OP == OP_AHELM ? 7 : 5, b);
   AEps E;
   const int o = off_int(L, i, j, k);
   E.a0[0] = e1[o];
@@ -195,6 +201,7 @@ __device__ __forceinline__ double aop_value(const OpCoef<OP>& K, const Nbr7& s, 
     const double a0 = E.a0[q >> 1];
     acc += 2 * i2[q] * a0 * E.a[q] / (a0 + E.a[q]) * (uu[q] - s.c);
   }
+  if (OP == OP_VLPL) return acc;
   return acc - K.lambda * s.c;
 }
 
@@ -212,6 +219,7 @@ __device__ __forceinline__ double ags_value(const OpCoef<OP>& K, const Nbr7& s, 
   for (int q = 0; q < 6; q++) scu += cc[q] * uu[q];
 #pragma unroll
   for (int q = 0; q < 6; q++) sc += cc[q];
+  if (OP == OP_VLPL) return (scu - f) / sc;
   return (scu - f) / (sc + K.lambda);
 }
 

@@ -111,8 +111,8 @@ __global__ void __launch_bounds__(256) k_gs_sub(LevelView L, double lambda, int 
       if (i > nc) continue;
       const int o = e * L.hv + q;
       const Nbr7 s = load7(L, u, i, j, k);
-      if (OP == OP_AHELM)
-        u[o] = ags_value<OP>(K, s, load_eps(L, b, i, j, k), f[o]);
+      if (is_varop(OP))
+        u[o] = ags_value<OP>(K, s, load_eps<OP>(L, b, i, j, k), f[o]);
       else
         u[o] = gs_value<OP>(K, s, f[o]);
     }
@@ -142,8 +142,8 @@ __global__ void __launch_bounds__(256) k_gs_lex(LevelView L, double lambda) {
         if (i < 1 || i > nc) continue;
         const int o = off_int(L, i, j, k);
         const Nbr7 s = load7(L, u, i, j, k);
-        if (OP == OP_AHELM)
-          u[o] = ags_value<OP>(K, s, load_eps(L, b, i, j, k), f[o]);
+        if (is_varop(OP))
+          u[o] = ags_value<OP>(K, s, load_eps<OP>(L, b, i, j, k), f[o]);
         else
           u[o] = gs_value<OP>(K, s, f[o]);
       }
@@ -156,7 +156,7 @@ template <int OP>
 __device__ __forceinline__ double apply_op(const LevelView& L, const OpCoef<OP>& K, int b, int i, int j,
                                            int k) {
   const Nbr7 s = load7(L, boxp(L, 1, b), i, j, k);
-  if (OP == OP_AHELM) return aop_value<OP>(K, s, load_eps(L, b, i, j, k));
+  if (is_varop(OP)) return aop_value<OP>(K, s, load_eps<OP>(L, b, i, j, k));
   return op_value<OP>(K, s);
 }
 
@@ -457,6 +457,8 @@ void launch_phi_bc_store(const LevelView& L, const GcBC& bc, int* nba, hipStream
   switch (op) {                                                                  \
     case OP_HELM: KERNEL<OP_HELM><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); break;   \
     case OP_AHELM: KERNEL<OP_AHELM><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); break; \
+    case OP_VLPL: KERNEL<OP_VLPL><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); break;   \
+    case OP_VHELM: KERNEL<OP_VHELM><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); break; \
     default: KERNEL<OP_LPL><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); break;         \
   }
 

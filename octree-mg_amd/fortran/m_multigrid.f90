@@ -19,7 +19,9 @@
 !> boundary_cond callback is tabulated on every physical face of every box of
 !> this rank at each call (the reference evaluates it at each ghost fill, with
 !> the same arguments).  Custom refinement_bnd callbacks, non-Cartesian
-!> geometry and NDIM /= 3 are rejected with error stop.
+!> geometry and NDIM /= 3 are rejected with error stop.  All five operators
+!> of the reference run on the GPU (Laplacian, Helmholtz and their variable-
+!> coefficient forms via the generic kernels; aniso-Helmholtz likewise).
 module m_multigrid
   use iso_c_binding
   use mpi
@@ -268,6 +270,7 @@ contains
   !> Methods, boundary conditions and all data of this rank onto the device.
   subroutine to_device(mg)
     use m_helmholtz, only: helmholtz_lambda
+    use m_vhelmholtz, only: vhelmholtz_lambda
     use m_ahelmholtz, only: ahelmholtz_lambda
     type(mg_t), intent(inout) :: mg
     real(c_double)            :: lambda
@@ -277,14 +280,16 @@ contains
     call mg_timer_start(mg%timers(timer_host_to_dev))
 
     select case (mg%operator_type)
-    case (mg_laplacian)
+    case (mg_laplacian, mg_vlaplacian)
        lambda = 0.0_dp
     case (mg_helmholtz)
        lambda = helmholtz_lambda
+    case (mg_vhelmholtz)
+       lambda = vhelmholtz_lambda
     case (mg_ahelmholtz)
        lambda = ahelmholtz_lambda
     case default
-       error stop "octree-mg GPU backend: operator not supported on the GPU yet"
+       error stop "octree-mg GPU backend: unknown operator"
     end select
     call omg_ok(omg_set_operator(ctx, int(mg%operator_type, c_int), lambda), "set_operator")
     call omg_ok(omg_set_smoother(ctx, int(mg%smoother_type, c_int), &

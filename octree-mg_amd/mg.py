@@ -25,7 +25,7 @@ import os
 import numpy as np
 
 from . import device
-from .tree import (MG_AHELMHOLTZ, MG_BC_DIRICHLET, MG_CARTESIAN, MG_HELMHOLTZ,
+from .tree import (MG_AHELMHOLTZ, MG_VHELMHOLTZ, MG_VLAPLACIAN, MG_BC_DIRICHLET, MG_CARTESIAN, MG_HELMHOLTZ,
                    MG_IPHI, MG_LAPLACIAN, MG_NO_BOX, MG_NUM_VARS,
                    MG_SMOOTHER_GS, MG_SMOOTHER_GSRB, MGTree)
 
@@ -159,6 +159,13 @@ def mg_set_methods(mg: MG):
             mg.subtract_mean = True
     elif mg.operator_type == MG_HELMHOLTZ:
         mg.subtract_mean = False
+    elif mg.operator_type in (MG_VLAPLACIAN, MG_VHELMHOLTZ):
+        # vlaplacian_set_methods / vhelmholtz_set_methods (m_vlaplacian.f90:13-49,
+        # m_vhelmholtz.f90:19-49): eps in var 5 with Neumann-0 ghosts
+        mg.n_extra_vars = max(1, mg.n_extra_vars)
+        mg.subtract_mean = False
+        for nb in range(1, 7):
+            mg.bc[nb][5] = BC(-11, 0.0)
     elif mg.operator_type == MG_AHELMHOLTZ:
         mg.n_extra_vars = max(3, mg.n_extra_vars)
         for nb in range(1, 7):

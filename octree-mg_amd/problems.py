@@ -57,6 +57,24 @@ def level_solution(tree, lvl: int, ids=None) -> np.ndarray:
     return (s[0][:, None, None, :] * s[1][:, None, :, None]) * s[2][:, :, None, None]
 
 
+TWO_PI = 2.0 * PI
+
+
+def level_eps(tree, lvl: int, ids=None) -> np.ndarray:
+    """The coefficient of the golden v-operator runs on every box of a level,
+    incl. ghosts: eps = (1.5 + sin(2 pi x)) * (1.5 + sin(2 pi y)) * (1.5 +
+    sin(2 pi z)) (oracle/omg_golden.f90 set_eps), [box, k, j, i]."""
+    ids = np.asarray(tree.lvls[lvl].ids if ids is None else ids, dtype=np.int64)
+    nc = tree.box_size_lvl[lvl]
+    if len(ids) == 0:
+        return np.zeros((0, nc + 2, nc + 2, nc + 2))
+    dr = tree.dr[lvl]
+    idx = np.arange(0, nc + 2, dtype=np.float64) - 0.5
+    rmin = tree.box_r_min[ids]
+    f = [1.5 + np.sin(TWO_PI * (rmin[:, d:d + 1] + idx[None, :] * dr[d])) for d in range(3)]
+    return (f[0][:, None, None, :] * f[1][:, None, :, None]) * f[2][:, :, None, None]
+
+
 def callback_bc_faces(tree, boxes=None):
     """Tabulate the Dirichlet-u callback for every physical face of every box.
 

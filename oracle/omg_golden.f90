@@ -18,7 +18,7 @@
 !   omg_golden box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres dump
 !     cycle    v | f
 !     smoother gs | gsrb
-!     op       lpl | helm
+!     op       lpl | helm | vlpl | vhelm   (v*: coefficient eps in var 5, solution in 6)
 !     bc       sol (callback Dirichlet u) | d0 (Dirichlet 0) | per (periodic)
 !              | n0 (Neumann 0) | c0 (continuous)
 !     rhs      sol (rhs = L u) | one (rhs = 1)
@@ -71,6 +71,16 @@ program omg_golden
   if (trim(a_op) == "helm") then
      mg%operator_type = mg_helmholtz
      call helmholtz_set_lambda(lambda)
+  else if (trim(a_op) == "vlpl" .or. trim(a_op) == "vhelm") then
+     ! variable coefficient eps in mg_iveps (= 5): the solution moves to 6
+     mg%n_extra_vars = 2
+     i_sol = mg_num_vars + 2
+     if (trim(a_op) == "vlpl") then
+        mg%operator_type = mg_vlaplacian
+     else
+        mg%operator_type = mg_vhelmholtz
+        call vhelmholtz_set_lambda(lambda)
+     end if
   else
      mg%operator_type = mg_laplacian
   end if
@@ -112,6 +122,7 @@ program omg_golden
   if (trim(a_lb) == "lbp") call mg_load_balance_parents(mg)
   call mg_allocate_storage(mg)
 
+  if (mg%operator_type == mg_vlaplacian .or. mg%operator_type == mg_vhelmholtz) call set_eps(mg)
   if (trim(a_rhs) == "sol") then
      call set_solution(mg, n_levels > 1)
      call compute_rhs_and_reset(mg)
@@ -173,6 +184,25 @@ contains
        call mg_fill_ghost_cells(mg, i_sol)
     end if
   end subroutine set_solution
+
+  ! eps = (1.5 + sin(2 pi x)) (1.5 + sin(2 pi y)) (1.5 + sin(2 pi z)) on every
+  ! cell incl. ghosts of every level (products only: no contraction)
+  subroutine set_eps(mg)
+    type(mg_t), intent(inout) :: mg
+    integer                   :: n, id, lvl, nc, IJK
+    real(dp)                  :: r(NDIM)
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       nc = mg%box_size_lvl(lvl)
+       do n = 1, size(mg%lvls(lvl)%my_ids)
+          id = mg%lvls(lvl)%my_ids(n)
+          do KJI_DO(0, nc+1)
+             r = mg%boxes(id)%r_min + ([IJK] - 0.5_dp) * mg%dr(:, lvl)
+             mg%boxes(id)%cc(IJK, mg_iveps) = (1.5_dp + sin(2 * pi * r(1))) * &
+                  (1.5_dp + sin(2 * pi * r(2))) * (1.5_dp + sin(2 * pi * r(3)))
+          end do; CLOSE_DO
+       end do
+    end do
+  end subroutine set_eps
 
   subroutine compute_rhs_and_reset(mg)
     type(mg_t), intent(inout) :: mg

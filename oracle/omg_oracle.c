@@ -430,6 +430,12 @@ static void box_gs_const(orc_mg *mg, int id, int nc, int cntr) {
  * evident intent a0(5:6) = eps3 (as the operator box_ahelmh, line 221, does).
  * Parity for this smoother is therefore unpinned against the reference. */
 static void box_gs_ahelm(orc_mg *mg, int id, int nc, int cntr) {
+    /* m_vlaplacian / m_vhelmholtz (src/m_vlaplacian.f90:51-131,
+     * src/m_vhelmholtz.f90:61-141) are the same update with one coefficient
+     * eps (var 5) for all directions; vlaplacian divides by sum(c) alone. */
+    const int v = (mg->op == ORC_AHELMHOLTZ);
+    const int e1 = 5, e2 = v ? 6 : 5, e3 = v ? 7 : 5;
+    const double lam = (mg->op == ORC_VLAPLACIAN) ? 0.0 : mg->lambda;
     double idr2[6];
     const double *d = DRL(mg, mg->lvl[id - 1]);
     for (int q = 0; q < 3; q++) idr2[2 * q] = idr2[2 * q + 1] = 1 / (d[q] * d[q]);
@@ -439,55 +445,64 @@ static void box_gs_ahelm(orc_mg *mg, int id, int nc, int cntr) {
             if (rb) i0 = 2 - ((cntr ^ (k + j)) & 1);
             for (int i = i0; i <= nc; i += di) {
                 double a0[6], a[6], u[6], c[6];
-                a0[0] = a0[1] = CC(id, nc, i, j, k, 5);
-                a0[2] = a0[3] = CC(id, nc, i, j, k, 6);
-                a0[4] = a0[5] = CC(id, nc, i, j, k, 7);
+                a0[0] = a0[1] = CC(id, nc, i, j, k, e1);
+                a0[2] = a0[3] = CC(id, nc, i, j, k, e2);
+                a0[4] = a0[5] = CC(id, nc, i, j, k, e3);
                 u[0] = CC(id, nc, i - 1, j, k, 1); u[1] = CC(id, nc, i + 1, j, k, 1);
-                a[0] = CC(id, nc, i - 1, j, k, 5); a[1] = CC(id, nc, i + 1, j, k, 5);
+                a[0] = CC(id, nc, i - 1, j, k, e1); a[1] = CC(id, nc, i + 1, j, k, e1);
                 u[2] = CC(id, nc, i, j - 1, k, 1); u[3] = CC(id, nc, i, j + 1, k, 1);
-                a[2] = CC(id, nc, i, j - 1, k, 6); a[3] = CC(id, nc, i, j + 1, k, 6);
+                a[2] = CC(id, nc, i, j - 1, k, e2); a[3] = CC(id, nc, i, j + 1, k, e2);
                 u[4] = CC(id, nc, i, j, k - 1, 1); u[5] = CC(id, nc, i, j, k + 1, 1);
-                a[4] = CC(id, nc, i, j, k - 1, 7); a[5] = CC(id, nc, i, j, k + 1, 7);
+                a[4] = CC(id, nc, i, j, k - 1, e3); a[5] = CC(id, nc, i, j, k + 1, e3);
                 double scu = 0.0, sc = 0.0;
                 for (int q = 0; q < 6; q++) c[q] = 2 * a0[q] * a[q] / (a0[q] + a[q]) * idr2[q];
                 for (int q = 0; q < 6; q++) scu += c[q] * u[q];
                 for (int q = 0; q < 6; q++) sc += c[q];
-                CC(id, nc, i, j, k, 1) = (scu - CC(id, nc, i, j, k, 2)) / (sc + mg->lambda);
+                if (mg->op == ORC_VLAPLACIAN)
+                    CC(id, nc, i, j, k, 1) = (scu - CC(id, nc, i, j, k, 2)) / sc;
+                else
+                    CC(id, nc, i, j, k, 1) = (scu - CC(id, nc, i, j, k, 2)) / (sc + lam);
             }
         }
 }
 
 void orc_box_smoother(orc_mg *mg, int id, int cntr) {
     int nc = box_nc(mg, id);
-    if (mg->op == ORC_AHELMHOLTZ) box_gs_ahelm(mg, id, nc, cntr);
-    else box_gs_const(mg, id, nc, cntr);
+    if (mg->op == ORC_AHELMHOLTZ || mg->op == ORC_VLAPLACIAN || mg->op == ORC_VHELMHOLTZ)
+        box_gs_ahelm(mg, id, nc, cntr);
+    else
+        box_gs_const(mg, id, nc, cntr);
 }
 
-/* box_lpl / box_helmh / box_ahelmh (reference: src/m_laplacian.f90:155-195,
- * src/m_helmholtz.f90:111-154, src/m_ahelmholtz.f90:165-237). */
+/* box_lpl / box_helmh / box_ahelmh / box_vlpl / box_vhelmh (reference:
+ * src/m_laplacian.f90:155-195, src/m_helmholtz.f90:111-154,
+ * src/m_ahelmholtz.f90:165-237, src/m_vlaplacian.f90:134-189,
+ * src/m_vhelmholtz.f90:144-205). */
 void orc_box_op(orc_mg *mg, int id, int i_out) {
     int nc = box_nc(mg, id);
     double idr2[3];
     idr2_of(mg, mg->lvl[id - 1], idr2);
-    if (mg->op == ORC_AHELMHOLTZ) {
+    if (mg->op == ORC_AHELMHOLTZ || mg->op == ORC_VLAPLACIAN || mg->op == ORC_VHELMHOLTZ) {
+        const int v = (mg->op == ORC_AHELMHOLTZ);
+        const int e1 = 5, e2 = v ? 6 : 5, e3 = v ? 7 : 5;
         double i2[6];
         for (int q = 0; q < 3; q++) i2[2 * q] = i2[2 * q + 1] = idr2[q];
         for (int k = 1; k <= nc; k++)
             for (int j = 1; j <= nc; j++)
                 for (int i = 1; i <= nc; i++) {
                     double u0 = CC(id, nc, i, j, k, 1), a0[6], u[6], a[6];
-                    a0[0] = a0[1] = CC(id, nc, i, j, k, 5);
-                    a0[2] = a0[3] = CC(id, nc, i, j, k, 6);
-                    a0[4] = a0[5] = CC(id, nc, i, j, k, 7);
+                    a0[0] = a0[1] = CC(id, nc, i, j, k, e1);
+                    a0[2] = a0[3] = CC(id, nc, i, j, k, e2);
+                    a0[4] = a0[5] = CC(id, nc, i, j, k, e3);
                     u[0] = CC(id, nc, i - 1, j, k, 1); u[1] = CC(id, nc, i + 1, j, k, 1);
                     u[2] = CC(id, nc, i, j - 1, k, 1); u[3] = CC(id, nc, i, j + 1, k, 1);
                     u[4] = CC(id, nc, i, j, k - 1, 1); u[5] = CC(id, nc, i, j, k + 1, 1);
-                    a[0] = CC(id, nc, i - 1, j, k, 5); a[1] = CC(id, nc, i + 1, j, k, 5);
-                    a[2] = CC(id, nc, i, j - 1, k, 6); a[3] = CC(id, nc, i, j + 1, k, 6);
-                    a[4] = CC(id, nc, i, j, k - 1, 7); a[5] = CC(id, nc, i, j, k + 1, 7);
+                    a[0] = CC(id, nc, i - 1, j, k, e1); a[1] = CC(id, nc, i + 1, j, k, e1);
+                    a[2] = CC(id, nc, i, j - 1, k, e2); a[3] = CC(id, nc, i, j + 1, k, e2);
+                    a[4] = CC(id, nc, i, j, k - 1, e3); a[5] = CC(id, nc, i, j, k + 1, e3);
                     double s = 0.0;
                     for (int q = 0; q < 6; q++) s += 2 * i2[q] * a0[q] * a[q] / (a0[q] + a[q]) * (u[q] - u0);
-                    CC(id, nc, i, j, k, i_out) = s - mg->lambda * u0;
+                    CC(id, nc, i, j, k, i_out) = (mg->op == ORC_VLAPLACIAN) ? s : s - mg->lambda * u0;
                 }
         return;
     }

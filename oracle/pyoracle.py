@@ -20,7 +20,7 @@ _IP = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 _DP = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _LP = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 
-LAPLACIAN, HELMHOLTZ, AHELMHOLTZ = 1, 3, 5
+LAPLACIAN, VLAPLACIAN, HELMHOLTZ, VHELMHOLTZ, AHELMHOLTZ = 1, 2, 3, 4, 5
 GS, GSRB = 1, 2
 
 

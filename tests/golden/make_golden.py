@@ -41,6 +41,13 @@ CONFIGS = {
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1]),
     "helm32_gs_c0": ("8 32 32 32 5 v gs helm 10 c0 sol 1 lb 0", True, [1]),
+    # §8(f) row 1: variable-coefficient Laplacian / Helmholtz (m_vlaplacian,
+    # m_vhelmholtz), eps = (1.5+sin 2pi x)(1.5+sin 2pi y)(1.5+sin 2pi z)
+    "vlpl32_gsrb_v": ("8 32 32 32 6 v gsrb vlpl 0 sol sol 1 lb 1", True, [1, 4]),
+    "vlpl32_gs_f": ("8 32 32 32 4 f gs vlpl 0 d0 sol 1 lb 0", True, [1]),
+    "vhelm32_gsrb_v": ("8 32 32 32 6 v gsrb vhelm 10 sol sol 1 lb 0", True, [1]),
+    "vhelm32_gs_n0": ("8 32 32 32 4 v gs vhelm 10 n0 sol 1 lb 0", True, [1]),
+    "vlpl_ref2_gs_v": ("8 32 32 32 4 v gs vlpl 0 sol sol 2 lb 0", True, [1, 3]),
     # C4-like: tests/test_refinement (centre-refined AMR tree)
     # ranks 3 put refinement boundaries across ranks (power-of-two rank counts
     # cut these trees along the octree and never do)

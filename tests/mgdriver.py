@@ -78,8 +78,23 @@ def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0):
     return tree
 
 
-I_SOL = 5
-N_VARS = 5
+I_EPS = 5   # mg_iveps: the coefficient of the v-operators (vlpl / vhelm)
+
+
+def is_vop(cfg):
+    return cfg["op"] in ("vlpl", "vhelm")
+
+
+def i_sol(cfg):
+    """omg_golden's solution variable: 5, or 6 when var 5 holds eps."""
+    return 6 if is_vop(cfg) else 5
+
+
+def n_vars(cfg):
+    return i_sol(cfg)
+
+
+OPS = {"lpl": 1, "vlpl": 2, "helm": 3, "vhelm": 4}
 
 
 class OracleBackend:
@@ -88,12 +103,12 @@ class OracleBackend:
         import pyoracle  # checker only
         self.cfg = cfg
         self.tree = build_tree(cfg, T.MGTree(), n_ranks)
-        self.o = pyoracle.Oracle(self.tree, N_VARS, n_ranks)
-        op = pyoracle.HELMHOLTZ if cfg["op"] == "helm" else pyoracle.LAPLACIAN
+        self.o = pyoracle.Oracle(self.tree, n_vars(cfg), n_ranks)
+        op = OPS[cfg["op"]]
         sm = pyoracle.GSRB if cfg["smoother"] == "gsrb" else pyoracle.GS
-        sub = bool(self.tree.subtract_mean) or (op == pyoracle.LAPLACIAN and cfg["bc"] == "per")
-        if op == pyoracle.HELMHOLTZ:
-            sub = False
+        # laplacian_set_methods only: periodic => subtract_mean (m_laplacian.f90:16-20);
+        # vlaplacian_set_methods sets it false (m_vlaplacian.f90:21)
+        sub = op == pyoracle.LAPLACIAN and cfg["bc"] == "per"
         self.o.configure(op=op, lam=cfg["lam"], smoother=sm, subtract_mean=sub)
         _apply_bc(cfg, self.tree, lambda iv, nb, t, v: self.o.set_bc(iv, nb, t, v),
                   lambda iv, a, b, c: self.o.set_bc_faces(iv, a, b, c))
@@ -130,8 +145,8 @@ class DeviceBackend:
     def __init__(self, cfg, comm=None):
         self.cfg = cfg
         mg = omg.MG()
-        mg.n_extra_vars = 1
-        mg.operator_type = T.MG_HELMHOLTZ if cfg["op"] == "helm" else T.MG_LAPLACIAN
+        mg.n_extra_vars = n_vars(cfg) - 4
+        mg.operator_type = OPS[cfg["op"]]
         mg.helmholtz_lambda = cfg["lam"]
         mg.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
         omg.mg_set_methods(mg)
@@ -198,6 +213,12 @@ def setup_problem(be):
     """set_solution + compute_rhs_and_reset (tests/test_uniform_grid.f90:
     137-170), or set_rhs (tests/test_performance.f90:102-115)."""
     cfg, tree = be.cfg, be.tree
+    I_SOL = i_sol(cfg)
+    if is_vop(cfg):
+        for lvl in be.levels():
+            ids = be.my_ids(lvl)
+            if len(ids):
+                be.set_level(lvl, I_EPS, P.level_eps(tree, lvl, ids))
     if cfg["rhs"] == "sol":
         for lvl in be.levels():
             ids = be.my_ids(lvl)
@@ -240,7 +261,7 @@ def measure(be):
         if not sel:
             continue
         phi = be.get_level(lvl, T.MG_IPHI)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
-        sol = be.get_level(lvl, I_SOL)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        sol = be.get_level(lvl, i_sol(be.cfg))[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
         r = be.get_level(lvl, T.MG_IRES)[sel, 1:nc + 1, 1:nc + 1, 1:nc + 1]
         err = max(err, float(np.max(np.abs(phi - sol))))
         res = max(res, float(np.max(np.abs(r))))
