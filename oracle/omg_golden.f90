@@ -19,6 +19,7 @@
 !     cycle    v | f
 !     smoother gs | gsrb
 !     op       lpl | helm | vlpl | vhelm   (v*: coefficient eps in var 5, solution in 6)
+!              | ahelm (eps1..3 in vars 5..7, solution in 8; the dump holds rhs)
 !     bc       sol (callback Dirichlet u) | d0 (Dirichlet 0) | per (periodic)
 !              | n0 (Neumann 0) | c0 (continuous)
 !     rhs      sol (rhs = L u) | one (rhs = 1)
@@ -71,6 +72,14 @@ program omg_golden
   if (trim(a_op) == "helm") then
      mg%operator_type = mg_helmholtz
      call helmholtz_set_lambda(lambda)
+  else if (trim(a_op) == "ahelm") then
+     ! eps1..3 in vars 5..7 (mg_iveps1..3), the solution in 8; the smoother
+     ! box_gs_ahelmh is broken in 3D (a0(4:5), m_ahelmholtz.f90:145), so only
+     ! the operator is pinned: run with n_its = 0, the dump holds rhs = L(u)
+     mg%n_extra_vars = 4
+     i_sol = mg_num_vars + 4
+     mg%operator_type = mg_ahelmholtz
+     call ahelmholtz_set_lambda(lambda)
   else if (trim(a_op) == "vlpl" .or. trim(a_op) == "vhelm") then
      ! variable coefficient eps in mg_iveps (= 5): the solution moves to 6
      mg%n_extra_vars = 2
@@ -123,6 +132,7 @@ program omg_golden
   call mg_allocate_storage(mg)
 
   if (mg%operator_type == mg_vlaplacian .or. mg%operator_type == mg_vhelmholtz) call set_eps(mg)
+  if (mg%operator_type == mg_ahelmholtz) call set_eps3(mg)
   if (trim(a_rhs) == "sol") then
      call set_solution(mg, n_levels > 1)
      call compute_rhs_and_reset(mg)
@@ -204,6 +214,27 @@ contains
     end do
   end subroutine set_eps
 
+  ! aniso: eps_d = eps * d (d = 1, 2, 3) in mg_iveps1..3
+  subroutine set_eps3(mg)
+    type(mg_t), intent(inout) :: mg
+    integer                   :: n, id, lvl, nc, IJK, d
+    real(dp)                  :: r(NDIM), e
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       nc = mg%box_size_lvl(lvl)
+       do n = 1, size(mg%lvls(lvl)%my_ids)
+          id = mg%lvls(lvl)%my_ids(n)
+          do KJI_DO(0, nc+1)
+             r = mg%boxes(id)%r_min + ([IJK] - 0.5_dp) * mg%dr(:, lvl)
+             e = (1.5_dp + sin(2 * pi * r(1))) * (1.5_dp + sin(2 * pi * r(2))) * &
+                  (1.5_dp + sin(2 * pi * r(3)))
+             do d = 1, NDIM
+                mg%boxes(id)%cc(IJK, mg_iveps1 + d - 1) = e * d
+             end do
+          end do; CLOSE_DO
+       end do
+    end do
+  end subroutine set_eps3
+
   subroutine compute_rhs_and_reset(mg)
     type(mg_t), intent(inout) :: mg
     integer                   :: n, id, lvl, nc
@@ -268,7 +299,11 @@ contains
        nc = mg%box_size_lvl(lvl)
        do n = 1, size(mg%lvls(lvl)%ids)
           id = mg%lvls(lvl)%ids(n)
-          write(u) mg%boxes(id)%cc(1:nc, 1:nc, 1:nc, mg_iphi)
+          if (mg%operator_type == mg_ahelmholtz) then
+             write(u) mg%boxes(id)%cc(1:nc, 1:nc, 1:nc, mg_irhs)
+          else
+             write(u) mg%boxes(id)%cc(1:nc, 1:nc, 1:nc, mg_iphi)
+          end if
        end do
     end do
     close(u)

@@ -48,6 +48,11 @@ CONFIGS = {
     "vhelm32_gsrb_v": ("8 32 32 32 6 v gsrb vhelm 10 sol sol 1 lb 0", True, [1]),
     "vhelm32_gs_n0": ("8 32 32 32 4 v gs vhelm 10 n0 sol 1 lb 0", True, [1]),
     "vlpl_ref2_gs_v": ("8 32 32 32 4 v gs vlpl 0 sol sol 2 lb 0", True, [1, 3]),
+    # aniso-Helmholtz (m_ahelmholtz): the reference's 3D smoother is broken
+    # (NaN), so only the operator box_ahelmh is pinned: no cycle,
+    # the sha256 is that of rhs = L(u) on every box
+    "ahelm32_op": ("8 32 32 32 0 v gsrb ahelm 10 sol sol 1 lb 0", True, [1]),
+    "ahelm_ref2_op": ("8 32 32 32 0 v gs ahelm 5 sol sol 2 lb 0", True, [1]),
     # C4-like: tests/test_refinement (centre-refined AMR tree)
     # ranks 3 put refinement boundaries across ranks (power-of-two rank counts
     # cut these trees along the octree and never do)
@@ -87,7 +92,8 @@ def main():
                 if fn:
                     with open(fn, "rb") as f:
                         b = f.read()
-                    run_entry["phi_sha256"] = hashlib.sha256(b).hexdigest()
+                    key = "rhs_sha256" if " ahelm " in args else "phi_sha256"
+                    run_entry[key] = hashlib.sha256(b).hexdigest()
                     run_entry["phi_bytes"] = len(b)
             entry["runs"][str(r)] = run_entry
             print(name, r, its[-1]["err"], its[-1]["res"], file=sys.stderr)

@@ -86,15 +86,16 @@ def is_vop(cfg):
 
 
 def i_sol(cfg):
-    """omg_golden's solution variable: 5, or 6 when var 5 holds eps."""
-    return 6 if is_vop(cfg) else 5
+    """omg_golden's solution variable: 5, or 6 when var 5 holds eps, or 8
+    after the three aniso coefficients."""
+    return 8 if cfg["op"] == "ahelm" else 6 if is_vop(cfg) else 5
 
 
 def n_vars(cfg):
     return i_sol(cfg)
 
 
-OPS = {"lpl": 1, "vlpl": 2, "helm": 3, "vhelm": 4}
+OPS = {"lpl": 1, "vlpl": 2, "helm": 3, "vhelm": 4, "ahelm": 5}
 
 
 class OracleBackend:
@@ -214,11 +215,16 @@ def setup_problem(be):
     137-170), or set_rhs (tests/test_performance.f90:102-115)."""
     cfg, tree = be.cfg, be.tree
     I_SOL = i_sol(cfg)
-    if is_vop(cfg):
+    if is_vop(cfg) or cfg["op"] == "ahelm":
         for lvl in be.levels():
             ids = be.my_ids(lvl)
             if len(ids):
-                be.set_level(lvl, I_EPS, P.level_eps(tree, lvl, ids))
+                e = P.level_eps(tree, lvl, ids)
+                if cfg["op"] == "ahelm":
+                    for d in (1, 2, 3):                 # eps_d = eps * d, vars 5..7
+                        be.set_level(lvl, I_EPS + d - 1, e * float(d))
+                else:
+                    be.set_level(lvl, I_EPS, e)
     if cfg["rhs"] == "sol":
         for lvl in be.levels():
             ids = be.my_ids(lvl)
@@ -268,14 +274,15 @@ def measure(be):
     return err, res
 
 
-def phi_digest(be):
+def phi_digest(be, iv=None):
+    iv = T.MG_IPHI if iv is None else iv
     h = hashlib.sha256()
     for lvl in be.levels():
         ids = be.my_ids(lvl)
         if not len(ids):
             continue
         nc = be.tree.box_size_lvl[lvl]
-        phi = be.get_level(lvl, T.MG_IPHI)[:, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        phi = be.get_level(lvl, iv)[:, 1:nc + 1, 1:nc + 1, 1:nc + 1]
         h.update(np.ascontiguousarray(phi).tobytes())
     return h.hexdigest()
 
@@ -309,7 +316,10 @@ def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None)
     be = OracleBackend(cfg, n_ranks) if backend == "oracle" else DeviceBackend(cfg)
     setup_problem(be)
     hist = _cycles(be, cfg, reduce)
-    return {"history": hist, "phi_sha256": phi_digest(be), "backend": be}
+    out = {"history": hist, "phi_sha256": phi_digest(be), "backend": be}
+    if cfg["op"] == "ahelm":
+        out["rhs_sha256"] = phi_digest(be, T.MG_IRHS)
+    return out
 
 
 def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600):

@@ -59,14 +59,15 @@ def test_dropin_fails_loudly_without_gpu():
 def test_dropin_golden(name):
     cfg = GOLDEN[name]
     ref = cfg["runs"]["1"]
+    key = "phi_sha256" if "phi_sha256" in ref else "rhs_sha256" if "rhs_sha256" in ref else None
     with tempfile.TemporaryDirectory() as td:
-        dump = os.path.join(td, "phi.bin") if "phi_sha256" in ref else None
+        dump = os.path.join(td, "dump.bin") if key else None   # phi, or rhs for ahelm
         p = run_driver(cfg["args"], dump)
         assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
         assert parse(p.stdout) == ref["history"]
         if dump:
             with open(dump, "rb") as f:
-                assert hashlib.sha256(f.read()).hexdigest() == ref["phi_sha256"]
+                assert hashlib.sha256(f.read()).hexdigest() == ref[key]
 
 
 REF_PROGRAMS = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_programs.json")))["runs"]

@@ -26,3 +26,5 @@ def test_oracle_matches_reference(name, ranks):
     assert out["history"] == run["history"]
     if "phi_sha256" in run:
         assert out["phi_sha256"] == run["phi_sha256"]
+    if "rhs_sha256" in run:   # aniso operator pinned through rhs = L(u)
+        assert out["rhs_sha256"] == run["rhs_sha256"]
