@@ -216,13 +216,13 @@ hipEvent_t loop_event(hipStream_t st) {
   return e;
 }
 
-void loop_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf) {
+void loop_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf, hipStream_t st) {
   omg_loop& G = *c->loop;
   const size_t per = (size_t)T.item_doubles;
   const int me = c->rank;
   for (auto& p : T.send) {
     const size_t n = p.items.size() / T.send_ints * per;
-    hipEvent_t ev = loop_event(c->stream);
+    hipEvent_t ev = loop_event(st);
     std::lock_guard<std::mutex> lk(G.mu);
     G.box[{me, p.peer, c->loop_seq_send[p.peer]}] = {sendbuf + (size_t)p.offset * per, n, ev};
     G.cv.notify_all();
@@ -240,13 +240,13 @@ void loop_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double*
       G.box.erase(k);
     }
     if (m.n != n) throw OmgError("loopback transport: message size mismatch");
-    HIPCHK(hipStreamWaitEvent(c->stream, m.ev, 0));
+    HIPCHK(hipStreamWaitEvent(st, m.ev, 0));
     HIPCHK(hipMemcpyAsync(recvbuf + (size_t)p.offset * per, m.src, n * sizeof(double),
-                          hipMemcpyDeviceToDevice, c->stream));
+                          hipMemcpyDeviceToDevice, st));
     HIPCHK(hipEventDestroy(m.ev));
   }
   for (auto& p : T.recv) {   // the sender may reuse its buffer once our copies ran
-    hipEvent_t ev = loop_event(c->stream);
+    hipEvent_t ev = loop_event(st);
     std::lock_guard<std::mutex> lk(G.mu);
     G.acks[{me, p.peer, c->loop_seq_recv[p.peer]++}] = ev;
     G.cv.notify_all();
@@ -262,7 +262,7 @@ void loop_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double*
       ev = G.acks[k];
       G.acks.erase(k);
     }
-    HIPCHK(hipStreamWaitEvent(c->stream, ev, 0));
+    HIPCHK(hipStreamWaitEvent(st, ev, 0));
     HIPCHK(hipEventDestroy(ev));
   }
 }
@@ -290,11 +290,12 @@ std::vector<double> loop_allgather(omg_ctx* c, double v) {
 
 // One grouped RCCL round: send segment i to peer i, receive likewise
 // (replaces sort_and_transfer_buffers, m_communication.f90:37-66).
-void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf) {
+void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf, hipStream_t st = nullptr) {
   if (c->n_ranks == 1) return;
   if (T.send.empty() && T.recv.empty()) return;
+  if (!st) st = c->stream;
   if (c->loop) {
-    loop_exchange(c, T, sendbuf, recvbuf);
+    loop_exchange(c, T, sendbuf, recvbuf, st);
     return;
   }
   ncclComm_t comm = (ncclComm_t)c->nccl;
@@ -302,11 +303,11 @@ void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recv
   NCCLCHK(ncclGroupStart());
   for (auto& p : T.send) {
     size_t n = p.items.size() / (T.send_ints) * per;
-    NCCLCHK(ncclSend(sendbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, c->stream));
+    NCCLCHK(ncclSend(sendbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, st));
   }
   for (auto& p : T.recv) {
     size_t n = p.items.size() / (T.recv_ints) * per;
-    NCCLCHK(ncclRecv(recvbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, c->stream));
+    NCCLCHK(ncclRecv(recvbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, st));
   }
   NCCLCHK(ncclGroupEnd());
 }
@@ -450,6 +451,29 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
     if (n == 1 && absorb) phi_mean_ready(c);
     const double* shift = (n == 1 && absorb) ? red_mean(c, 0) : nullptr;
     if (n == 1) L->shift_pending = false;
+    if (L->n_bnd && L->n_int && !odd && gs_tiled(L->nc, c->op, L->has_rb)) {
+      // boxes with faces on other GPUs first; their halo travels on the comm
+      // stream while the interior boxes run (interior boxes never touch a
+      // remote ghost face, the unpack touches nothing else)
+      {
+        Prof p(c, "smoother_gsrb", 0.5 * L->n_bnd * L->nc * L->nc * L->nc, lvl);
+        launch_gs_substep(L->view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
+                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_bnd, L->n_bnd);
+      }
+      HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
+      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm);
+      launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream_comm);
+      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
+      {
+        Prof p(c, "smoother_gsrb", 0.5 * L->n_int * L->nc * L->nc * L->nc, lvl);
+        launch_gs_substep(L->view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
+                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int);
+      }
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+      if (!L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
+      continue;
+    }
     if (L->n) {
       Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc, lvl);
       launch_gs_substep(L->view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
@@ -978,7 +1002,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
-    dfree(L.d_rbsend); dfree(L.d_rbrecv);
+    dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
@@ -1108,6 +1132,21 @@ void build_plan(omg_ctx* c) {
     L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
+    {
+      // boxes with a face toward another GPU (halo overlap in smooth_boxes)
+      std::vector<int> bnd, in;
+      for (int b = 0; b < L.n; b++) {
+        bool r = false;
+        for (int nb = 0; nb < 6; nb++) r |= L.h_nbk[(size_t)b * 6 + nb] == NB_REMOTE;
+        (r ? bnd : in).push_back(b);
+      }
+      if (!bnd.empty()) {
+        L.n_bnd = (int)bnd.size();
+        L.n_int = (int)in.size();
+        L.d_bnd = to_device(bnd);
+        L.d_int = to_device(in);
+      }
+    }
     L.d_phi = L.d_data;
     L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);
@@ -1259,6 +1298,9 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream_comm, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_phi, hipEventDisableTiming));
@@ -1303,6 +1345,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamSynchronize(c->stream_comm);
     free_levels(c);
     dfree(c->d_scalar);
     dfree(c->d_red);
@@ -1311,6 +1354,9 @@ int omg_ctx_destroy(omg_ctx* c) {
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);
     if (c->ev_phi) (void)hipEventDestroy(c->ev_phi);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->stream_comm) (void)hipStreamDestroy(c->stream_comm);
+    if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
+    if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
     if (c->loop) {   // the last context of a loopback group removes it

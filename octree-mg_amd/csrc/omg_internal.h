@@ -123,6 +123,9 @@ struct Level {
   Transfer rbx;         // refinement-boundary faces across ranks at this level (send: coarse idx at
                         // lvl-1, coarse-side nb, child offset; recv: box*6+nb of my fine face)
   double* d_scratch_rhs = nullptr;   // leaf sums of rhs for the next get_sum
+  int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
+  int* d_int = nullptr;
+  int n_bnd = 0, n_int = 0;
   double* d_rbsend = nullptr;
   double* d_rbrecv = nullptr;
   double* d_sendbuf = nullptr;
@@ -199,6 +202,8 @@ struct omg_ctx {
   // scalars
   double* d_red = nullptr;             // device reductions (get_sum / subtract_mean)
   hipStream_t stream2 = nullptr;       // side stream (rhs sum chain)
+  hipStream_t stream_comm = nullptr;   // halo exchange overlapped with interior boxes
+  hipEvent_t ev_bnd = nullptr, ev_comm = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_phi = nullptr;
   bool phi_mean_on_side = false;
   bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)       // the pending phi mean is still being finished on stream2

@@ -19,9 +19,10 @@ struct GcBC {
 // kernel (omg_sweep.hip) when the level allows, else the generic one
 // shift (device scalar or null): subtract it from every value the substep
 // loads (a pending subtract_mean of phi, bit-identical to applying it first)
+// boxes/n_boxes: only these boxes (local indices), else the whole level
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
-                       hipStream_t st);
+                       hipStream_t st, const int* boxes = nullptr, int n_boxes = 0);
 // whether launch_gs_substep takes the LDS-tiled kernel (which alone takes a shift)
 inline bool gs_tiled(int nc, int op, bool has_rb) {
   return !has_rb && (op == OP_LPL || op == OP_HELM) && (nc == 16 || nc == 8 || nc == 4 || nc == 2);

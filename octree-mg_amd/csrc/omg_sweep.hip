@@ -27,15 +27,18 @@ namespace omg {
 
 template <int NC, int OP, int BS, int NT>
 __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
-                                                  double* __restrict__ sendbuf, const double* __restrict__ shift) {
+                                                  double* __restrict__ sendbuf, const double* __restrict__ shift,
+                                                  const int* __restrict__ boxes) {
   __shared__ double lds[gsrb_lds<NC>()];
-  gsrb_box<NC, OP, BS, NT>(L, lambda, e, colours, bc, sendbuf, shift, xcd_box(blockIdx.x, gridDim.x), lds);
+  const int q = xcd_box(blockIdx.x, gridDim.x);
+  gsrb_box<NC, OP, BS, NT>(L, lambda, e, colours, bc, sendbuf, shift, boxes ? boxes[q] : q, lds);
 }
 
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
-                       hipStream_t st) {
+                       hipStream_t st, const int* boxes, int n_boxes) {
   if (L.n == 0) return;
+  if (boxes && !gs_tiled(L.nc, op, has_rb)) return;   // subsets only exist for the tiled kernel
   if (!gs_tiled(L.nc, op, has_rb)) {
     launch_gs_sub(L, op, lambda, e, colours, C, rb, bc, sendbuf, st);
     return;
@@ -46,12 +49,13 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   // boxes fits); streaming loads/stores are non-temporal: nothing a substep
   // reads or writes is touched again before the next substep has swept the
   // level, far beyond L2 / MALL at the sizes that matter.
-  const dim3 g(L.n);
+  const dim3 g(boxes ? n_boxes : L.n);
+  if (g.x == 0) return;
 #define OMG_TILE(NC, BS)                                                                   \
   if (op == OP_HELM)                                                                       \
-    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift); \
+    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes); \
   else                                                                                     \
-    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift);
+    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes);
   switch (L.nc) {
     case 16: OMG_TILE(16, 512) break;
     case 8: OMG_TILE(8, 256) break;
