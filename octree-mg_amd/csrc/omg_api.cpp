@@ -676,7 +676,7 @@ void leaf_box_sums(omg_ctx* c, int iv, int ch, hipStream_t st) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
-    launch_box_sums2(L->view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
+    launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
   }
 }
 
@@ -687,7 +687,7 @@ void leaf_chain(omg_ctx* c, int ch, hipStream_t st) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     Prof p(c, "seq_sum", (double)L->leaves.size(), l);
-    launch_seq_sum2(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, st);
+    launch_seq_sum(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, st);
   }
 }
 

@@ -54,8 +54,6 @@ void launch_prolong_pack(const LevelView& C, const LevelView& F, int iv, const i
                          double* buf, hipStream_t st);
 void launch_prolong_unpack(const LevelView& F, int iv_to, int add, const int* items, int n,
                            const double* buf, hipStream_t st);
-void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
-void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st);
 void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts, hipStream_t st);
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st);
 void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t st);
@@ -101,11 +99,11 @@ void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const i
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
                             hipStream_t st);
-void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
+void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);
 bool subtract_sums_nc(int nc);
 void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
                           hipStream_t st);
 void launch_mean(const double* all, int n, double volume, double* mean, hipStream_t st);
-void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st);
+void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st);
 
 }  // namespace omg

@@ -327,40 +327,6 @@ __global__ void __launch_bounds__(256) k_prolong_unpack(LevelView F, int iv_to, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// get_sum (m_multigrid.f90:278-294): per-leaf sequential interior sums in the
-// reference's column-major order (one thread per leaf box) ...
-__global__ void __launch_bounds__(64) k_box_sums(LevelView L, int iv, const int* leaves, int n_leaves,
-                                                 double* out) {
-  const int nc = L.nc;
-  const int q = blockIdx.x * 64 + threadIdx.x;
-  if (q >= n_leaves) return;
-  const double* u = boxp(L, iv, leaves[q]);
-  double acc = 0.0;
-  for (int k = 1; k <= nc; k++)
-    for (int j = 1; j <= nc; j++) {
-      const int r0 = L.h * ((j - 1) + nc * (k - 1));
-      const int e0 = ((1 + j + k) & 1) * L.hv, e1 = ((j + k) & 1) * L.hv;  // colours of odd / even i
-      for (int i = 1; i <= nc; i++) acc += u[((i & 1) ? e0 : e1) + r0 + ((i - 1) >> 1)];
-    }
-  out[q] = acc;
-}
-
-// ... then acc = acc + w * box_sum in my_leaves order, one thread (exact order).
-__global__ void k_seq_sum(const double* box_sums, int n, double w, double* acc) {
-  __shared__ double stage[1024];
-  double a = *acc;
-  for (int base = 0; base < n; base += 1024) {
-    const int m = min(1024, n - base);
-    for (int q = threadIdx.x; q < m; q += blockDim.x) stage[q] = box_sums[base + q];
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int q = 0; q < m; q++) a = a + w * stage[q];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *acc = a;
-}
-
 // subtract_mean's update (m_multigrid.f90:262-275): interior, or every stored cell.
 __global__ void __launch_bounds__(256) k_subtract(LevelView L, int iv, const double* mean, int ghosts) {
   const double m = *mean;
@@ -568,16 +534,6 @@ void launch_prolong_unpack(const LevelView& F, int iv_to, int add, const int* it
   const long long work = 2LL * F.hv * n;
   if (work == 0) return;
   k_prolong_unpack<<<grid_for(work), 256, 0, st>>>(F, iv_to, add, items, n, buf);
-}
-
-void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
-  if (n == 0) return;
-  k_box_sums<<<(n + 63) / 64, 64, 0, st>>>(L, iv, leaves, n, out);
-}
-
-void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
-  if (n == 0) return;
-  k_seq_sum<<<1, 256, 0, st>>>(box_sums, n, w, acc);
 }
 
 void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts, hipStream_t st) {

@@ -451,7 +451,7 @@ bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int
   return true;
 }
 
-void launch_box_sums2(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
+void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
   if (n == 0) return;
   const dim3 g((n + 31) / 32);
   switch (L.nc) {
@@ -492,7 +492,7 @@ void launch_mean(const double* all, int n, double volume, double* mean, hipStrea
   k_mean<<<1, 64, 0, st>>>(all, n, volume, mean);
 }
 
-void launch_seq_sum2(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
+void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
   if (n == 0) return;
   k_seq_sum3<<<1, 64, 0, st>>>(box_sums, n, w, acc);
 }

@@ -38,6 +38,11 @@ module m_multigrid
   integer     :: ctx_lowest  = huge(1)
   integer     :: ctx_highest = -huge(1)
 
+  !> Resident mode (opt-in, see mg_gpu_set_resident): the data stays on the
+  !> GPU between calls instead of round-tripping through mg%boxes(:)%cc.
+  logical :: resident = .false.
+  logical :: device_current = .false.
+
   integer :: timer_device_vcycle = -1
   integer :: timer_device_fmg    = -1
   integer :: timer_host_to_dev   = -1
@@ -47,6 +52,10 @@ module m_multigrid
   public :: mg_fas_fmg
   public :: mg_set_methods
   public :: mg_apply_op
+  ! additions of the GPU backend (not in the reference's API)
+  public :: mg_gpu_set_resident
+  public :: mg_gpu_to_host
+  public :: mg_gpu_to_device
 
 contains
 
@@ -120,14 +129,14 @@ contains
 
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
-    call to_device(mg)
+    call sync_in(mg)
     want = merge(1_c_int, 0_c_int, present(max_res))
     call mg_timer_start(mg%timers(timer_device_fmg))
     call omg_ok(omg_fas_fmg(ctx, merge(1_c_int, 0_c_int, have_guess), want, res), &
          "mg_fas_fmg")
     call omg_ok(omg_synchronize(ctx), "synchronize")
     call mg_timer_end(mg%timers(timer_device_fmg))
-    call to_host(mg)
+    call sync_out(mg)
     if (present(max_res)) max_res = res
   end subroutine mg_fas_fmg
 
@@ -142,7 +151,7 @@ contains
 
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
-    call to_device(mg)
+    call sync_in(mg)
     hl = mg%lowest_lvl - 1              ! "absent" for the C side
     if (present(highest_lvl)) hl = highest_lvl
     sa = 1
@@ -152,7 +161,7 @@ contains
     call omg_ok(omg_fas_vcycle(ctx, hl, want, res, sa), "mg_fas_vcycle")
     call omg_ok(omg_synchronize(ctx), "synchronize")
     call mg_timer_end(mg%timers(timer_device_vcycle))
-    call to_host(mg)
+    call sync_out(mg)
     if (present(max_res)) max_res = res
   end subroutine mg_fas_vcycle
 
@@ -176,10 +185,50 @@ contains
     end if
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
-    call to_device(mg)
+    call sync_in(mg)
     call omg_ok(omg_apply_op(ctx, int(i_out, c_int)), "mg_apply_op")
-    call copy_var_to_host(mg, i_out)
+    if (.not. resident) call copy_var_to_host(mg, i_out)
   end subroutine mg_apply_op
+
+  !> Resident mode on/off.  When on, mg_fas_vcycle / mg_fas_fmg / mg_apply_op
+  !> neither upload mg%boxes(:)%cc before nor download it after: the GPU copy
+  !> is the current one until mg_gpu_to_host (after the host changed nothing)
+  !> or mg_gpu_to_device (after the host changed data) is called.  Switching
+  !> it off downloads the GPU state first.
+  subroutine mg_gpu_set_resident(mg, on)
+    type(mg_t), intent(inout) :: mg
+    logical, intent(in)       :: on
+    if (resident .and. .not. on .and. device_current) call to_host(mg)
+    resident = on
+  end subroutine mg_gpu_set_resident
+
+  !> Copy phi, rhs, old and res of the GPU into mg%boxes(:)%cc.
+  subroutine mg_gpu_to_host(mg)
+    type(mg_t), intent(inout) :: mg
+    if (device_current) call to_host(mg)
+  end subroutine mg_gpu_to_host
+
+  !> Copy every variable of mg%boxes(:)%cc to the GPU (and the methods and
+  !> boundary conditions in mg).
+  subroutine mg_gpu_to_device(mg)
+    type(mg_t), intent(inout) :: mg
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call to_device(mg)
+    device_current = .true.
+  end subroutine mg_gpu_to_device
+
+  subroutine sync_in(mg)
+    type(mg_t), intent(inout) :: mg
+    if (resident .and. device_current .and. ctx_n_boxes == mg%n_boxes) return
+    call to_device(mg)
+    device_current = .true.
+  end subroutine sync_in
+
+  subroutine sync_out(mg)
+    type(mg_t), intent(inout) :: mg
+    if (.not. resident) call to_host(mg)
+  end subroutine sync_out
 
   ! ------------------------------------------------------------------------
   ! Host <-> device

@@ -88,3 +88,22 @@ def test_reference_programs_unchanged(name):
     lines = [ln.rstrip() for ln in p.stdout.splitlines()
              if "max solution error" in ln or "max err" in ln]
     assert lines == run["lines"]
+
+
+RESIDENT = os.path.join(BUILD, "omg_golden_gpu_resident")
+RESIDENT_CASES = ["c1_gsrb_f_maxres", "per32_gsrb_v", "helm32_gs_c0", "ref3_gsrb_v", "vlpl32_gsrb_v",
+                  "u32_gs_d0_one"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", RESIDENT_CASES)
+def test_dropin_resident_mode(name):
+    """mg_gpu_set_resident(.true.): the cycles run back to back on GPU data and
+    the host copy is only refreshed (mg_gpu_to_host) for printing; the
+    histories are still the reference's."""
+    if not os.path.exists(RESIDENT):
+        pytest.skip("Fortran drop-in drivers not built")
+    cfg = GOLDEN[name]
+    p = subprocess.run([RESIDENT] + cfg["args"].split() + ["x"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    assert parse(p.stdout) == cfg["runs"]["1"]["history"]
