@@ -78,8 +78,10 @@ int omg_tree_setup(omg_ctx *ctx, int n_boxes, const int *lvl, const int *parent,
                    const double *dr, const int *list_off, const int *lists,
                    int n_vars);
 
-/* mg_set_methods equivalents (src/m_multigrid.f90:27-60, m_helmholtz.f90:
- * 39-46, m_ahelmholtz.f90:59-66). */
+/* mg_set_methods equivalents (src/m_multigrid.f90:27-60; the operators'
+ * *_set_methods: m_laplacian.f90:13-49, m_vlaplacian.f90:13-49,
+ * m_helmholtz.f90:18-37, m_vhelmholtz.f90:19-49, m_ahelmholtz.f90:19-57;
+ * lambda as helmholtz_set_lambda m_helmholtz.f90:39-46 and its v/a forms). */
 int omg_set_operator(omg_ctx *ctx, int op, double lambda);
 int omg_set_smoother(omg_ctx *ctx, int smoother, int n_cycle_down, int n_cycle_up,
                      int max_coarse_cycles, double residual_coarse_abs,
@@ -94,34 +96,43 @@ int omg_set_bc(omg_ctx *ctx, int iv, int nb, int bc_type, double bc_value);
 int omg_set_bc_faces(omg_ctx *ctx, int iv, const long long *face_off,
                      const int *face_type, const double *data, long long n_data);
 
-/* Number of boxes this rank owns at lvl (size(mg%lvls(lvl)%my_ids)). */
+/* Number of boxes this rank owns at lvl (size(mg%lvls(lvl)%my_ids),
+ * src/m_data_structures.f90:196-206). */
 int omg_level_size(omg_ctx *ctx, int lvl, int *n_boxes, int *nc);
 
 /* Bulk copy of variable iv of all my_ids boxes at lvl, in my_ids order,
- * (nc+2)^3 doubles per box, host memory (blocking). */
+ * (nc+2)^3 doubles per box as mg%boxes(id)%cc(:,:,:,iv) stores them
+ * (src/m_data_structures.f90:209-221), host memory (blocking). */
 int omg_upload_level(omg_ctx *ctx, int lvl, int iv, const double *host);
 int omg_download_level(omg_ctx *ctx, int lvl, int iv, double *host);
 
-/* The hot path (src/m_multigrid.f90): highest_lvl < lowest means default. */
+/* The hot path.  omg_fas_vcycle = mg_fas_vcycle (src/m_multigrid.f90:150-243);
+ * highest_lvl < lowest_lvl means "not present".  omg_fas_fmg = mg_fas_fmg
+ * (:84-147).  max_res is written when want_max_res (the optional argument). */
 int omg_fas_vcycle(omg_ctx *ctx, int highest_lvl, int want_max_res, double *max_res,
                    int standalone);
 int omg_fas_fmg(omg_ctx *ctx, int have_guess, int want_max_res, double *max_res);
 
-/* Per-level steps (each as in the reference routine named). */
-int omg_apply_op(omg_ctx *ctx, int i_out);                       /* mg_apply_op */
-int omg_restrict(omg_ctx *ctx, int iv);                          /* mg_restrict */
-int omg_restrict_lvl(omg_ctx *ctx, int iv, int lvl);             /* mg_restrict_lvl */
-int omg_fill_ghost_cells(omg_ctx *ctx, int iv);                  /* mg_fill_ghost_cells */
-int omg_fill_ghost_cells_lvl(omg_ctx *ctx, int lvl, int iv);     /* mg_fill_ghost_cells_lvl */
-int omg_prolong(omg_ctx *ctx, int lvl, int iv, int iv_to, int add); /* mg_prolong (sparse) */
-int omg_smooth_boxes(omg_ctx *ctx, int lvl, int n_cycle);        /* smooth_boxes */
-int omg_update_coarse(omg_ctx *ctx, int lvl);                    /* update_coarse */
-int omg_correct_children(omg_ctx *ctx, int lvl);                 /* correct_children */
-int omg_residual_lvl(omg_ctx *ctx, int lvl);                     /* residual_box over my_ids */
-int omg_max_residual_lvl(omg_ctx *ctx, int lvl, double *out);    /* max_residual_lvl */
-int omg_get_sum(omg_ctx *ctx, int iv, double *out);              /* get_sum + allreduce */
-int omg_subtract_mean(omg_ctx *ctx, int iv, int include_ghostcells); /* subtract_mean */
-int omg_phi_bc_store(omg_ctx *ctx);                              /* mg_phi_bc_store */
+/* Per-level steps, each the reference routine named (all in src/). */
+int omg_apply_op(omg_ctx *ctx, int i_out);            /* mg_apply_op, m_multigrid.f90:439-456 */
+int omg_restrict(omg_ctx *ctx, int iv);               /* mg_restrict, m_restrict.f90:72-80 */
+int omg_restrict_lvl(omg_ctx *ctx, int iv, int lvl);  /* mg_restrict_lvl, m_restrict.f90:83-114 */
+int omg_fill_ghost_cells(omg_ctx *ctx, int iv);       /* mg_fill_ghost_cells, m_ghost_cells.f90:120-128 */
+int omg_fill_ghost_cells_lvl(omg_ctx *ctx, int lvl, int iv);
+                                                      /* mg_fill_ghost_cells_lvl, m_ghost_cells.f90:131-175 */
+int omg_prolong(omg_ctx *ctx, int lvl, int iv, int iv_to, int add);
+                                                      /* mg_prolong + mg_prolong_sparse, m_prolong.f90:51-85,159-240 */
+int omg_smooth_boxes(omg_ctx *ctx, int lvl, int n_cycle);
+                                                      /* smooth_boxes, m_multigrid.f90:404-424 */
+int omg_update_coarse(omg_ctx *ctx, int lvl);         /* update_coarse, m_multigrid.f90:347-384 */
+int omg_correct_children(omg_ctx *ctx, int lvl);      /* correct_children, m_multigrid.f90:387-402 */
+int omg_residual_lvl(omg_ctx *ctx, int lvl);          /* residual_box over my_ids, m_multigrid.f90:426-436 */
+int omg_max_residual_lvl(omg_ctx *ctx, int lvl, double *out);
+                                                      /* max_residual_lvl, m_multigrid.f90:296-311 */
+int omg_get_sum(omg_ctx *ctx, int iv, double *out);   /* get_sum + MPI_Allreduce, m_multigrid.f90:253-294 */
+int omg_subtract_mean(omg_ctx *ctx, int iv, int include_ghostcells);
+                                                      /* subtract_mean, m_multigrid.f90:245-276 */
+int omg_phi_bc_store(omg_ctx *ctx);                   /* mg_phi_bc_store, m_ghost_cells.f90:66-117 */
 
 /* The communication plan of level lvl as built by omg_tree_setup: transfer
  * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,
