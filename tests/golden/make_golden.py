@@ -27,19 +27,19 @@ CONFIGS = {
     "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
     "c1_gsrb_v": ("8 64 64 64 10 v gsrb lpl 0 sol sol 1 lb 0", False, [1]),
     "c1_gs_f": ("8 64 64 64 10 f gs lpl 0 sol sol 1 lb 0", False, [1]),
-    "c1_gsrb_f_maxres": ("8 64 64 64 5 f gsrb lpl 0 sol sol 1 lb 1", False, [1]),
+    "c1_gsrb_f_maxres": ("8 64 64 64 5 f gsrb lpl 0 sol sol 1 lb 1", False, [1, 4, 8]),
     "u32_gsrb_v": ("8 32 32 32 6 v gsrb lpl 0 sol sol 1 lb 1", True, [1]),
     "u32_gs_d0_one": ("8 32 32 32 4 v gs lpl 0 d0 one 1 lbp 1", True, [1]),
-    "u64_box16_gsrb_d0_one": ("16 64 64 64 3 v gsrb lpl 0 d0 one 1 lbp 1", True, [1]),
+    "u64_box16_gsrb_d0_one": ("16 64 64 64 3 v gsrb lpl 0 d0 one 1 lbp 1", True, [1, 2, 8]),
     "nonsquare_gsrb": ("8 64 32 32 6 v gsrb lpl 0 sol sol 1 lb 1", True, [1]),
     "odd48_gsrb": ("8 48 48 48 4 v gsrb lpl 0 d0 sol 1 lb 0", True, [1]),
     "odd48_gs": ("8 48 48 48 4 v gs lpl 0 d0 sol 1 lb 0", True, [1]),
     # C3-like periodic GSRB (subtract_mean), rank counts pin the allreduce order
     "per32_gsrb_v": ("8 32 32 32 10 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 3, 4, 5, 6, 8]),
-    "per32_gs_f": ("8 32 32 32 5 f gs lpl 0 per sol 1 lb 1", True, [1]),
+    "per32_gs_f": ("8 32 32 32 5 f gs lpl 0 per sol 1 lb 1", True, [1, 4]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
-    "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1]),
+    "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),
     "helm32_gs_c0": ("8 32 32 32 5 v gs helm 10 c0 sol 1 lb 0", True, [1]),
     # §8(f) row 1: variable-coefficient Laplacian / Helmholtz (m_vlaplacian,
     # m_vhelmholtz), eps = (1.5+sin 2pi x)(1.5+sin 2pi y)(1.5+sin 2pi z)
