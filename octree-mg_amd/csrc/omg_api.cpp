@@ -420,7 +420,7 @@ double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
 
 // smooth_boxes (m_multigrid.f90:404-424)
-void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
+void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1) {
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps;
   if (!L) return;
@@ -439,7 +439,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle) {
     }
     return;
   }
-  for (int n = 1; n <= n_sub; n++) {
+  for (int n = first_substep; n <= n_sub; n++) {
     // substep n updates the cells with i+j+k+n even, i.e. colour e = n mod 2,
     // and ends with the ghost fill; same-GPU neighbours only need colour e
     // when their ghost faces were consistent before the substep.
@@ -597,6 +597,29 @@ void correct_children(omg_ctx* c, int lvl) {
     launch_sub_parents(C->view(), C->d_parents, (int)C->parents.size(), c->stream);
   }
   prolong(c, lvl, 4, 1, 1);
+}
+
+// correct_children(lvl) + fill of lvl+1 + its first up-smoothing substep in
+// one pass (k_prolong_smooth), when the level allows; returns whether it ran
+// (the caller then starts smooth_boxes at substep 2).
+bool prolong_smooth(omg_ctx* c, int lvl) {
+  Level* F = level_ptr(c, lvl + 1);
+  Level* C = level_ptr(c, lvl);
+  if (c->no_fuse_up || !F || !C || !F->prolong_smooth_ok || c->smoother != OMG_SMOOTHER_GSRB ||
+      c->n_cycle_up < 1 || F->has_rb || F->has_remote || !gs_tiled(F->nc, c->op, F->has_rb) ||
+      !((size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc) ||
+      (c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv)))
+    return false;
+  if (F->shift_pending) materialize_level(c, F);
+  {
+    Prof p(c, "prolong_smooth", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
+    launch_prolong_smooth(C->view(), F->view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
+                          bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, c->stream);
+  }
+  // colour-0 ghost halves hold pre-correction values, but the next substep
+  // reads only colour 1 and pushes colour 0 itself
+  F->phi_gc_ok = true;
+  return true;
 }
 
 // correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
@@ -948,8 +971,12 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
   }
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
-    correct_and_fill(c, l - 1);
-    smooth_boxes(c, l, c->n_cycle_up);
+    if (prolong_smooth(c, l - 1)) {
+      smooth_boxes(c, l, c->n_cycle_up, 2);
+    } else {
+      correct_and_fill(c, l - 1);
+      smooth_boxes(c, l, c->n_cycle_up);
+    }
   }
   double max_res = 0.0;
   if (want_max_res) {
@@ -1215,6 +1242,25 @@ void build_plan(omg_ctx* c) {
     F.d_pairs = to_device(pairs);
     F.d_parent_local = to_device(F.parent_local);
     F.d_dix = to_device(F.dix_packed);
+    // k_prolong_smooth needs, for every same-GPU fine face whose neighbour has
+    // another parent, that parent on this GPU as the coarse neighbour
+    F.prolong_smooth_ok = F.n > 0 && F.n_pairs == F.n;
+    const bool one_child = C.nc * 2 == F.nc;
+    for (int b = 0; b < F.n && F.prolong_smooth_ok; b++) {
+      int d[3];
+      T.child_offset(F.ids[b], d);
+      for (int nb = 1; nb <= 6; nb++) {
+        const int kind = F.h_nbk[(size_t)b * 6 + nb - 1];
+        if (kind == NB_PHYS) continue;
+        if (kind != NB_LOCAL) { F.prolong_smooth_ok = false; break; }
+        const bool low = nb & 1;
+        const bool sib = !one_child && (low ? d[(nb - 1) >> 1] == F.nc / 2 : d[(nb - 1) >> 1] == 0);
+        if (!sib && C.h_nbk[(size_t)F.parent_local[b] * 6 + nb - 1] != NB_LOCAL) {
+          F.prolong_smooth_ok = false;
+          break;
+        }
+      }
+    }
   }
   // communication buffers, sized for the largest transfer touching each level
   if (c->n_ranks > 1) {
@@ -1292,6 +1338,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->rank = rank;
     c->n_ranks = n_ranks;
     c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
+    c->no_fuse_up = getenv("OMG_NO_FUSE_UP") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));

@@ -12,23 +12,51 @@ template <int NC>
 constexpr int gsrb_lds() { return 2 * (NC / 2) * NC * NC + 6 * (NC / 2) * NC; }
 
 // One substep on box b (the workgroup's BS threads), LDS at `lds`.
-template <int NC, int OP, int BS, int NT>
+// PRE: the caller has already put colour 1-e and the colour-(1-e) ghost
+// halves into LDS (k_prolong_smooth), only rhs is loaded here.
+template <int NC, int BS>
+struct GsrbRhs {
+  static constexpr int NP2 = ((NC / 2) * NC * NC / 2 + BS - 1) / BS;   // double2 cell pairs per thread
+  double2 v[NP2];
+};
+
+// colour e of rhs for box b, into registers (issued early by callers that
+// have other latency to hide)
+template <int NC, int BS, int NT>
+__device__ __forceinline__ void gsrb_load_rhs(const LevelView& L, int e, int b, GsrbRhs<NC, BS>& fr) {
+  constexpr int HV = (NC / 2) * NC * NC;
+  const double* __restrict__ f = L.data + L.vstride + (long long)b * L.stride;
+#pragma unroll
+  for (int r = 0; r < GsrbRhs<NC, BS>::NP2; r++) {
+    const int q2 = threadIdx.x + BS * r;
+    if (q2 < HV / 2) {
+      const double2* fp = reinterpret_cast<const double2*>(f + e * HV) + q2;
+      if (NT) {
+        const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(fp));
+        fr.v[r] = make_double2(t.x, t.y);
+      } else {
+        fr.v[r] = *fp;
+      }
+    }
+  }
+}
+
+template <int NC, int OP, int BS, int NT, bool PRE = false>
 __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int e, int colours, const GcBC& bc,
                                          double* __restrict__ sendbuf, const double* __restrict__ shift, int b,
-                                         double* lds) {
+                                         double* lds, const GsrbRhs<NC, BS>* pre_rhs = nullptr) {
   constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
-  constexpr int NP2 = (HV / 2 + BS - 1) / BS;  // double2 cell pairs per thread
+  constexpr int NP2 = GsrbRhs<NC, BS>::NP2;
   double* so = lds;                            // colour 1-e of the interior
   double* se = lds + HV;                       // colour e, updated
   double* sg = lds + 2 * HV;                   // colour 1-e halves of the ghost faces
   const int tid = threadIdx.x, o = 1 - e;
   const long long boff = (long long)b * L.stride;
   double* __restrict__ u = L.phi + boff;
-  const double* __restrict__ f = L.data + L.vstride + boff;
   const OpCoef<OP> K(L, lambda);
 
   // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
-  {
+  if (!PRE) {
     const v2d* src = reinterpret_cast<const v2d*>(u + o * HV);
     v2d* dst = reinterpret_cast<v2d*>(so);
     const double m = shift ? *shift : 0.0;
@@ -51,20 +79,12 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       reinterpret_cast<v2d*>(sg + nb * FH)[r] = x;
     }
   }
-  double2 fr[NP2];
-#pragma unroll
-  for (int r = 0; r < NP2; r++) {
-    const int q2 = tid + BS * r;
-    if (q2 < HV / 2) {
-      const double2* fp = reinterpret_cast<const double2*>(f + e * HV) + q2;
-      if (NT) {
-        const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(fp));
-        fr[r] = make_double2(t.x, t.y);
-      } else {
-        fr[r] = *fp;
-      }
-    }
-  }
+  GsrbRhs<NC, BS> frs;
+  if (pre_rhs)
+    frs = *pre_rhs;
+  else
+    gsrb_load_rhs<NC, BS, NT>(L, e, b, frs);
+  const double2* fr = frs.v;
   __syncthreads();
 
   // ---- colour e update ----------------------------------------------------

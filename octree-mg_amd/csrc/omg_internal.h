@@ -92,6 +92,7 @@ struct Level {
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
   bool has_rb = false, has_remote = false, has_phys = false;
   bool all_parents = false;      // every box of this rank at this level is a parent
+  bool prolong_smooth_ok = false;  // k_prolong_smooth can serve this level (see build_plan)
   bool shift_pending = false;    // phi -= mean still to apply (see subtract_mean)
   int8_t* d_nbk = nullptr;
   int* d_nba = nullptr;
@@ -206,7 +207,8 @@ struct omg_ctx {
   hipEvent_t ev_bnd = nullptr, ev_comm = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_phi = nullptr;
   bool phi_mean_on_side = false;
-  bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)       // the pending phi mean is still being finished on stream2
+  bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)
+  bool no_fuse_up = false;             // OMG_NO_FUSE_UP: separate prolongation and first up-substep       // the pending phi mean is still being finished on stream2
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

@@ -95,6 +95,10 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 // reading it (correct_children's parent loop fused in)
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, bool sub, hipStream_t st);
+// correct_children + fill + the first up-smoothing substep (colour 1) in one
+// pass; every fine box with its parent here and no remote / refinement faces
+void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
+                           const int* dixp, const GcBC& bc, int one_child, hipStream_t st);
 // update_coarse's parent loop, LDS-tiled; false when the box size / operator
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,

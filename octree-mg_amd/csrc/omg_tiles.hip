@@ -120,6 +120,47 @@ __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv
 template <int NC>
 constexpr int prolong_cb() { return ((NC / 2 + 2) * (NC / 2 + 2) * (NC / 2 + 2) + 1) & ~1; }
 
+// The parent's octant + one face layer around it into LDS `cb` (the
+// prolongation of the octant never reads edges or corners; EDGES also loads
+// the edge cells the parent stores, for the siblings' boundary cells).  Loads
+// are all issued before any store: the res stores alias the phi/old loads, so
+// an interleaved loop would serialise every load behind the previous store.
+template <int NC, int BS, bool SUB, bool EDGES = false>
+__device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, int pb, int dx, int dy, int dz,
+                                                   double* cb) {
+  constexpr int CB = NC / 2 + 2, N = CB * CB * CB, NQ = (N + BS - 1) / BS;
+  const int tid = threadIdx.x;
+  const int n1 = Cv.nc + 1;
+  double rv[NQ];
+  int off[NQ];
+  unsigned store = 0;
+#pragma unroll
+  for (int r = 0; r < NQ; r++) {
+    const int q = tid + BS * r;
+    off[r] = -1;
+    if (q >= N) continue;
+    const int p = q % CB, s = (q / CB) % CB, t = q / (CB * CB);
+    const int nbnd = (p == 0 || p == CB - 1) + (s == 0 || s == CB - 1) + (t == 0 || t == CB - 1);
+    const int x = dx + p, y = dy + s, z = dz + t;
+    const int nghost = (x == 0 || x == n1) + (y == 0 || y == n1) + (z == 0 || z == n1);
+    if (EDGES ? (nbnd == 3 || nghost >= 2) : nbnd >= 2) continue;
+    const int o = off_cell(Cv, x, y, z);
+    off[r] = o;
+    if (SUB) {
+      rv[r] = boxp(Cv, 1, pb)[o] - boxp(Cv, 3, pb)[o];
+      if (nbnd == 0 || (nbnd == 1 && nghost)) store |= 1u << r;
+    } else {
+      rv[r] = boxp(Cv, iv, pb)[o];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NQ; r++) {
+    if (off[r] < 0) continue;
+    cb[tid + BS * r] = rv[r];
+    if (SUB && (store >> r & 1)) boxp(Cv, 4, pb)[off[r]] = rv[r];
+  }
+}
+
 template <int NC, int BS, bool SUB>
 __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
                                                  const int* parent_local, const int* dixp, const GcBC& bc,
@@ -131,22 +172,6 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
   const int tid = threadIdx.x;
   const int pb = parent_local[b], dp = dixp[b];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
-  const double* __restrict__ cu = boxp(Cv, iv, pb);
-  for (int q = tid; q < CB * CB * CB; q += BS) {
-    const int p = q % CB, s = (q / CB) % CB, t = q / (CB * CB);
-    const int nbnd = (p == 0 || p == CB - 1) + (s == 0 || s == CB - 1) + (t == 0 || t == CB - 1);
-    if (nbnd >= 2) continue;
-    const int x = dx + p, y = dy + s, z = dz + t, o = off_cell(Cv, x, y, z);
-    if (SUB) {
-      const double r = boxp(Cv, 1, pb)[o] - boxp(Cv, 3, pb)[o];
-      cb[q] = r;
-      const int n1 = Cv.nc + 1;
-      const bool ghost = x == 0 || x == n1 || y == 0 || y == n1 || z == 0 || z == n1;
-      if (nbnd == 0 || ghost) boxp(Cv, 4, pb)[o] = r;
-    } else {
-      cb[q] = cu[o];
-    }
-  }
   double* __restrict__ u = F.phi + (long long)b * F.stride;
   v2d old[NR];
 #pragma unroll
@@ -154,6 +179,7 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     const int q2 = tid + BS * r;
     if (q2 < HV) old[r] = ld_nt(u + 2 * q2);
   }
+  load_parent_octant<NC, BS, SUB>(Cv, iv, pb, dx, dy, dz, cb);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < NR; r++) {
@@ -187,6 +213,226 @@ __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, 
                                                      double* sendbuf) {
   __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
   prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, xcd_box(blockIdx.x, gridDim.x), lds);
+}
+
+// correct_children + fill + the first up-smoothing substep in one pass
+// (m_multigrid.f90:216-222 with smooth_boxes :404-424, substep 1 = colour 1).
+// The box adds the prolonged correction to both colours, and forms the ghost
+// values the substep reads (colour 0) itself: a neighbour's new boundary value
+// is its old one (still in our ghost slot) plus the prolongation at that cell,
+// computed from the neighbour's parent exactly as the neighbour computes it.
+// Colour-0 ghost halves in HBM are left stale: nothing reads them before the
+// next substep has pushed colour 0 again.
+template <int NC>
+__device__ __forceinline__ double prolong_at(const LevelView& Cv, int pc, const int dix[3], int fi, int fj,
+                                             int fk) {
+  // mg_prolong_sparse (m_prolong.f90:219-233) of res = phi - old of parent pc
+  const int ic = ((fi + 1) >> 1) + dix[0], jc = ((fj + 1) >> 1) + dix[1], kc = ((fk + 1) >> 1) + dix[2];
+  const double* ph = boxp(Cv, 1, pc);
+  const double* ol = boxp(Cv, 3, pc);
+  auto r = [&](int x, int y, int z) {
+    const int o = off_cell(Cv, x, y, z);
+    return ph[o] - ol[o];
+  };
+  const double f0 = 0.25 * r(ic, jc, kc);
+  const double fx = 0.25 * r((fi & 1) ? ic - 1 : ic + 1, jc, kc);
+  const double fy = 0.25 * r(ic, (fj & 1) ? jc - 1 : jc + 1, kc);
+  const double fz = 0.25 * r(ic, jc, (fk & 1) ? kc - 1 : kc + 1);
+  return f0 + fx + fy + fz;
+}
+
+// the parent octant (phase 1-2) shares its space with the ghost halves
+// (phase 3 on): 4 workgroups of 16^3 boxes fit one CU
+template <int NC>
+constexpr int prolong_smooth_lds() {
+  return 2 * Tl<NC>::HV + (prolong_cb<NC>() > 6 * Tl<NC>::FH ? prolong_cb<NC>() : 6 * Tl<NC>::FH);
+}
+
+template <int NC, int OP, int BS>
+__device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const LevelView& F, double lambda,
+                                                   const int* parent_local, const int* dixp, const GcBC& bc,
+                                                   int one_child, int b, double* lds) {
+  using TL = Tl<NC>;
+  constexpr int HV = TL::HV, FH = TL::FH, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
+  double* sb = lds;                     // both colours of the corrected interior (so | se of gsrb_box)
+  double* sg = lds + 2 * HV;            // colour-0 ghost halves, 6 x FH
+  double* cb = sg;                      // parent octant + face layer (res), until phase 3
+  const int tid = threadIdx.x;
+  const int pb = parent_local[b], dp = dixp[b];
+  const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
+  // all loads that do not depend on LDS first
+  double* __restrict__ u = F.phi + (long long)b * F.stride;
+  v2d old[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 < HV) old[r] = ld_nt(u + 2 * q2);
+  }
+  // ---- colour-0 ghost values from same-GPU neighbours: the neighbour's
+  // old boundary value (still in our ghost slot) + its prolongation
+  constexpr int NG = (6 * FH + BS - 1) / BS;
+  double gv[NG], rva[NG], rvc[NG];
+  unsigned defm = 0, rima = 0, rimc = 0;   // from the tile after it is loaded; rim taps
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    const int q = tid + BS * g;
+    gv[g] = 0.0;
+    if (q >= 6 * FH) continue;
+    const int nb = q / FH + 1, rr = q % FH;
+    const long long fidx = (long long)b * 6 + nb - 1;
+    if (F.nbk[fidx] != NB_LOCAL) continue;
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
+    const int c = rr / HN + 1, ah = rr % HN;
+    const int a = 2 * ah + 1 + ((1 + gpos + c) & 1);   // the colour-0 ghost cell (a, c)
+    // the neighbour's cell: along d at NC (low face) or 1 (high face)
+    const int xn = low ? NC : 1;
+    int fi, fj, fk;
+    if (d == 1) { fi = xn; fj = a; fk = c; }
+    else if (d == 2) { fi = a; fj = xn; fk = c; }
+    else { fi = a; fj = c; fk = xn; }
+    const double og = u[TL::ogh(nb, a, c)];
+    if (!one_child) {
+      // From the tile once it is loaded: a sibling's cells are the parent's
+      // own; a neighbour parent's boundary layer is our parent's ghost layer
+      // (same phi and old bits, hence same res), its ghost layer our parent's
+      // boundary.  Only where a tangential tap leaves both parents' stored
+      // cells (the parent's edge) is the neighbour parent's face ghost read.
+      gv[g] = og;
+      defm |= 1u << g;
+      const bool sib = low ? dix[d - 1] == HN : dix[d - 1] == 0;
+      if (sib) continue;
+      const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
+      const int da = d == 1 ? 1 : 0, dc = d == 3 ? 1 : 2;   // tangential dims of a and c
+      const int pa = (a + 1) >> 1, pc = (c + 1) >> 1;
+      const int oa_ = da == 0 ? dix[0] : dix[1], oc_ = dc == 1 ? dix[1] : dix[2];   // octant offsets
+      const int ta = oa_ + ((a & 1) ? pa - 1 : pa + 1), tc = oc_ + ((c & 1) ? pc - 1 : pc + 1);
+      const int n1 = NC + 1, xd = low ? NC : 1;   // the neighbour parent's boundary along d
+      const int ba = oa_ + pa, bc_ = oc_ + pc;
+      if (ta == 0 || ta == n1) {   // (d, a, c) -> (x, y, z)
+        const int o = d == 1 ? off_cell(Cv, xd, ta, bc_) : (d == 2 ? off_cell(Cv, ta, xd, bc_) : off_cell(Cv, ta, bc_, xd));
+        rva[g] = boxp(Cv, 1, pn)[o] - boxp(Cv, 3, pn)[o];
+        rima |= 1u << g;
+      }
+      if (tc == 0 || tc == n1) {
+        const int o = d == 1 ? off_cell(Cv, xd, ba, tc) : (d == 2 ? off_cell(Cv, ba, xd, tc) : off_cell(Cv, ba, tc, xd));
+        rvc[g] = boxp(Cv, 1, pn)[o] - boxp(Cv, 3, pn)[o];
+        rimc |= 1u << g;
+      }
+      continue;
+    }
+    int nd[3] = {dix[0], dix[1], dix[2]};
+    const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
+    nd[d - 1] = 0;
+    gv[g] = og + prolong_at<NC>(Cv, pn, nd, fi, fj, fk);
+  }
+  // ---- parent's res = phi - old on its octant + face layer (stored by owner)
+  load_parent_octant<NC, BS, true, true>(Cv, 4, pb, dix[0], dix[1], dix[2], cb);
+  __syncthreads();
+  // ---- phi += prolong(res), both colours; colour 0 is final here
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 >= HV) continue;
+    double nv[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int q = 2 * q2 + s;
+      int i, j, k;
+      TL::decode(q, i, j, k);
+      const int ic = (i + 1) >> 1, jc = (j + 1) >> 1, kc = (k + 1) >> 1;
+      const int c0 = ic + CB * (jc + CB * kc);
+      const double f0 = 0.25 * cb[c0];
+      const double fx = 0.25 * cb[(i & 1) ? c0 - 1 : c0 + 1];
+      const double fy = 0.25 * cb[(j & 1) ? c0 - CB : c0 + CB];
+      const double fz = 0.25 * cb[(k & 1) ? c0 - CB * CB : c0 + CB * CB];
+      const double o = s ? old[r].y : old[r].x;
+      nv[s] = o + (f0 + fx + fy + fz);
+      sb[q] = nv[s];
+    }
+    if (2 * q2 < HV) st_nt(u + 2 * q2, nv[0], nv[1]);   // colour 0 to HBM
+  }
+  // neighbours' boundary cells from the tile (+ rim taps)
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    if (!(defm >> g & 1)) continue;
+    const int q = tid + BS * g;
+    const int nb = q / FH + 1, rr = q % FH;
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
+    const int c = rr / HN + 1, ah = rr % HN;
+    const int a = 2 * ah + 1 + ((1 + gpos + c) & 1);
+    const int pd = low ? 0 : CB - 1, pa = (a + 1) >> 1, pc = (c + 1) >> 1;
+    // cb strides of the normal and the two tangential directions
+    const int sn = d == 1 ? 1 : (d == 2 ? CB : CB * CB);
+    const int sa = d == 1 ? CB : 1, sc = d == 3 ? CB : CB * CB;
+    const int c0 = pd * sn + pa * sa + pc * sc;
+    // parity of the neighbour's fine index: NC (low face, even) or 1 (high, odd)
+    const double tn = cb[low ? c0 + sn : c0 - sn];
+    const double ta = (rima >> g & 1) ? rva[g] : cb[(a & 1) ? c0 - sa : c0 + sa];
+    const double tc = (rimc >> g & 1) ? rvc[g] : cb[(c & 1) ? c0 - sc : c0 + sc];
+    const double f0 = 0.25 * cb[c0];
+    const double fx = 0.25 * (d == 1 ? tn : ta);
+    const double fy = 0.25 * (d == 1 ? ta : (d == 2 ? tn : tc));
+    const double fz = 0.25 * (d == 3 ? tn : tc);
+    gv[g] = gv[g] + (f0 + fx + fy + fz);
+  }
+  __syncthreads();
+  // ---- colour-0 ghost values the substep reads (physical faces from the
+  // corrected boundary cells: bc_to_gc)
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    const int q = tid + BS * g;
+    if (q >= 6 * FH) continue;
+    const int nb = q / FH + 1, rr = q % FH;
+    const long long fidx = (long long)b * 6 + nb - 1;
+    const int kind = F.nbk[fidx];
+    if (kind == NB_PHYS) {
+      const bool low = nb & 1;
+      const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
+      const int c = rr / HN + 1, ah = rr % HN;
+      const int a = 2 * ah + 1 + ((1 + gpos + c) & 1);
+      const int x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
+      int i1, j1, k1;
+      if (d == 1) { i1 = x1; j1 = a; k1 = c; }
+      else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
+      else { i1 = a; j1 = c; k1 = x1; }
+      const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
+      gv[g] = phys_ghost(F, bc, b, fidx, nb, F.nba[fidx], a, c, TL::ogh(nb, a, c), sb[TL::oint(i1, j1, k1)],
+                         sb[TL::oint(i2, j2, k2)]);
+    }
+    sg[(nb - 1) * FH + rr] = gv[g];
+  }
+  __syncthreads();
+  // ---- substep 1: colour 1 from colour 0, then its ghost fill (push colour 1)
+  gsrb_box<NC, OP, BS, 2, true>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds);
+}
+
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
+                                                       const int* parent_local, const int* dixp, GcBC bc,
+                                                       int one_child) {
+  __shared__ double lds[prolong_smooth_lds<NC>()];
+  prolong_smooth_box<NC, OP, BS>(Cv, F, lambda, parent_local, dixp, bc, one_child,
+                                 xcd_box(blockIdx.x, gridDim.x), lds);
+}
+
+void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
+                           const int* dixp, const GcBC& bc, int one_child, hipStream_t st) {
+  if (F.n == 0) return;
+  const dim3 g(F.n);
+#define OMG_PS(NC, BS)                                                                                \
+  if (op == OP_HELM)                                                                                  \
+    k_prolong_smooth<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child); \
+  else                                                                                                \
+    k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child);
+  switch (F.nc) {
+    case 16: OMG_PS(16, 512) break;
+    case 8: OMG_PS(8, 256) break;
+    case 4: OMG_PS(4, 256) break;
+    default: OMG_PS(2, 256) break;
+  }
+#undef OMG_PS
 }
 
 // get_sum's per-leaf interior sums (m_multigrid.f90:286-290): one lane per

@@ -62,7 +62,8 @@ SIGNATURES = {
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "libomg.so")
+    # OMG_LIB: another build of the same library (kernel A/B timing only)
+    return os.environ.get("OMG_LIB") or os.path.join(_HERE, "libomg.so")
 
 
 def lib():

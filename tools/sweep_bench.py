@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the level-1 smoother at 512^3 (box 16, periodic, GSRB):
-times smooth_boxes(highest_lvl, n_cycle) in isolation, for rocprofv3 PMC
+times smooth_boxes(highest_lvl, n_cycle) (or another level op, or a
+whole V-cycle) in isolation, for rocprofv3 PMC
 passes and kernel A/B work.  Usage: tools/sweep_bench.py [reps] [domain]"""
 import os
 import sys
@@ -20,6 +21,8 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 512
     which = sys.argv[3] if len(sys.argv) > 3 else "smooth"
+    if which == "vcycle_nofuse":
+        os.environ["OMG_NO_FUSE_UP"] = "1"
     mg = omg.MG()
     mg.smoother_type = T.MG_SMOOTHER_GSRB
     omg.mg_set_methods(mg)
@@ -40,6 +43,8 @@ def main():
         "fill": lambda: c.call("fill_ghost_cells_lvl", hi, 1),
         "update_coarse": lambda: c.call("update_coarse", hi),
         "correct": lambda: c.call("correct_children", hi - 1),
+        "vcycle": lambda: omg.mg_fas_vcycle(mg),
+        "vcycle_nofuse": lambda: omg.mg_fas_vcycle(mg),
     }
     f = ops[which]
     for _ in range(3):
