@@ -83,6 +83,45 @@ __device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc,
   return c0 * bv + c1 * x1v + c2 * x2v;
 }
 
+// Same-GPU ghost pushes of box b: for every face with a LOCAL neighbour, the
+// boundary cells of the colours in `colours` go to the neighbour's ghost
+// half, two consecutive slots of the half per thread as one 16-B store (the
+// half of colour e on the opposite face lists exactly our colour-e boundary
+// cells, in the same order).  get(i, j, k) reads our (final) interior value.
+template <int NC, int NT, class Get>
+__device__ __forceinline__ void face_push_local(const LevelView& L, int b, int colours, Get get) {
+  using TL = Tl<NC>;
+  constexpr int H = TL::H, PF = TL::FH / 2;   // 16-B pairs per face half
+  const int ncol = (colours & 1) + ((colours >> 1) & 1);
+  const int c_first = (colours & 1) ? 0 : 1;
+  for (int p = threadIdx.x; p < 6 * PF * ncol; p += blockDim.x) {
+    const int f = p / (PF * ncol), rem = p % (PF * ncol);
+    const int col = ncol == 2 ? rem / PF : c_first, r = rem % PF;
+    const long long fidx = (long long)b * 6 + f;
+    if (L.nbk[fidx] != NB_LOCAL) continue;
+    const int nb = f + 1;
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1, x1 = low ? 1 : NC;
+    double v[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int hi = 2 * r + s, ah = hi % H, c = hi / H + 1;
+      const int a = 2 * ah + 1 + ((col + x1 + 1 + c) & 1);
+      if (d == 1) v[s] = get(x1, a, c);
+      else if (d == 2) v[s] = get(a, x1, c);
+      else v[s] = get(a, c, x1);
+    }
+    const int nbo = low ? nb + 1 : nb - 1;
+    v2d* dst = reinterpret_cast<v2d*>(L.phi + (long long)L.nba[fidx] * L.stride + 2 * TL::HV +
+                                      (nbo - 1) * TL::FS + col * TL::FH) + r;
+    const v2d x = {v[0], v[1]};
+    if (NT >= 2)
+      __builtin_nontemporal_store(x, dst);
+    else
+      *dst = x;
+  }
+}
+
 // Ghost fill of phi for box b whose final interior is staged in LDS `sb`
 // (Tl<NC> layout): same-GPU faces pushed (colours mask), physical ghosts
 // recomputed, remote faces packed.  Refinement boundaries are not handled
@@ -91,12 +130,14 @@ template <int NC>
 __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const double* sb, int colours,
                                                const GcBC& bc, double* sendbuf) {
   using TL = Tl<NC>;
+  face_push_local<NC, 0>(L, b, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
   double* u = L.phi + (long long)b * L.stride;
   for (int p = threadIdx.x; p < 6 * NC * NC; p += blockDim.x) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
-    const int a = cell % NC + 1, c = cell / NC + 1;
     const long long fidx = (long long)b * 6 + nb - 1;
-    const int kind = L.nbk[fidx], arg = L.nba[fidx];
+    const int kind = L.nbk[fidx];
+    if (kind == NB_LOCAL) continue;
+    const int a = cell % NC + 1, c = cell / NC + 1, arg = L.nba[fidx];
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
     int i1, j1, k1;
@@ -104,10 +145,7 @@ __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const 
     else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
     else { i1 = a; j1 = c; k1 = x1; }
     const double v1 = sb[TL::oint(i1, j1, k1)];
-    if (kind == NB_LOCAL) {
-      if ((colours >> ((i1 + j1 + k1) & 1)) & 1)
-        L.phi[(long long)arg * L.stride + TL::ogh(low ? nb + 1 : nb - 1, a, c)] = v1;
-    } else if (kind == NB_REMOTE) {
+    if (kind == NB_REMOTE) {
       sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
     } else if (kind == NB_PHYS) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;

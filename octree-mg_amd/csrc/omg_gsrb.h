@@ -154,38 +154,32 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   __syncthreads();
 
   // ---- ghost fill after the substep ---------------------------------------
+  auto cellv = [&](int i, int j, int k) {
+    const int idx = ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
+    return ((i + j + k) & 1) == e ? se[idx] : so[idx];
+  };
+  face_push_local<NC, NT>(L, b, colours, cellv);
   for (int p = tid; p < 6 * NC * NC; p += BS) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
-    const int a = cell % NC + 1, c = cell / NC + 1;
     const long long fidx = (long long)b * 6 + nb - 1;
-    const int kind = L.nbk[fidx], arg = L.nba[fidx];
+    const int kind = L.nbk[fidx];
+    if (kind == NB_LOCAL) continue;
+    const int a = cell % NC + 1, c = cell / NC + 1, arg = L.nba[fidx];
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1;
-    // boundary cell x1 (and x2) of this face: colour and index
+    // boundary cell x1 (and x2) of this face
     const int x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
     int i1, j1, k1;
     if (d == 1) { i1 = x1; j1 = a; k1 = c; }
     else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
     else { i1 = a; j1 = c; k1 = x1; }
-    const int c1 = (i1 + j1 + k1) & 1;
-    const int idx1 = ((i1 - 1) >> 1) + H * ((j1 - 1) + NC * (k1 - 1));
-    const double v1 = c1 == e ? se[idx1] : so[idx1];
-    if (kind == NB_LOCAL) {
-      if ((colours >> c1) & 1) {
-        double* gp = L.phi + (long long)arg * L.stride + off_gh(L, low ? nb + 1 : nb - 1, a, c);
-        if (NT >= 2)
-          __builtin_nontemporal_store(v1, gp);
-        else
-          *gp = v1;
-      }
-    } else if (kind == NB_REMOTE) {
+    const double v1 = cellv(i1, j1, k1);
+    if (kind == NB_REMOTE) {
       sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
     } else {  // NB_PHYS (refinement boundaries take the generic kernel)
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
-      const int idx2 = ((i2 - 1) >> 1) + H * ((j2 - 1) + NC * (k2 - 1));
-      const double v2 = c1 == e ? so[idx2] : se[idx2];   // x2 has the other colour
       const int gi = off_gh(L, nb, a, c);
-      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, v2);
+      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, cellv(i2, j2, k2));
     }
   }
 }
