@@ -88,7 +88,7 @@ __device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc,
 // half, two consecutive slots of the half per thread as one 16-B store (the
 // half of colour e on the opposite face lists exactly our colour-e boundary
 // cells, in the same order).  get(i, j, k) reads our (final) interior value.
-template <int NC, int NT, class Get>
+template <int NC, class Get>
 __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int colours, Get get) {
   using TL = Tl<NC>;
   constexpr int H = TL::H, PF = TL::FH / 2;   // 16-B pairs per face half
@@ -114,11 +114,9 @@ __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int c
     const int nbo = low ? nb + 1 : nb - 1;
     v2d* dst = reinterpret_cast<v2d*>(L.phi + (long long)L.nba[fidx] * L.stride + 2 * TL::HV +
                                       (nbo - 1) * TL::FS + col * TL::FH) + r;
-    const v2d x = {v[0], v[1]};
-    if (NT >= 2)
-      __builtin_nontemporal_store(x, dst);
-    else
-      *dst = x;
+    // default cache policy even in the streaming kernels: measured 5 % faster
+    // per substep than non-temporal stores for these 1-KB face halves
+    *dst = v2d{v[0], v[1]};
   }
 }
 
@@ -130,7 +128,7 @@ template <int NC>
 __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const double* sb, int colours,
                                                const GcBC& bc, double* sendbuf) {
   using TL = Tl<NC>;
-  face_push_local<NC, 0>(L, b, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
+  face_push_local<NC>(L, b, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
   double* u = L.phi + (long long)b * L.stride;
   for (int p = threadIdx.x; p < 6 * NC * NC; p += blockDim.x) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);

@@ -158,7 +158,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     const int idx = ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
     return ((i + j + k) & 1) == e ? se[idx] : so[idx];
   };
-  face_push_local<NC, NT>(L, b, colours, cellv);
+  face_push_local<NC>(L, b, colours, cellv);
   for (int p = tid; p < 6 * NC * NC; p += BS) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
     const long long fidx = (long long)b * 6 + nb - 1;
