@@ -52,7 +52,7 @@ def pmc_traffic():
         try:
             d = json.load(open(f))
             for k, e in d["kernels"].items():
-                if k.startswith("void omg::k_gsrb_tile<16, 1>") and "hbm_bytes_per_launch" in e:
+                if re.match(r"void omg::k_gsrb_tile<16, 1[,>]", k) and "hbm_bytes_per_launch" in e:
                     if e["workgroups"] == (PER_GPU // BOX) ** 3:
                         return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
         except (OSError, ValueError, KeyError):
