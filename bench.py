@@ -36,6 +36,7 @@ import __graft_entry__  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 PER_GPU = 512
 BOX = 16
+REPLICATE_CELLS = int(os.environ.get("OMG_REPLICATE_CELLS", 64 * 16 ** 3))
 
 
 KERNEL_FAMILIES = ("smoother_gsrb", "fill_gc", "resid_restrict", "residual", "restrict",
@@ -87,18 +88,20 @@ def build(omg, n_ranks, dev):
                            [True] * 3, 0)
     omg.mg_load_balance(mg)
     omg.mg_set_methods(mg)
+    # coarse levels of at most 64 boxes of 16^3 live on every GPU: no
+    # latency-bound exchanges below them (omg_set_coarse_replication)
+    mg.coarse_replication_cells = REPLICATE_CELLS
     t1 = time.time()
     omg.mg_allocate_storage(mg, device_index=dev)
-    # u on every level, rhs = L_h u, phi = 0 (tests/test_uniform_grid.f90:137-170)
+    # u on every level, rhs = L_h u, phi = 0 (tests/test_uniform_grid.f90:137-170);
+    # every rank uploads every level (collective on replicated levels)
     for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
         ids = mg.lvls[lvl].my_ids
-        if len(ids):
-            mg.set_level(lvl, T.MG_IPHI, omg.problems.level_solution(mg, lvl, ids))
+        mg.set_level(lvl, T.MG_IPHI, omg.problems.level_solution(mg, lvl, ids))
     omg.mg_apply_op(mg, T.MG_IRHS)
     for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
         n, nc = mg.ctx.level_size(lvl)
-        if n:
-            mg.set_level(lvl, T.MG_IPHI, np.zeros((n, nc + 2, nc + 2, nc + 2)))
+        mg.set_level(lvl, T.MG_IPHI, np.zeros((n, nc + 2, nc + 2, nc + 2)))
     mg.ctx.call("synchronize")
     return mg, domain, t1 - t0, time.time() - t1
 

@@ -88,6 +88,23 @@ int omg_set_smoother(omg_ctx *ctx, int smoother, int n_cycle_down, int n_cycle_u
                      double residual_coarse_rel);
 int omg_set_subtract_mean(omg_ctx *ctx, int on);
 
+/* Replicated coarse levels (no reference counterpart: a scaling option of
+ * this library, call before omg_tree_setup).  With n_ranks > 1, the lowest
+ * levels, as long as each holds at most max_cells cells and has neither leaves
+ * nor refinement boundaries, are kept on EVERY rank instead of being split by
+ * mg%boxes(:)%rank: the restriction into the highest such level is sent to all
+ * ranks and the levels below it run without any exchange (the latency-bound
+ * part of a multi-GPU V-cycle).  Results are bit-identical (every box computes
+ * the same arithmetic; get_sum only reads leaves).  The host still sees its
+ * own partition: omg_level_size / omg_download_level cover the boxes
+ * mg_load_balance gave this rank, and omg_upload_level on a replicated level
+ * is collective (every rank calls it, with its own boxes, possibly none).
+ * Boundary tables (omg_set_bc_faces) must cover every box of a replicated
+ * level.  0 (the default) = off.  omg_replicated_level gives the highest
+ * replicated level (lowest_lvl - 1: none). */
+int omg_set_coarse_replication(omg_ctx *ctx, long long max_cells);
+int omg_replicated_level(omg_ctx *ctx, int *lvl);
+
 /* Boundary conditions for variable iv (mg%bc(nb, iv), src/m_data_structures
  * .f90:235-242).  omg_set_bc_faces tabulates a boundary_cond callback:
  * face_off[(id-1)*6 + nb-1] = offset of nc*nc values in data (first
@@ -136,10 +153,12 @@ int omg_phi_bc_store(omg_ctx *ctx);                   /* mg_phi_bc_store, m_ghos
 
 /* The communication plan of level lvl as built by omg_tree_setup: transfer
  * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,
- * 3 refinement-boundary faces), direction dir (0 send, 1 receive); fills
+ * 3 refinement-boundary faces, 4 copies of the host's boxes of a replicated
+ * level), direction dir (0 send, 1 receive); fills
  * min(cap, n) (peer, key) pairs in wire order.  Keys are the ordering keys of
  * sort_and_transfer_buffers (src/m_communication.f90:37-66): 6*id+nb for
- * faces, 8*parent+child slot for restriction, child id for prolongation. */
+ * faces, 8*parent+child slot for restriction, child id for prolongation,
+ * box id for replicated-level copies. */
 int omg_plan_transfer(omg_ctx *ctx, int lvl, int which, int dir, int cap, int *peers,
                       long long *keys, int *n_items, int *item_doubles);
 

@@ -625,7 +625,9 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
 // correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
 // V-cycle and FMG run them (m_multigrid.f90:127-136, 216-219); fused when every
 // box of lvl+1 has its parent on this GPU and no refinement boundary.
-void correct_and_fill(omg_ctx* c, int lvl) {
+// then_gsrb: the caller smooths lvl+1 with red-black substeps right after
+// (colour 1 first), so colour 1's correction is dead where no face needs it.
+void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
   if (F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
@@ -640,7 +642,7 @@ void correct_and_fill(omg_ctx* c, int lvl) {
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
-                          F->d_sendbuf, sub, c->stream);
+                          F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream);
     }
     finish_halo(c, F, 1);
     F->phi_gc_ok = true;
@@ -961,7 +963,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     // coarse grid: all its boxes live on one rank (error stop otherwise, :197-200)
     const auto& ids = c->ids[min_lvl];
     for (int id : ids)
-      if (c->rank_of[id - 1] != c->rank_of[ids[0] - 1])
+      if (min_lvl > c->rep_lvl && c->rank_of[id - 1] != c->rank_of[ids[0] - 1])
         throw OmgError("Multiple CPUs for coarse grid (not implemented yet)");
     double init_res = max_residual_lvl(c, min_lvl);
     for (int i = 1; i <= c->max_coarse_cycles; i++) {
@@ -974,7 +976,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     if (prolong_smooth(c, l - 1)) {
       smooth_boxes(c, l, c->n_cycle_up, 2);
     } else {
-      correct_and_fill(c, l - 1);
+      correct_and_fill(c, l - 1, c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_up >= 1);
       smooth_boxes(c, l, c->n_cycle_up);
     }
   }
@@ -1030,7 +1032,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int);
-    for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx}) {
+    for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
     }
@@ -1049,18 +1051,53 @@ void build_plan(omg_ctx* c) {
   Tree T{c};
   const int me = c->rank;
   c->local_index.assign(c->n_boxes + 1, -1);
+  // Replicated coarse levels: the lowest levels, while they hold at most
+  // rep_cells cells and neither leaves nor refinement boundaries, live on every
+  // rank.  Their exchanges (latency-bound at a few boxes per GPU) disappear:
+  // the restriction into the highest replicated level goes to every rank, and
+  // the prolongation out of it is local everywhere.  Bits do not change: each
+  // box's arithmetic is the same wherever it runs, and get_sum reads leaves only.
+  c->rep_lvl = INT_MIN;
+  if (c->rep_cells > 0 && c->n_ranks > 1)
+    for (int l = c->lowest; l < c->highest; l++) {
+      const long long nc = c->bsl[l];
+      if ((long long)c->ids[l].size() * nc * nc * nc > c->rep_cells || !c->leaves[l].empty() ||
+          !c->ref_bnds[l].empty())
+        break;
+      c->rep_lvl = l;
+    }
+  auto owns = [&](int id) { return T.lvl(id) <= c->rep_lvl || T.rank(id) == me; };
   for (int l = c->lowest; l <= c->highest; l++) {
     Level& L = c->levels[l];
     L.lvl = l;
     L.nc = c->bsl[l];
+    L.replicated = l <= c->rep_lvl;
     for (int d = 0; d < 3; d++) L.dr[d] = c->drl[l][d];
     for (int id : c->ids[l])
-      if (T.rank(id) == me) {
+      if (owns(id)) {
         c->local_index[id] = (int)L.ids.size();
+        if (T.rank(id) == me) L.host_local.push_back((int)L.ids.size());
         L.ids.push_back(id);
       }
     L.n = (int)L.ids.size();
     L.stride = ((stored_cells(L.nc) + 63) / 64) * 64;   // 512-B aligned boxes
+    if (L.replicated) {
+      // the host's boxes of this level go to every peer (upload_level)
+      std::vector<Rec> rs, rr;
+      for (int b = 0; b < L.n; b++) {
+        const int id = L.ids[b];
+        if (T.rank(id) == me) {
+          for (int r = 0; r < c->n_ranks; r++)
+            if (r != me) rs.push_back({r, (long long)id, b, 0});
+        } else {
+          rr.push_back({T.rank(id), (long long)id, b, 0});
+        }
+      }
+      L.repl.send = group(rs, 1);
+      L.repl.recv = group(rr, 1);
+      L.repl.item_doubles = (int)L.stride;
+      finalize_transfer(L.repl);
+    }
   }
   for (int l = c->lowest; l <= c->highest; l++) {
     Level& L = c->levels[l];
@@ -1080,7 +1117,7 @@ void build_plan(omg_ctx* c) {
         const int nid = T.nbr(id, nb);
         const size_t f = (size_t)b * 6 + nb - 1;
         if (nid > 0) {
-          if (T.rank(nid) == me) {
+          if (owns(nid)) {
             L.h_nbk[f] = NB_LOCAL;
             L.h_nba[f] = c->local_index[nid];
           } else {
@@ -1094,7 +1131,7 @@ void build_plan(omg_ctx* c) {
           const int p_id = T.parent(id);
           const int p_nb = p_id > 0 ? T.nbr(p_id, nb) : 0;
           if (p_nb <= 0) throw OmgError("refinement boundary without coarse neighbour");
-          if (T.rank(p_nb) != me) {
+          if (!owns(p_nb)) {
             L.h_nbk[f] = NB_RBREM;
             rbrecv.push_back({T.rank(p_nb), (long long)id * 6 + nb, (int)f, 0});
             continue;
@@ -1114,7 +1151,8 @@ void build_plan(omg_ctx* c) {
     // coarse side of the refinement boundaries toward other ranks: my
     // ref_bnds at lvl-1 next to a refined box with children elsewhere
     // (buffer_refinement_boundaries, m_ghost_cells.f90:200-229)
-    if (l > c->lowest)
+    // (a replicated coarse level is on every rank: nothing to send)
+    if (l > c->lowest && l - 1 > c->rep_lvl)
       for (int cid : c->ref_bnds[l - 1]) {
         if (T.rank(cid) != me) continue;
         for (int nb = 1; nb <= 6; nb++) {
@@ -1181,9 +1219,9 @@ void build_plan(omg_ctx* c) {
     L.d_rb = to_device(L.h_rb);
     // parents / leaves (my_parents, my_leaves) as local indices
     for (int id : c->parents[l])
-      if (T.rank(id) == me) L.parents.push_back(c->local_index[id]);
+      if (owns(id)) L.parents.push_back(c->local_index[id]);
     for (int id : c->leaves[l])
-      if (T.rank(id) == me) L.leaves.push_back(c->local_index[id]);
+      if (owns(id)) L.leaves.push_back(c->local_index[id]);
     L.d_parents = to_device(L.parents);
     L.d_leaves = to_device(L.leaves);
     dmalloc(&L.d_scratch, sizeof(double) * L.leaves.size());
@@ -1207,9 +1245,14 @@ void build_plan(omg_ctx* c) {
       int slot = 0;
       for (int s = 1; s <= 8; s++)
         if (T.child(p, s) == id) slot = s;
-      if (T.rank(p) == me) {
+      if (owns(p)) {
         F.parent_local[b] = c->local_index[p];
         pairs.push_back(b);
+        // a replicated parent of a distributed child: every peer restricts
+        // into its own copy of the parent
+        if (C.replicated && !F.replicated)
+          for (int r = 0; r < c->n_ranks; r++)
+            if (r != me) rsend.push_back({r, (long long)p * 8 + slot, b, 0});
       } else {
         rsend.push_back({T.rank(p), (long long)p * 8 + slot, b, 0});   // restrict_set_buffer
         precv.push_back({T.rank(p), (long long)id, b, 0});             // prolong_onto remote
@@ -1219,11 +1262,12 @@ void build_plan(omg_ctx* c) {
       const int p = C.ids[pb];
       for (int s = 1; s <= 8; s++) {
         const int ch = T.child(p, s);
-        if (ch <= 0 || T.rank(ch) == me) continue;
+        if (ch <= 0 || owns(ch)) continue;
         int d[3];
         T.child_offset(ch, d);
         rrecv.push_back({T.rank(ch), (long long)p * 8 + s, pb, pack_dix(d)});   // restrict_onto
-        psend.push_back({T.rank(ch), (long long)ch, pb, pack_dix(d)});          // prolong_set_buffer
+        // (the child's owner holds a replicated parent itself)
+        if (!C.replicated) psend.push_back({T.rank(ch), (long long)ch, pb, pack_dix(d)});   // prolong_set_buffer
       }
     }
     F.restr.send = group(rsend, 1);
@@ -1270,6 +1314,8 @@ void build_plan(omg_ctx* c) {
       auto upd = [](std::map<int, size_t>& m, int k, size_t v) { m[k] = std::max(m[k], v); };
       upd(sendn, l, (size_t)L.halo.n_send * L.halo.item_doubles);
       upd(recvn, l, (size_t)L.halo.n_recv * L.halo.item_doubles);
+      upd(sendn, l, (size_t)L.repl.n_send * L.repl.item_doubles);
+      upd(recvn, l, (size_t)L.repl.n_recv * L.repl.item_doubles);
       if (l > c->lowest) {
         upd(sendn, l, (size_t)L.restr.n_send * L.restr.item_doubles);      // fine side packs
         upd(recvn, l - 1, (size_t)L.restr.n_recv * L.restr.item_doubles);  // coarse side receives
@@ -1339,6 +1385,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->n_ranks = n_ranks;
     c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
     c->no_fuse_up = getenv("OMG_NO_FUSE_UP") != nullptr;
+    c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
@@ -1474,8 +1521,8 @@ int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* pee
   return guarded([&] {
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
-    if (which < 0 || which > 3) throw OmgError("omg_plan_transfer: bad transfer");
-    const Transfer* T[4] = {&L->halo, &L->restr, &L->prol, &L->rbx};
+    if (which < 0 || which > 4) throw OmgError("omg_plan_transfer: bad transfer");
+    const Transfer* T[5] = {&L->halo, &L->restr, &L->prol, &L->rbx, &L->repl};
     const auto& lists = dir ? T[which]->recv : T[which]->send;
     int n = 0;
     for (auto& p : lists)
@@ -1553,6 +1600,20 @@ int omg_set_bc_faces(omg_ctx* c, int iv, const long long* face_off, const int* f
       std::vector<long long> off(L.n * 6, -1);
       std::vector<int> typ(L.n * 6, 0);
       const long long n2 = (long long)L.nc * L.nc;
+      if (L.replicated) {
+        // every copy needs the table: a face tabulated for one box of the
+        // level must be tabulated for every box with that physical face
+        bool any[6] = {}, miss[6] = {};
+        for (int b = 0; b < L.n; b++)
+          for (int nb = 0; nb < 6; nb++) {
+            if (L.h_nbk[(size_t)b * 6 + nb] != NB_PHYS) continue;
+            (face_off[(size_t)(L.ids[b] - 1) * 6 + nb] >= 0 ? any : miss)[nb] = true;
+          }
+        for (int nb = 0; nb < 6; nb++)
+          if (any[nb] && miss[nb])
+            throw OmgError("omg_set_bc_faces: replicated level " + std::to_string(L.lvl) +
+                           " needs the boundary table of every box (omg_replicated_level)");
+      }
       for (int b = 0; b < L.n; b++)
         for (int nb = 0; nb < 6; nb++) {
           const long long o = face_off[(size_t)(L.ids[b] - 1) * 6 + nb];
@@ -1573,9 +1634,21 @@ int omg_level_size(omg_ctx* c, int lvl, int* n_boxes, int* nc) {
   return guarded([&] {
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
-    *n_boxes = L->n;
+    *n_boxes = (int)L->host_local.size();
     *nc = L->nc;
   });
+}
+
+int omg_set_coarse_replication(omg_ctx* c, long long max_cells) {
+  return guarded([&] {
+    if (!c->levels.empty()) throw OmgError("omg_set_coarse_replication: call before omg_tree_setup");
+    if (max_cells < 0) throw OmgError("omg_set_coarse_replication: max_cells < 0");
+    c->rep_cells = max_cells;
+  });
+}
+
+int omg_replicated_level(omg_ctx* c, int* lvl) {
+  return guarded([&] { *lvl = c->rep_lvl == INT_MIN ? c->lowest - 1 : c->rep_lvl; });
 }
 
 // staging buffer in the reference's box layout
@@ -1595,9 +1668,24 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
     if (!L->n) return;
-    const size_t s = L->nc + 2, n = s * s * s * L->n;
+    const size_t s = L->nc + 2, box = s * s * s, n = box * L->n;
     if (iv == 1) L->phi_gc_ok = false;
     double* st = stage(c, n);
+    if (L->replicated) {
+      // the host's boxes into their slots, then to every peer (collective)
+      std::vector<double> full(n, 0.0);
+      for (size_t q = 0; q < L->host_local.size(); q++)
+        std::memcpy(full.data() + box * L->host_local[q], host + box * q, sizeof(double) * box);
+      HIPCHK(hipMemcpyAsync(st, full.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+      launch_from_ref(L->view(), iv, st, c->stream);
+      if (L->repl.n_send || L->repl.n_recv) {
+        launch_box_pack(L->view(), iv, L->repl.d_send_items, L->repl.n_send, L->d_sendbuf, c->stream);
+        exchange(c, L->repl, L->d_sendbuf, L->d_recvbuf);
+        launch_box_unpack(L->view(), iv, L->repl.d_recv_items, L->repl.n_recv, L->d_recvbuf, c->stream);
+      }
+      HIPCHK(hipStreamSynchronize(c->stream));
+      return;
+    }
     HIPCHK(hipMemcpyAsync(st, host, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
     launch_from_ref(L->view(), iv, st, c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1611,9 +1699,17 @@ int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
     if (!L->n) return;
-    const size_t s = L->nc + 2, n = s * s * s * L->n;
+    const size_t s = L->nc + 2, box = s * s * s, n = box * L->n;
     double* st = stage(c, n);
     launch_to_ref(L->view(), iv, st, c->stream);
+    if (L->replicated) {   // the host's boxes only
+      std::vector<double> full(n);
+      HIPCHK(hipMemcpyAsync(full.data(), st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      for (size_t q = 0; q < L->host_local.size(); q++)
+        std::memcpy(host + box * q, full.data() + box * L->host_local[q], sizeof(double) * box);
+      return;
+    }
     HIPCHK(hipMemcpyAsync(host, st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   });

@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -87,6 +88,12 @@ struct Level {
   long long stride = 0;
   double dr[3] = {0, 0, 0};
   std::vector<int> ids;                 // global ids of my boxes (my_ids order)
+  // Replicated coarse level (omg_set_coarse_replication): every rank holds
+  // every box; host_local lists the boxes the host's partition gives this rank
+  // (what upload/download/level_size see), repl copies them to the peers.
+  bool replicated = false;
+  std::vector<int> host_local;
+  Transfer repl;
   double* d_data = nullptr;
   double* d_phi = nullptr;              // phi (d_data's var 1)
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
@@ -188,6 +195,8 @@ struct omg_ctx {
   std::map<int, std::vector<double>> drl;   // dr per level
   std::map<int, std::vector<int>> ids, leaves, parents, ref_bnds;
   std::vector<int> local_index;             // id -> local index at its level (or -1)
+  long long rep_cells = 0;                  // replicate coarse levels up to this many cells (0: off)
+  int rep_lvl = INT_MIN;                    // highest replicated level (INT_MIN: none)
   std::map<int, omg::Level> levels;
   // method configuration
   int op = omg::OP_LPL, smoother = 1, n_substeps = 1;
@@ -208,7 +217,8 @@ struct omg_ctx {
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_phi = nullptr;
   bool phi_mean_on_side = false;
   bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)
-  bool no_fuse_up = false;             // OMG_NO_FUSE_UP: separate prolongation and first up-substep       // the pending phi mean is still being finished on stream2
+  bool no_fuse_up = false;             // OMG_NO_FUSE_UP: separate prolongation and first up-substep
+  bool no_skip1 = false;               // OMG_NO_SKIP1: correct colour 1 before the up-smoothing too
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

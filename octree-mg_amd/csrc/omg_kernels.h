@@ -43,6 +43,8 @@ void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* 
                      const int* parent_local, const int* dixp, hipStream_t st);
 void launch_restrict_pack(const LevelView& F, int iv, const int* items, int n, double* buf,
                           hipStream_t st);
+void launch_box_pack(const LevelView& L, int iv, const int* items, int n, double* buf, hipStream_t st);
+void launch_box_unpack(const LevelView& L, int iv, const int* items, int n, const double* buf, hipStream_t st);
 void launch_restrict_unpack(const LevelView& C, int iv, const int* items, int n, int hnc,
                             const double* buf, hipStream_t st);
 void launch_coarse_rhs(const LevelView& C, int op, double lambda, const int* parents, int n_par,
@@ -92,9 +94,11 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st);
 // sub: form the parent's res = phi - old on the fly (and store it) instead of
-// reading it (correct_children's parent loop fused in)
+// reading it (correct_children's parent loop fused in); skip1: a colour-1
+// red-black substep follows, so all-local boxes correct and push colour 0 only
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
-                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, hipStream_t st);
+                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
+                         hipStream_t st);
 // correct_children + fill + the first up-smoothing substep (colour 1) in one
 // pass; every fine box with its parent here and no remote / refinement faces
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,

@@ -234,6 +234,23 @@ __global__ void __launch_bounds__(256) k_restrict_pack(LevelView F, int iv, cons
   }
 }
 
+// Whole stored boxes of one variable (replicated coarse levels: the host's
+// boxes go to every peer after an upload).
+__global__ void __launch_bounds__(256) k_box_pack(LevelView L, int iv, const int* items, int n_items,
+                                                  double* buf) {
+  GRID_STRIDE(t, L.stride * n_items) {
+    const int q = (int)(t / L.stride);
+    buf[t] = boxp(L, iv, items[q])[t % L.stride];
+  }
+}
+__global__ void __launch_bounds__(256) k_box_unpack(LevelView L, int iv, const int* items, int n_items,
+                                                    const double* buf) {
+  GRID_STRIDE(t, L.stride * n_items) {
+    const int q = (int)(t / L.stride);
+    boxp(L, iv, items[q])[t % L.stride] = buf[t];
+  }
+}
+
 // restrict_onto's remote branch: items = (parent local idx, packed dix) pairs.
 __global__ void __launch_bounds__(256) k_restrict_unpack(LevelView Cv, int iv, const int* items,
                                                          int n_items, int hnc, const double* buf) {
@@ -493,6 +510,18 @@ void launch_restrict_pack(const LevelView& F, int iv, const int* items, int n, d
   const long long work = (long long)h * h * h * n;
   if (work == 0) return;
   k_restrict_pack<<<grid_for(work), 256, 0, st>>>(F, iv, items, n, buf);
+}
+
+void launch_box_pack(const LevelView& L, int iv, const int* items, int n, double* buf, hipStream_t st) {
+  const long long work = L.stride * n;
+  if (work == 0) return;
+  k_box_pack<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, buf);
+}
+
+void launch_box_unpack(const LevelView& L, int iv, const int* items, int n, const double* buf, hipStream_t st) {
+  const long long work = L.stride * n;
+  if (work == 0) return;
+  k_box_unpack<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, buf);
 }
 
 void launch_restrict_unpack(const LevelView& C, int iv, const int* items, int n, int hnc, const double* buf,

@@ -161,10 +161,15 @@ __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, 
   }
 }
 
+// skip1: a red-black substep of colour 1 follows (the V-cycle's up-smoothing,
+// m_multigrid.f90:216-222), which overwrites colour 1 and its ghosts without
+// reading them, so boxes whose six faces all have same-GPU neighbours correct
+// and push colour 0 only.  Boxes with a physical face (bc_to_gc reads the
+// colour-1 boundary cell) or a remote face (whole faces travel) do both.
 template <int NC, int BS, bool SUB>
 __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
                                                  const int* parent_local, const int* dixp, const GcBC& bc,
-                                                 double* sendbuf, int b, double* lds) {
+                                                 double* sendbuf, int b, double* lds, bool skip1) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
   double* cb = lds;                     // the parent's octant + one face layer around it
@@ -172,19 +177,23 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
   const int tid = threadIdx.x;
   const int pb = parent_local[b], dp = dixp[b];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
+  bool only0 = skip1;
+#pragma unroll
+  for (int nb = 0; nb < 6; nb++) only0 = only0 && F.nbk[(long long)b * 6 + nb] == NB_LOCAL;
+  const int npair = only0 ? HV / 2 : HV;
   double* __restrict__ u = F.phi + (long long)b * F.stride;
   v2d old[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < HV) old[r] = ld_nt(u + 2 * q2);
+    if (q2 < npair) old[r] = ld_nt(u + 2 * q2);
   }
   load_parent_octant<NC, BS, SUB>(Cv, iv, pb, dx, dy, dz, cb);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 >= HV) continue;
+    if (q2 >= npair) continue;
     double nv[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -204,15 +213,16 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     st_nt(u + 2 * q2, nv[0], nv[1]);
   }
   __syncthreads();
-  tile_face_fill<NC>(F, b, sb, 3, bc, sendbuf);
+  tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf);
 }
 
 template <int NC, int BS, bool SUB>
 __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
                                                      const int* parent_local, const int* dixp, GcBC bc,
-                                                     double* sendbuf) {
+                                                     double* sendbuf, int skip1) {
   __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
-  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, xcd_box(blockIdx.x, gridDim.x), lds);
+  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, xcd_box(blockIdx.x, gridDim.x), lds,
+                                skip1 != 0);
 }
 
 // correct_children + fill + the first up-smoothing substep in one pass
@@ -260,13 +270,21 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   const int tid = threadIdx.x;
   const int pb = parent_local[b], dp = dixp[b];
   const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
+  // The substep overwrites colour 1 without reading it (gs_value has no
+  // centre term), so colour 1's corrected values are dead, except where a
+  // physical face's colour-0 ghost takes its boundary cell x1 (bc_to_gc).
+  // Boxes without a physical face prolong colour 0 only.
+  bool phys = false;
+#pragma unroll
+  for (int nb = 0; nb < 6; nb++) phys |= F.nbk[(long long)b * 6 + nb] == NB_PHYS;
+  const int npair = phys ? HV : HV / 2;
   // all loads that do not depend on LDS first
   double* __restrict__ u = F.phi + (long long)b * F.stride;
   v2d old[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < HV) old[r] = ld_nt(u + 2 * q2);
+    if (q2 < npair) old[r] = ld_nt(u + 2 * q2);
   }
   // ---- colour-0 ghost values from same-GPU neighbours: the neighbour's
   // old boundary value (still in our ghost slot) + its prolongation
@@ -329,11 +347,11 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   // ---- parent's res = phi - old on its octant + face layer (stored by owner)
   load_parent_octant<NC, BS, true, true>(Cv, 4, pb, dix[0], dix[1], dix[2], cb);
   __syncthreads();
-  // ---- phi += prolong(res), both colours; colour 0 is final here
+  // ---- phi += prolong(res): colour 0 (final here), colour 1 for bc_to_gc
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 >= HV) continue;
+    if (q2 >= npair) continue;
     double nv[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -598,14 +616,15 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 }
 
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
-                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, hipStream_t st) {
+                         const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
+                         hipStream_t st) {
   if (F.n == 0) return;
   const dim3 g(F.n);
 #define OMG_PF(NC, BS)                                                                                \
   if (sub)                                                                                            \
-    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf);        \
+    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1); \
   else                                                                                                \
-    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf);
+    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1);
   switch (F.nc) {
     case 16: OMG_PF(16, 512) break;
     case 8: OMG_PF(8, 256) break;
@@ -826,10 +845,10 @@ __device__ void tail_correct(const TailArgs& A, int li, double* lds) {
   const LevelView C = A.lv[li - 1].L;
   for (int b = 0; b < T.L.n; b++) {
     switch (T.L.nc) {
-      case 16: prolong_fill_box<16, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
-      case 8: prolong_fill_box<8, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
-      case 4: prolong_fill_box<4, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
-      default: prolong_fill_box<2, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds); break;
+      case 16: prolong_fill_box<16, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds, false); break;
+      case 8: prolong_fill_box<8, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds, false); break;
+      case 4: prolong_fill_box<4, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds, false); break;
+      default: prolong_fill_box<2, kTailBS, true>(C, T.L, 4, T.parent_local, T.dixp, T.bc, nullptr, b, lds, false); break;
     }
     __syncthreads();
   }

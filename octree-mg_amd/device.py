@@ -32,6 +32,8 @@ SIGNATURES = {
     "omg_set_operator": (_I, [_P, _I, _D]),
     "omg_set_smoother": (_I, [_P, _I, _I, _I, _I, _D, _D]),
     "omg_set_subtract_mean": (_I, [_P, _I]),
+    "omg_set_coarse_replication": (_I, [_P, _LL]),
+    "omg_replicated_level": (_I, [_P, C.POINTER(_I)]),
     "omg_set_bc": (_I, [_P, _I, _I, _I, _D]),
     "omg_set_bc_faces": (_I, [_P, _I, _LP, _IP, _DP, _LL]),
     "omg_level_size": (_I, [_P, _I, C.POINTER(_I), C.POINTER(_I)]),
@@ -142,6 +144,11 @@ class Context:
 
     def stream(self) -> int:
         return self.L.omg_stream(self.h) or 0
+
+    def replicated_level(self):
+        r = _I()
+        self.call("replicated_level", C.byref(r))
+        return r.value
 
     def level_size(self, lvl):
         n, nc = _I(), _I()

@@ -62,6 +62,9 @@ class MG(MGTree):
         self.ctx: device.Context | None = None
         self.device_index = 0
         self._uid = None
+        # replicate coarse levels of up to this many cells on every rank
+        # (omg_set_coarse_replication; 0 = split them like the reference)
+        self.coarse_replication_cells = 0
 
     # -- data access -------------------------------------------------------
     @property
@@ -104,9 +107,11 @@ class MG(MGTree):
                 face_off = np.full(n * 6, -1, dtype=np.int64)
                 face_type = np.zeros(n * 6, dtype=np.int32)
                 chunks, pos = [], 0
+                rep = c.replicated_level()
                 for lvl in range(self.lowest_lvl, self.highest_lvl + 1):
                     nc = self.box_size_lvl[lvl]
-                    for id_ in self.lvls[lvl].my_ids:
+                    # a replicated level needs the table of every box
+                    for id_ in (self.lvls[lvl].ids if lvl <= rep else self.lvls[lvl].my_ids):
                         for nb in range(1, 7):
                             if self.neighbors[id_, nb - 1] < MG_NO_BOX and cbs[nb - 1] is not None:
                                 t, vals = cbs[nb - 1](self, int(id_), nc, iv, nb)
@@ -247,6 +252,8 @@ def mg_allocate_storage(mg: MG, device_index=None):
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
     mg.ctx = device.Context(device_index, mg.my_rank, mg.n_cpu, uid)
+    if mg.coarse_replication_cells:
+        mg.ctx.call("set_coarse_replication", int(mg.coarse_replication_cells))
     arrs = _tree_arrays(mg)
     mg.ctx.call("tree_setup", mg.n_boxes, *arrs[:6], mg.lowest_lvl, mg.highest_lvl,
                 mg.first_normal_lvl, mg.box_size, arrs[6], arrs[7], arrs[8], arrs[9], mg.n_vars)

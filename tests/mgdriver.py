@@ -120,6 +120,9 @@ class OracleBackend:
     def my_ids(self, lvl):
         return self.tree.lvls[lvl].ids
 
+    def collective(self, lvl):
+        return False
+
     def set_level(self, lvl, iv, data):
         self.o.set_level(lvl, iv, data)
 
@@ -143,9 +146,10 @@ class OracleBackend:
 
 
 class DeviceBackend:
-    def __init__(self, cfg, comm=None):
+    def __init__(self, cfg, comm=None, rep_cells=0):
         self.cfg = cfg
         mg = omg.MG()
+        mg.coarse_replication_cells = rep_cells
         mg.n_extra_vars = n_vars(cfg) - 4
         mg.operator_type = OPS[cfg["op"]]
         mg.helmholtz_lambda = cfg["lam"]
@@ -169,6 +173,7 @@ class DeviceBackend:
             mg.ctx.call("set_bc_faces", iv, off, typ, data, len(data))
         self.mg = mg
         self.tree = mg
+        self.rep_lvl = mg.ctx.replicated_level()
 
     def levels(self):
         return range(self.mg.lowest_lvl, self.mg.highest_lvl + 1)
@@ -176,8 +181,12 @@ class DeviceBackend:
     def my_ids(self, lvl):
         return self.mg.lvls[lvl].my_ids
 
+    def collective(self, lvl):
+        # uploads to a replicated level: every rank calls (omg_set_coarse_replication)
+        return lvl <= self.rep_lvl
+
     def set_level(self, lvl, iv, data):
-        if len(self.my_ids(lvl)):
+        if len(self.my_ids(lvl)) or self.collective(lvl):
             self.mg.set_level(lvl, iv, data)
 
     def get_level(self, lvl, iv):
@@ -215,41 +224,47 @@ def setup_problem(be):
     137-170), or set_rhs (tests/test_performance.f90:102-115)."""
     cfg, tree = be.cfg, be.tree
     I_SOL = i_sol(cfg)
+
+    def empty(lvl):
+        nc = tree.box_size_lvl[lvl]
+        return np.zeros((0, nc + 2, nc + 2, nc + 2))
+
+    def put(lvl, iv, make):
+        # a rank without boxes still calls when the upload is collective
+        ids = be.my_ids(lvl)
+        if len(ids):
+            be.set_level(lvl, iv, make(ids))
+        elif be.collective(lvl):
+            be.set_level(lvl, iv, empty(lvl))
+
     if is_vop(cfg) or cfg["op"] == "ahelm":
         for lvl in be.levels():
-            ids = be.my_ids(lvl)
-            if len(ids):
-                e = P.level_eps(tree, lvl, ids)
-                if cfg["op"] == "ahelm":
-                    for d in (1, 2, 3):                 # eps_d = eps * d, vars 5..7
-                        be.set_level(lvl, I_EPS + d - 1, e * float(d))
-                else:
-                    be.set_level(lvl, I_EPS, e)
+            e = P.level_eps(tree, lvl, be.my_ids(lvl)) if len(be.my_ids(lvl)) else empty(lvl)
+            if cfg["op"] == "ahelm":
+                for d in (1, 2, 3):                 # eps_d = eps * d, vars 5..7
+                    put(lvl, I_EPS + d - 1, lambda ids: e * float(d))
+            else:
+                put(lvl, I_EPS, lambda ids: e)
     if cfg["rhs"] == "sol":
         for lvl in be.levels():
-            ids = be.my_ids(lvl)
-            if len(ids):
-                be.set_level(lvl, I_SOL, P.level_solution(tree, lvl, ids))
+            put(lvl, I_SOL, lambda ids: P.level_solution(tree, lvl, ids))
         if cfg["n_levels"] > 1:
             be.restrict(I_SOL)
             be.fill_ghost_cells(I_SOL)
         for lvl in be.levels():
-            if len(be.my_ids(lvl)):
-                be.set_level(lvl, T.MG_IPHI, be.get_level(lvl, I_SOL))
+            put(lvl, T.MG_IPHI, lambda ids: be.get_level(lvl, I_SOL))
         be.apply_op(T.MG_IRHS)
         for lvl in be.levels():
-            ids = be.my_ids(lvl)
-            if len(ids):
-                nc = tree.box_size_lvl[lvl]
-                be.set_level(lvl, T.MG_IPHI, np.zeros((len(ids), nc + 2, nc + 2, nc + 2)))
+            nc = tree.box_size_lvl[lvl]
+            put(lvl, T.MG_IPHI, lambda ids: np.zeros((len(ids), nc + 2, nc + 2, nc + 2)))
     else:
+        def ones(ids):
+            a = np.zeros((len(ids), nc + 2, nc + 2, nc + 2))
+            a[:, 1:nc + 1, 1:nc + 1, 1:nc + 1] = 1.0
+            return a
         for lvl in be.levels():
-            ids = be.my_ids(lvl)
-            if len(ids):
-                nc = tree.box_size_lvl[lvl]
-                a = np.zeros((len(ids), nc + 2, nc + 2, nc + 2))
-                a[:, 1:nc + 1, 1:nc + 1, 1:nc + 1] = 1.0
-                be.set_level(lvl, T.MG_IRHS, a)
+            nc = tree.box_size_lvl[lvl]
+            put(lvl, T.MG_IRHS, ones)
 
 
 def measure(be):
@@ -322,7 +337,7 @@ def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None)
     return out
 
 
-def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600):
+def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0):
     """The same configuration on n_ranks device contexts of this process (one
     thread per rank, all on GPU 0), exchanging through the loopback transport
     (omg_loopback_unique_id): the multi-rank path of libomg.so (plans, packing,
@@ -347,7 +362,7 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600):
             bar.wait()
             return E, R
         try:
-            be = DeviceBackend(cfg, omg.Loopback(tag, rank, n_ranks))
+            be = DeviceBackend(cfg, omg.Loopback(tag, rank, n_ranks), rep_cells)
             setup_problem(be)
             out[rank] = _cycles(be, cfg, reduce)
             be.mg.ctx.call("synchronize")

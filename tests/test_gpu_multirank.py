@@ -22,3 +22,15 @@ def test_multirank_matches_reference_golden(name, ranks):
     e = GOLDEN[name]
     out = run_problem_loopback(e["args"], ranks)
     assert out["history"] == e["runs"][str(ranks)]["history"]
+
+
+# Replicated coarse levels (omg_set_coarse_replication): every coarse level
+# on every rank (1 << 40 cells), or only the smallest ones (4096 cells, so the
+# restriction into a replicated level from a distributed one is exercised at
+# several box sizes).  Same bits as the reference's distributed coarse levels.
+@pytest.mark.parametrize("rep", [1 << 40, 4096])
+@pytest.mark.parametrize("name,ranks", MULTI)
+def test_multirank_replicated_coarse_matches_golden(name, ranks, rep):
+    e = GOLDEN[name]
+    out = run_problem_loopback(e["args"], ranks, rep_cells=rep)
+    assert out["history"] == e["runs"][str(ranks)]["history"]

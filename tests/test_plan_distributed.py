@@ -23,13 +23,18 @@ import torch.multiprocessing as mp
 from tests.mgdriver import T, build_tree, omg, parse
 
 CASES = [
-    ("8 32 32 32 1 v gsrb lpl 0 per sol 1 lb 0", 2),     # periodic halo
-    ("8 64 32 32 1 v gs lpl 0 d0 sol 1 lbp 0", 2),       # non-cube, parents balanced
-    ("8 32 32 32 1 v gs lpl 0 sol sol 3 lb 0", 2),       # 3-level refined tree
-    ("8 32 32 32 1 v gs lpl 0 sol sol 2 lb 0", 3),       # refinement boundaries across ranks
-    ("8 32 32 32 1 v gsrb lpl 0 d0 sol 3 lb 0", 3),
+    ("8 32 32 32 1 v gsrb lpl 0 per sol 1 lb 0", 2, 0),     # periodic halo
+    ("8 64 32 32 1 v gs lpl 0 d0 sol 1 lbp 0", 2, 0),       # non-cube, parents balanced
+    ("8 32 32 32 1 v gs lpl 0 sol sol 3 lb 0", 2, 0),       # 3-level refined tree
+    ("8 32 32 32 1 v gs lpl 0 sol sol 2 lb 0", 3, 0),       # refinement boundaries across ranks
+    ("8 32 32 32 1 v gsrb lpl 0 d0 sol 3 lb 0", 3, 0),
+    # replicated coarse levels (omg_set_coarse_replication): all coarse
+    # levels, or only those of at most 4096 cells
+    ("8 64 64 64 1 v gsrb lpl 0 per sol 1 lb 0", 3, 1 << 40),
+    ("8 64 64 64 1 v gsrb lpl 0 per sol 1 lb 0", 2, 4096),
+    ("8 32 32 32 1 v gs lpl 0 sol sol 2 lb 0", 3, 1 << 40),  # + refinement boundaries
 ]
-WHICH = {0: "halo", 1: "restrict", 2: "prolong", 3: "refinement-boundary"}
+WHICH = {0: "halo", 1: "restrict", 2: "prolong", 3: "refinement-boundary", 4: "replica"}
 
 
 def _free_port():
@@ -40,10 +45,12 @@ def _free_port():
     return p
 
 
-def _plans(args, rank, world):
+def _plans(args, rank, world, rep):
     cfg = parse(args)
     tree = build_tree(cfg, T.MGTree(), world, rank)
     ctx = omg.device.Context(-2, rank, world)   # OMG_DEVICE_NONE
+    if rep:
+        ctx.call("set_coarse_replication", rep)
     arrs = omg.mg._tree_arrays(tree)
     ctx.call("tree_setup", tree.n_boxes, *arrs[:6], tree.lowest_lvl, tree.highest_lvl,
              tree.first_normal_lvl, tree.box_size, arrs[6], arrs[7], arrs[8], arrs[9], 5)
@@ -52,37 +59,40 @@ def _plans(args, rank, world):
         for w in WHICH:
             for d in (0, 1):
                 out[(lvl, w, d)] = ctx.plan_transfer(lvl, w, d)
+    rep_lvl = ctx.replicated_level()
     ctx.close()
-    return out
+    return out, rep_lvl
 
 
-def _expected_remote(args, rank, world):
-    """Faces of my boxes that need data from another rank, from the tree alone."""
+def _expected_remote(args, rank, world, rep_lvl):
+    """Faces of my boxes that need data from another rank, from the tree
+    alone (a box of a replicated level is on every rank)."""
     cfg = parse(args)
     t = build_tree(cfg, T.MGTree(), world, rank)
+    mine = lambda i: t.lvl[i] <= rep_lvl or t.rank[i] == rank  # noqa: E731
     halo, rb = {}, {}
     for lvl in range(t.lowest_lvl, t.highest_lvl + 1):
         h, r = set(), set()
         for id_ in t.lvls[lvl].ids:
-            if t.rank[id_] != rank:
+            if not mine(id_):
                 continue
             for nb in range(1, 7):
                 nid = t.neighbors[id_][nb - 1]
-                if nid > 0 and t.rank[nid] != rank:
+                if nid > 0 and not mine(nid):
                     h.add(6 * int(id_) + nb)
                 elif nid == 0:
                     pn = t.neighbors[t.parent[id_]][nb - 1]
-                    if t.rank[pn] != rank:
+                    if not mine(pn):
                         r.add(6 * int(id_) + nb)
         halo[lvl], rb[lvl] = h, r
     return halo, rb
 
 
-def _worker(rank, world, port, args, q):
+def _worker(rank, world, port, args, rep, q):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
-        mine = _plans(args, rank, world)
+        mine, rep_lvl = _plans(args, rank, world, rep)
         allp = [None] * world
         dist.all_gather_object(allp, mine)
         problems = []
@@ -102,7 +112,21 @@ def _worker(rank, world, port, args, q):
                                     f"{b} expects {len(expected)}")
                 if sent and per != per_b:
                     problems.append(f"lvl {lvl} {WHICH[w]}: item size {per} vs {per_b}")
-        halo, rb = _expected_remote(args, rank, world)
+        halo, rb = _expected_remote(args, rank, world, rep_lvl)
+        if rep:
+            lo = min(lv for lv, _, _ in mine)
+            if rep_lvl < lo:
+                problems.append("replication requested but no level replicated")
+            # a replicated level has no halo, and no prolongation out of it
+            for (lvl, w, d), (items, _) in mine.items():
+                if items and ((lvl <= rep_lvl and w in (0, 3)) or (lvl <= rep_lvl + 1 and w == 2)):
+                    problems.append(f"lvl {lvl} {WHICH[w]}: {len(items)} items on a replicated level")
+            # every rank restricts into every copy of the highest replicated level
+            up = rep_lvl + 1
+            if world > 1 and (up, 1, 0) in mine:
+                peers = {p for p, _ in mine[(up, 1, 0)][0]}
+                if peers != set(range(world)) - {rank}:
+                    problems.append(f"lvl {up} restrict goes to {sorted(peers)}, not to every peer")
         for lvl in halo:
             got_h = [k for _, k in mine[(lvl, 0, 1)][0]]
             got_r = [k for _, k in mine[(lvl, 3, 1)][0]]
@@ -118,12 +142,12 @@ def _worker(rank, world, port, args, q):
         q.put((rank, [f"{type(e).__name__}: {e}"], 0))
 
 
-@pytest.mark.parametrize("args,world", CASES)
-def test_plans_pair_up_across_ranks(args, world):
+@pytest.mark.parametrize("args,world,rep", CASES)
+def test_plans_pair_up_across_ranks(args, world, rep):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, rep, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -131,5 +155,5 @@ def test_plans_pair_up_across_ranks(args, world):
         p.join(60)
     problems = [f"rank {r}: {m}" for r, ms, _ in res for m in ms]
     assert not problems, "\n".join(problems)
-    if world == 3 and " 2 lb" in args:
+    if world == 3 and " 2 lb" in args and not rep:
         assert sum(n for _, _, n in res) > 0, "case meant to cross refinement boundaries has none"

@@ -6,7 +6,7 @@ orchestration the driver's multi-GPU run exercises (plans, comm stream,
 collective decisions, reductions) at bench scale; timings share one GPU and
 say nothing about scaling.
 
-usage: loopback_bench.py N [per_rank_n] [cycles]"""
+usage: loopback_bench.py N [per_rank_n] [cycles] [replicate_cells]"""
 import os
 import sys
 import threading
@@ -27,6 +27,7 @@ def main():
     n = int(sys.argv[1])
     per = int(sys.argv[2]) if len(sys.argv) > 2 else 128
     cycles = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    rep = int(sys.argv[4]) if len(sys.argv) > 4 else bench.REPLICATE_CELLS
     tag = int.from_bytes(os.urandom(6), "little")
     bar = threading.Barrier(n)
     res = [None] * n
@@ -43,16 +44,15 @@ def main():
             omg.mg_build_rectangle(mg, domain, 16, 1.0 / domain.astype(np.float64), [0.0] * 3, [True] * 3, 0)
             omg.mg_load_balance(mg)
             omg.mg_set_methods(mg)
+            mg.coarse_replication_cells = rep
             omg.mg_allocate_storage(mg)
             for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
                 ids = mg.lvls[lvl].my_ids
-                if len(ids):
-                    mg.set_level(lvl, T.MG_IPHI, omg.problems.level_solution(mg, lvl, ids))
+                mg.set_level(lvl, T.MG_IPHI, omg.problems.level_solution(mg, lvl, ids))
             omg.mg_apply_op(mg, T.MG_IRHS)
             for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
                 k, nc = mg.ctx.level_size(lvl)
-                if k:
-                    mg.set_level(lvl, T.MG_IPHI, np.zeros((k, nc + 2, nc + 2, nc + 2)))
+                mg.set_level(lvl, T.MG_IPHI, np.zeros((k, nc + 2, nc + 2, nc + 2)))
             r = omg.mg_fas_vcycle(mg, max_res=True)
             mg.ctx.call("synchronize")
             bar.wait()
@@ -75,7 +75,8 @@ def main():
     if errs:
         raise RuntimeError(errs)
     dt = max(x[0] for x in res)
-    print(f"loopback ranks={n} per_rank={per}^3 grid={bench.rank_grid(n)}: {dt / cycles * 1e3:.2f} ms/cycle "
+    print(f"loopback ranks={n} per_rank={per}^3 grid={bench.rank_grid(n)} replicate<={rep} cells: "
+          f"{dt / cycles * 1e3:.2f} ms/cycle "
           f"(all ranks on one GPU), max_res={res[0][1]:.6e}, same on all ranks: "
           f"{len(set(x[1] for x in res)) == 1}")
 
