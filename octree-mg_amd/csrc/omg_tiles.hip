@@ -278,13 +278,15 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
 #pragma unroll
   for (int nb = 0; nb < 6; nb++) phys |= F.nbk[(long long)b * 6 + nb] == NB_PHYS;
   const int npair = phys ? HV : HV / 2;
-  // all loads that do not depend on LDS first
+  // all loads that do not depend on LDS first (colour 0; a physical-face box
+  // reads its colour 1 when it corrects it)
+  constexpr int NR0 = (HV / 2 + BS - 1) / BS;
   double* __restrict__ u = F.phi + (long long)b * F.stride;
-  v2d old[NR];
+  v2d old[NR0];
 #pragma unroll
-  for (int r = 0; r < NR; r++) {
+  for (int r = 0; r < NR0; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < npair) old[r] = ld_nt(u + 2 * q2);
+    if (q2 < HV / 2) old[r] = ld_nt(u + 2 * q2);
   }
   // ---- colour-0 ghost values from same-GPU neighbours: the neighbour's
   // old boundary value (still in our ghost slot) + its prolongation
@@ -352,6 +354,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
     if (q2 >= npair) continue;
+    const v2d ov = q2 < HV / 2 ? old[r < NR0 ? r : 0] : ld_nt(u + 2 * q2);
     double nv[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -364,7 +367,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       const double fx = 0.25 * cb[(i & 1) ? c0 - 1 : c0 + 1];
       const double fy = 0.25 * cb[(j & 1) ? c0 - CB : c0 + CB];
       const double fz = 0.25 * cb[(k & 1) ? c0 - CB * CB : c0 + CB * CB];
-      const double o = s ? old[r].y : old[r].x;
+      const double o = s ? ov.y : ov.x;
       nv[s] = o + (f0 + fx + fy + fz);
       sb[q] = nv[s];
     }
@@ -427,7 +430,11 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
 }
 
 template <int NC, int OP, int BS>
-__global__ void __launch_bounds__(BS) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
+#ifndef OMG_PS_WAVES
+#define OMG_PS_WAVES 8
+#endif
+// 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64
+__global__ void __launch_bounds__(BS, OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
                                                        int one_child) {
   __shared__ double lds[prolong_smooth_lds<NC>()];
