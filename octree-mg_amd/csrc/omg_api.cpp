@@ -380,15 +380,21 @@ void phi_dirty_all(omg_ctx* c) {
 
 // halo exchange of the faces packed by the last fill/substep kernel, then
 // fill_buffered_nb (m_ghost_cells.f90:163-174, 424-454)
+void finish_rb(omg_ctx* c, Level* L, int iv);
 void finish_halo(omg_ctx* c, Level* L, int iv) {
   if (c->n_ranks == 1) return;
   if (L->halo.n_send || L->halo.n_recv) {
     exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
     launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
   }
-  // refinement boundaries across ranks (buffer_refinement_boundaries,
-  // m_ghost_cells.f90:157-162, 200-229): coarse faces go out interpolated,
-  // the fine side applies sides_rb once they arrive
+  finish_rb(c, L, iv);
+}
+
+// refinement boundaries across ranks (buffer_refinement_boundaries,
+// m_ghost_cells.f90:157-162, 200-229): coarse faces go out interpolated,
+// the fine side applies sides_rb once they arrive
+void finish_rb(omg_ctx* c, Level* L, int iv) {
+  if (c->n_ranks == 1) return;
   if (L->rbx.n_send || L->rbx.n_recv) {
     launch_rb_pack(view_of(c, L->lvl - 1), iv, L->rbx.d_send_items, L->rbx.n_send, L->nc, L->d_rbsend,
                    c->stream);
@@ -426,8 +432,9 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1) {
   if (!L) return;
   // a pending phi shift is subtracted by the first tiled substep while it
   // loads (the values it reads are dead afterwards); otherwise applied now
+  // (not next to refinement boundaries: their ghosts read the coarse level)
   const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 2 && L->phi_gc_ok &&
-                      gs_tiled(L->nc, c->op, L->has_rb);
+                      !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
     for (int n = 1; n <= n_sub; n++) {
@@ -471,6 +478,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1) {
                           bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int);
       }
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+      finish_rb(c, L, 1);
       if (!L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
       continue;
     }
@@ -606,6 +614,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
   if (c->no_fuse_up || !F || !C || !F->prolong_smooth_ok || c->smoother != OMG_SMOOTHER_GSRB ||
+      (c->op != OP_LPL && c->op != OP_HELM) ||
       c->n_cycle_up < 1 || F->has_rb || F->has_remote || !gs_tiled(F->nc, c->op, F->has_rb) ||
       !((size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc) ||
       (c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv)))

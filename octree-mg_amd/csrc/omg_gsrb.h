@@ -41,10 +41,54 @@ __device__ __forceinline__ void gsrb_load_rhs(const LevelView& L, int e, int b, 
   }
 }
 
-template <int NC, int OP, int BS, int NT, bool PRE = false>
+// The coarse side of refinement-boundary faces (fine side of sides_rb):
+// the level below and the per-face records; rb == nullptr: none on this level.
+struct RbSide {
+  LevelView C;
+  const RBRec* rb;
+};
+
+// Refinement-boundary ghost (box_gc_for_fine_neighbor + sides_rb,
+// m_ghost_cells.f90:287-328, 500-577, 769-861) of face nb at (a, c) from the
+// two boundary cells v1 (layer x1) and v2 (layer x2) of the fine box.
+__device__ __forceinline__ double rb_ghost(const LevelView& L, const RbSide& R, int arg, int nb, int a, int c,
+                                           double v1, double v2) {
+  const RBRec rec = R.rb[arg];
+  const double* cu = R.C.phi + (long long)rec.coarse_idx * R.C.stride;
+  const int d = (nb + 1) >> 1;
+  const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;
+  const int clayer = (nb & 1) ? L.nc : 1;
+  const int i = (a + 1) >> 1, j = (c + 1) >> 1;
+  auto T = [&](int p, int q) { return cu[off_face_cell(R.C, nb, clayer, rec.dix[t1] + p, rec.dix[t2] + q)]; };
+  const double tc = T(i, j);
+  const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
+  const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
+  double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
+  gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
+  return 0.5 * gv + 0.75 * v1 - 0.25 * v2;
+}
+
+// Variable-coefficient operators read eps (var 5; vars 5..7 for the
+// anisotropic one) at the cell and at its six neighbours from HBM / L2, at
+// the same slots the stencil reads phi from LDS (same layout, same colour).
+template <int OP>
+struct EpsPtr {
+  const double* v[3];
+  __device__ __forceinline__ EpsPtr(const LevelView& L, int b) {
+    const long long bo = (long long)b * L.stride;
+    v[0] = L.data + 4 * L.vstride + bo;
+    v[1] = OP == OP_AHELM ? L.data + 5 * L.vstride + bo : v[0];
+    v[2] = OP == OP_AHELM ? L.data + 6 * L.vstride + bo : v[0];
+  }
+};
+
+// RB: the level has refinement-boundary faces (a separate instantiation keeps
+// their interpolation out of the plain kernels)
+template <int NC, int OP, int BS, int NT, bool PRE = false, bool RB = false>
 __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int e, int colours, const GcBC& bc,
                                          double* __restrict__ sendbuf, const double* __restrict__ shift, int b,
-                                         double* lds, const GsrbRhs<NC, BS>* pre_rhs = nullptr) {
+                                         double* lds, const GsrbRhs<NC, BS>* pre_rhs = nullptr,
+                                         const RbSide* rbs = nullptr) {
   constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
   constexpr int NP2 = GsrbRhs<NC, BS>::NP2;
   double* so = lds;                            // colour 1-e of the interior
@@ -101,19 +145,27 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     if constexpr (H % 2 == 0) {
       const int q = 2 * q2, ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
       const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
-      const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
+      // neighbour slots: interior colour 1-e (so-relative) or ghost face half
+      // (sg-relative, face nb-1 of the colour 1-e halves); lds offset = slot of
+      // so / sg, global offset = the same slot in the box's stored layout
       const int xgi = ((j - 1) >> 1) + H * (k - 1);   // x ghosts of this row
-      const double* xs_ptr = p ? (ih + 2 == H ? sg + FH + xgi : so + ih + 2 + H * row)
-                               : (ih == 0 ? sg + xgi : so + ih - 1 + H * row);
-      const double xs = *xs_ptr;
-      const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
-                                                               : sg + 2 * FH + ih + H * (k - 1));
-      const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
-                                                                : sg + 3 * FH + ih + H * (k - 1));
-      const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
-                                                               : sg + 4 * FH + ih + H * (j - 1));
-      const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
-                                                                : sg + 5 * FH + ih + H * (j - 1));
+      const bool xs_g = p ? ih + 2 == H : ih == 0;
+      const int xs_s = p ? (xs_g ? FH + xgi : ih + 2 + H * row) : (xs_g ? xgi : ih - 1 + H * row);
+      const bool ym_g = j == 1, yp_g = j == NC, zm_g = k == 1, zp_g = k == NC;
+      const int ym_s = ym_g ? 2 * FH + ih + H * (k - 1) : ih + H * (row - 1);
+      const int yp_s = yp_g ? 3 * FH + ih + H * (k - 1) : ih + H * (row + 1);
+      const int zm_s = zm_g ? 4 * FH + ih + H * (j - 1) : ih + H * (row - NC);
+      const int zp_s = zp_g ? 5 * FH + ih + H * (j - 1) : ih + H * (row + NC);
+      const int xc_s = ih + H * row;
+      auto lp = [&](bool g, int sl) { return (g ? sg : so) + sl; };
+      // stored-layout offset of a slot: interior colour o, or ghost face half
+      auto go = [&](bool g, int sl) { return g ? 2 * HV + (sl / FH) * FS + o * FH + sl % FH : o * HV + sl; };
+      const double2 xc = *reinterpret_cast<const double2*>(so + xc_s);
+      const double xs = *lp(xs_g, xs_s);
+      const double2 ym = *reinterpret_cast<const double2*>(lp(ym_g, ym_s));
+      const double2 yp = *reinterpret_cast<const double2*>(lp(yp_g, yp_s));
+      const double2 zm = *reinterpret_cast<const double2*>(lp(zm_g, zm_s));
+      const double2 zp = *reinterpret_cast<const double2*>(lp(zp_g, zp_s));
       Nbr7 s0, s1;
       s0.xm = p ? xc.x : xs;
       s0.xp = p ? xc.y : xc.x;
@@ -123,7 +175,31 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       s0.yp = yp.x; s1.yp = yp.y;
       s0.zm = zm.x; s1.zm = zm.y;
       s0.zp = zp.x; s1.zp = zp.y;
-      nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));
+      if constexpr (is_varop(OP)) {
+        const EpsPtr<OP> EP(L, b);
+        auto ld2 = [&](const double* v, bool g, int sl) { return *reinterpret_cast<const double2*>(v + go(g, sl)); };
+        AEps E0, E1;
+        const double2 c0 = *reinterpret_cast<const double2*>(EP.v[0] + e * HV + q);
+        const double2 c1 = *reinterpret_cast<const double2*>(EP.v[1] + e * HV + q);
+        const double2 c2 = *reinterpret_cast<const double2*>(EP.v[2] + e * HV + q);
+        E0.a0[0] = c0.x; E0.a0[1] = c1.x; E0.a0[2] = c2.x;
+        E1.a0[0] = c0.y; E1.a0[1] = c1.y; E1.a0[2] = c2.y;
+        const double2 exc = ld2(EP.v[0], false, xc_s);
+        const double exs = EP.v[0][go(xs_g, xs_s)];
+        E0.a[0] = p ? exc.x : exs;
+        E0.a[1] = p ? exc.y : exc.x;
+        E1.a[0] = p ? exc.y : exc.x;
+        E1.a[1] = p ? exs : exc.y;
+        const double2 eym = ld2(EP.v[1], ym_g, ym_s), eyp = ld2(EP.v[1], yp_g, yp_s);
+        const double2 ezm = ld2(EP.v[2], zm_g, zm_s), ezp = ld2(EP.v[2], zp_g, zp_s);
+        E0.a[2] = eym.x; E1.a[2] = eym.y;
+        E0.a[3] = eyp.x; E1.a[3] = eyp.y;
+        E0.a[4] = ezm.x; E1.a[4] = ezm.y;
+        E0.a[5] = ezp.x; E1.a[5] = ezp.y;
+        nv = make_double2(ags_value<OP>(K, s0, E0, fr[r].x), ags_value<OP>(K, s1, E1, fr[r].y));
+      } else {
+        nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));
+      }
     } else {   // NC == 2: one cell per row
       double v[2];
 #pragma unroll
@@ -139,7 +215,10 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
         st.yp = j < NC ? so[tj + H * (row + 1)] : sg[3 * FH + tj + H * (k - 1)];
         st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
         st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
-        v[s] = gs_value<OP>(K, st, s ? fr[r].y : fr[r].x);
+        if constexpr (is_varop(OP))
+          v[s] = ags_value<OP>(K, st, load_eps<OP>(L, b, i, j, k), s ? fr[r].y : fr[r].x);
+        else
+          v[s] = gs_value<OP>(K, st, s ? fr[r].y : fr[r].x);
       }
       nv = make_double2(v[0], v[1]);
     }
@@ -176,11 +255,14 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     const double v1 = cellv(i1, j1, k1);
     if (kind == NB_REMOTE) {
       sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
-    } else {  // NB_PHYS (refinement boundaries take the generic kernel)
+    } else if (kind == NB_PHYS) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const int gi = off_gh(L, nb, a, c);
       u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, cellv(i2, j2, k2));
-    }
+    } else if (RB && kind == NB_RB) {
+      const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
+      u[off_gh(L, nb, a, c)] = rb_ghost(L, *rbs, arg, nb, a, c, v1, cellv(i2, j2, k2));
+    }   // NB_RBREM: the caller's refinement-boundary exchange (finish_rb)
   }
 }
 

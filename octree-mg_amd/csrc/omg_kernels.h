@@ -24,8 +24,11 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
                        hipStream_t st, const int* boxes = nullptr, int n_boxes = 0);
 // whether launch_gs_substep takes the LDS-tiled kernel (which alone takes a shift)
+// (every operator; refinement-boundary faces are filled in its epilogue)
 inline bool gs_tiled(int nc, int op, bool has_rb) {
-  return !has_rb && (op == OP_LPL || op == OP_HELM) && (nc == 16 || nc == 8 || nc == 4 || nc == 2);
+  (void)op;
+  (void)has_rb;
+  return nc == 16 || nc == 8 || nc == 4 || nc == 2;
 }
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);

@@ -25,13 +25,14 @@
 namespace omg {
 
 
-template <int NC, int OP, int BS, int NT>
+template <int NC, int OP, int BS, int NT, bool RB>
 __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, int e, int colours, GcBC bc,
                                                   double* __restrict__ sendbuf, const double* __restrict__ shift,
-                                                  const int* __restrict__ boxes) {
+                                                  const int* __restrict__ boxes, RbSide rbs) {
   __shared__ double lds[gsrb_lds<NC>()];
   const int q = xcd_box(blockIdx.x, gridDim.x);
-  gsrb_box<NC, OP, BS, NT>(L, lambda, e, colours, bc, sendbuf, shift, boxes ? boxes[q] : q, lds);
+  gsrb_box<NC, OP, BS, NT, false, RB>(L, lambda, e, colours, bc, sendbuf, shift, boxes ? boxes[q] : q, lds,
+                                      nullptr, &rbs);
 }
 
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
@@ -51,11 +52,29 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   // level, far beyond L2 / MALL at the sizes that matter.
   const dim3 g(boxes ? n_boxes : L.n);
   if (g.x == 0) return;
-#define OMG_TILE(NC, BS)                                                                   \
-  if (op == OP_HELM)                                                                       \
-    k_gsrb_tile<NC, OP_HELM, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes); \
-  else                                                                                     \
-    k_gsrb_tile<NC, OP_LPL, BS, 2><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes);
+  const RbSide rbs{C, has_rb ? rb : nullptr};
+#define OMG_TILE_RB(NC, BS, RB)                                                                    \
+  switch (op) {                                                                                      \
+    case OP_HELM:                                                                                    \
+      k_gsrb_tile<NC, OP_HELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      break;                                                                                         \
+    case OP_VLPL:                                                                                    \
+      k_gsrb_tile<NC, OP_VLPL, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      break;                                                                                         \
+    case OP_VHELM:                                                                                   \
+      k_gsrb_tile<NC, OP_VHELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      break;                                                                                         \
+    case OP_AHELM:                                                                                   \
+      k_gsrb_tile<NC, OP_AHELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      break;                                                                                         \
+    default:                                                                                         \
+      k_gsrb_tile<NC, OP_LPL, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+  }
+#define OMG_TILE(NC, BS)          \
+  if (has_rb)                     \
+    OMG_TILE_RB(NC, BS, true)     \
+  else                            \
+    OMG_TILE_RB(NC, BS, false)
   switch (L.nc) {
     case 16: OMG_TILE(16, 512) break;
     case 8: OMG_TILE(8, 256) break;
@@ -63,6 +82,7 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
     default: OMG_TILE(2, 256) break;
   }
 #undef OMG_TILE
+#undef OMG_TILE_RB
 }
 
 }  // namespace omg
