@@ -493,7 +493,8 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1) {
 }
 
 bool tiled_level(omg_ctx* c, const Level* L) {
-  return L && tiled_nc(L->nc) && (c->op == OP_LPL || c->op == OP_HELM);
+  (void)c;
+  return L && tiled_nc(L->nc);
 }
 
 void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {

@@ -82,6 +82,60 @@ struct EpsPtr {
   }
 };
 
+// eps of the cell pair (colour e, colour-relative slot q of the first cell)
+// and of its neighbours, as load_eps gives them cell by cell; the neighbour
+// slots are pair_stencil's, in the eps variables (unused loads fold away)
+template <int NC, int OP>
+__device__ __forceinline__ void pair_eps(const LevelView& L, int b, int e, int q, AEps& E0, AEps& E1) {
+  constexpr int H = NC / 2, HV = H * NC * NC, FH = H * NC, FS = 2 * FH;
+  const EpsPtr<OP> EP(L, b);
+  const int o = 1 - e;
+  Nbr7 n0[3], n1[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (d > 0 && OP != OP_AHELM) {
+      n0[d] = n0[0];
+      n1[d] = n1[0];
+      continue;
+    }
+    pair_stencil<NC>(EP.v[d] + o * HV, EP.v[d] + 2 * HV + o * FH, FS, e, q, n0[d], n1[d]);
+    const double2 cv = *reinterpret_cast<const double2*>(EP.v[d] + e * HV + q);
+    E0.a0[d] = cv.x;
+    E1.a0[d] = cv.y;
+  }
+  E0.a[0] = n0[0].xm; E0.a[1] = n0[0].xp; E0.a[2] = n0[1].ym; E0.a[3] = n0[1].yp; E0.a[4] = n0[2].zm; E0.a[5] = n0[2].zp;
+  E1.a[0] = n1[0].xm; E1.a[1] = n1[0].xp; E1.a[2] = n1[1].ym; E1.a[3] = n1[1].yp; E1.a[4] = n1[2].zm; E1.a[5] = n1[2].zp;
+  if (OP != OP_AHELM) {
+    E0.a0[1] = E0.a0[2] = E0.a0[0];
+    E1.a0[1] = E1.a0[2] = E1.a0[0];
+  }
+}
+
+// box operator of a same-colour cell pair (box_lpl / box_helmh / box_vlpl /
+// box_vhelmh / box_ahelmh): s0, s1 hold phi; the eps pair is read for the
+// variable-coefficient operators.  NC == 2 has one cell per row: cell by cell.
+template <int NC, int OP>
+__device__ __forceinline__ void op_pair(const OpCoef<OP>& K, const LevelView& L, int b, int e, int q,
+                                        const Nbr7& s0, const Nbr7& s1, double& v0, double& v1) {
+  if constexpr (is_varop(OP)) {
+    AEps E0, E1;
+    if constexpr ((NC / 2) % 2 == 0) {
+      pair_eps<NC, OP>(L, b, e, q, E0, E1);
+    } else {
+      int i, j, k;
+      Tl<NC>::decode(e * Tl<NC>::HV + q, i, j, k);
+      E0 = load_eps<OP>(L, b, i, j, k);
+      Tl<NC>::decode(e * Tl<NC>::HV + q + 1, i, j, k);
+      E1 = load_eps<OP>(L, b, i, j, k);
+    }
+    v0 = aop_value<OP>(K, s0, E0);
+    v1 = aop_value<OP>(K, s1, E1);
+  } else {
+    v0 = op_value<OP>(K, s0);
+    v1 = op_value<OP>(K, s1);
+  }
+}
+
 // RB: the level has refinement-boundary faces (a separate instantiation keeps
 // their interpolation out of the plain kernels)
 template <int NC, int OP, int BS, int NT, bool PRE = false, bool RB = false>
@@ -145,27 +199,19 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     if constexpr (H % 2 == 0) {
       const int q = 2 * q2, ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
       const int p = (1 + j + k + e) & 1;   // i = 2*ih + 1 + p for the first cell
-      // neighbour slots: interior colour 1-e (so-relative) or ghost face half
-      // (sg-relative, face nb-1 of the colour 1-e halves); lds offset = slot of
-      // so / sg, global offset = the same slot in the box's stored layout
+      const double2 xc = *reinterpret_cast<const double2*>(so + ih + H * row);
       const int xgi = ((j - 1) >> 1) + H * (k - 1);   // x ghosts of this row
-      const bool xs_g = p ? ih + 2 == H : ih == 0;
-      const int xs_s = p ? (xs_g ? FH + xgi : ih + 2 + H * row) : (xs_g ? xgi : ih - 1 + H * row);
-      const bool ym_g = j == 1, yp_g = j == NC, zm_g = k == 1, zp_g = k == NC;
-      const int ym_s = ym_g ? 2 * FH + ih + H * (k - 1) : ih + H * (row - 1);
-      const int yp_s = yp_g ? 3 * FH + ih + H * (k - 1) : ih + H * (row + 1);
-      const int zm_s = zm_g ? 4 * FH + ih + H * (j - 1) : ih + H * (row - NC);
-      const int zp_s = zp_g ? 5 * FH + ih + H * (j - 1) : ih + H * (row + NC);
-      const int xc_s = ih + H * row;
-      auto lp = [&](bool g, int sl) { return (g ? sg : so) + sl; };
-      // stored-layout offset of a slot: interior colour o, or ghost face half
-      auto go = [&](bool g, int sl) { return g ? 2 * HV + (sl / FH) * FS + o * FH + sl % FH : o * HV + sl; };
-      const double2 xc = *reinterpret_cast<const double2*>(so + xc_s);
-      const double xs = *lp(xs_g, xs_s);
-      const double2 ym = *reinterpret_cast<const double2*>(lp(ym_g, ym_s));
-      const double2 yp = *reinterpret_cast<const double2*>(lp(yp_g, yp_s));
-      const double2 zm = *reinterpret_cast<const double2*>(lp(zm_g, zm_s));
-      const double2 zp = *reinterpret_cast<const double2*>(lp(zp_g, zp_s));
+      const double* xs_ptr = p ? (ih + 2 == H ? sg + FH + xgi : so + ih + 2 + H * row)
+                               : (ih == 0 ? sg + xgi : so + ih - 1 + H * row);
+      const double xs = *xs_ptr;
+      const double2 ym = *reinterpret_cast<const double2*>(j > 1 ? so + ih + H * (row - 1)
+                                                               : sg + 2 * FH + ih + H * (k - 1));
+      const double2 yp = *reinterpret_cast<const double2*>(j < NC ? so + ih + H * (row + 1)
+                                                                : sg + 3 * FH + ih + H * (k - 1));
+      const double2 zm = *reinterpret_cast<const double2*>(k > 1 ? so + ih + H * (row - NC)
+                                                               : sg + 4 * FH + ih + H * (j - 1));
+      const double2 zp = *reinterpret_cast<const double2*>(k < NC ? so + ih + H * (row + NC)
+                                                                : sg + 5 * FH + ih + H * (j - 1));
       Nbr7 s0, s1;
       s0.xm = p ? xc.x : xs;
       s0.xp = p ? xc.y : xc.x;
@@ -176,26 +222,8 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       s0.zm = zm.x; s1.zm = zm.y;
       s0.zp = zp.x; s1.zp = zp.y;
       if constexpr (is_varop(OP)) {
-        const EpsPtr<OP> EP(L, b);
-        auto ld2 = [&](const double* v, bool g, int sl) { return *reinterpret_cast<const double2*>(v + go(g, sl)); };
         AEps E0, E1;
-        const double2 c0 = *reinterpret_cast<const double2*>(EP.v[0] + e * HV + q);
-        const double2 c1 = *reinterpret_cast<const double2*>(EP.v[1] + e * HV + q);
-        const double2 c2 = *reinterpret_cast<const double2*>(EP.v[2] + e * HV + q);
-        E0.a0[0] = c0.x; E0.a0[1] = c1.x; E0.a0[2] = c2.x;
-        E1.a0[0] = c0.y; E1.a0[1] = c1.y; E1.a0[2] = c2.y;
-        const double2 exc = ld2(EP.v[0], false, xc_s);
-        const double exs = EP.v[0][go(xs_g, xs_s)];
-        E0.a[0] = p ? exc.x : exs;
-        E0.a[1] = p ? exc.y : exc.x;
-        E1.a[0] = p ? exc.y : exc.x;
-        E1.a[1] = p ? exs : exc.y;
-        const double2 eym = ld2(EP.v[1], ym_g, ym_s), eyp = ld2(EP.v[1], yp_g, yp_s);
-        const double2 ezm = ld2(EP.v[2], zm_g, zm_s), ezp = ld2(EP.v[2], zp_g, zp_s);
-        E0.a[2] = eym.x; E1.a[2] = eym.y;
-        E0.a[3] = eyp.x; E1.a[3] = eyp.y;
-        E0.a[4] = ezm.x; E1.a[4] = ezm.y;
-        E0.a[5] = ezp.x; E1.a[5] = ezp.y;
+        pair_eps<NC, OP>(L, b, e, q, E0, E1);
         nv = make_double2(ags_value<OP>(K, s0, E0, fr[r].x), ags_value<OP>(K, s1, E1, fr[r].y));
       } else {
         nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));

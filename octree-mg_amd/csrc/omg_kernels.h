@@ -24,6 +24,16 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
                        hipStream_t st, const int* boxes = nullptr, int n_boxes = 0);
 // whether launch_gs_substep takes the LDS-tiled kernel (which alone takes a shift)
+// M(NC, BS, OPV) for the operator op (OPV a compile-time Op)
+#define OMG_FOR_OP(op, M, NC, BS)         \
+  switch (op) {                           \
+    case OP_HELM: M(NC, BS, OP_HELM) break;   \
+    case OP_VLPL: M(NC, BS, OP_VLPL) break;   \
+    case OP_VHELM: M(NC, BS, OP_VHELM) break; \
+    case OP_AHELM: M(NC, BS, OP_AHELM) break; \
+    default: M(NC, BS, OP_LPL) break;         \
+  }
+
 // (every operator; refinement-boundary faces are filled in its epilogue)
 inline bool gs_tiled(int nc, int op, bool has_rb) {
   (void)op;

@@ -63,7 +63,9 @@ __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const Lev
     const double2 cc = reinterpret_cast<const double2*>(sb)[q2];
     s0.c = cc.x;
     s1.c = cc.y;
-    const double r0 = fr[r].x - op_value<OP>(K, s0), r1 = fr[r].y - op_value<OP>(K, s1);
+    double l0, l1;
+    op_pair<NC, OP>(K, F, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
+    const double r0 = fr[r].x - l0, r1 = fr[r].y - l1;
     mx = fmax(mx, fmax(fabs(r0), fabs(r1)));
     rv[r] = make_double2(r0, r1);
     st_nt(res + 2 * q2, r0, r1);
@@ -606,13 +608,9 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
                            const int* dixp, hipStream_t st) {
   if (F.n == 0) return;
   const dim3 g(F.n);
-#define OMG_RR(NC, BS)                                                                                 \
-  if (op == OP_HELM)                                                                                   \
-    k_resid_restrict<NC, OP_HELM, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on,      \
-                                                              parent_local, dixp);                     \
-  else                                                                                                 \
-    k_resid_restrict<NC, OP_LPL, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on,       \
-                                                             parent_local, dixp);
+#define OMG_RR_OP(NC, BS, OPV) \
+  k_resid_restrict<NC, OPV, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, dixp);
+#define OMG_RR(NC, BS) OMG_FOR_OP(op, OMG_RR_OP, NC, BS)
   switch (F.nc) {
     case 16: OMG_RR(16, 512) break;
     case 8: OMG_RR(8, 256) break;
@@ -620,6 +618,7 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
     default: OMG_RR(2, 256) break;
   }
 #undef OMG_RR
+#undef OMG_RR_OP
 }
 
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
@@ -690,9 +689,11 @@ __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambd
     const double2 cc = reinterpret_cast<const double2*>(sb)[q2];
     s0.c = cc.x;
     s1.c = cc.y;
+    double l0, l1;
+    op_pair<NC, OP>(K, Cv, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
     v2d out;
-    out.x = op_value<OP>(K, s0) + rr[r].x;
-    out.y = op_value<OP>(K, s1) + rr[r].y;
+    out.x = l0 + rr[r].x;
+    out.y = l1 + rr[r].y;
     reinterpret_cast<v2d*>(rhs)[q2] = out;
   }
 }
@@ -705,14 +706,11 @@ __global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lam
 
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
                             hipStream_t st) {
-  if (!tiled_nc(C.nc) || (op != OP_LPL && op != OP_HELM)) return false;
+  if (!tiled_nc(C.nc)) return false;
   if (n_par == 0) return true;
   const dim3 g(n_par);
-#define OMG_CR(NC, BS)                                                                                  \
-  if (op == OP_HELM)                                                                                    \
-    k_coarse_rhs_tile<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, lambda, parents);                          \
-  else                                                                                                  \
-    k_coarse_rhs_tile<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, lambda, parents);
+#define OMG_CR_OP(NC, BS, OPV) k_coarse_rhs_tile<NC, OPV, BS><<<g, BS, 0, st>>>(C, lambda, parents);
+#define OMG_CR(NC, BS) OMG_FOR_OP(op, OMG_CR_OP, NC, BS)
   switch (C.nc) {
     case 16: OMG_CR(16, 512) break;
     case 8: OMG_CR(8, 256) break;
@@ -720,6 +718,7 @@ bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int
     default: OMG_CR(2, 256) break;
   }
 #undef OMG_CR
+#undef OMG_CR_OP
   return true;
 }
 

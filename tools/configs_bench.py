@@ -7,9 +7,8 @@ For each configuration (omg_golden argument strings, tests/mgdriver.py):
     V-cycles (FMG for 'f'), everything resident in HBM; cells = leaf cells of
     the tree, value = cells x cycles / s; the finest-level smoother launch time
     from HIP events (omg_set_profiling) gives its HBM roofline fraction at the
-    algorithmic 12 B per level cell per red-black substep (24 B per GS sweep);
-  * optional loopback run (N contexts on this one GPU, RCCL replaced by device
-    copies): checks the multi-rank path at that configuration, not a timing;
+    algorithmic 24 B per cell update (+16 B per eps variable of the
+    variable-coefficient operators);
   * CPU: the reference itself (oracle/_ref/omg_golden, amdflang -O2, MPICH,
     mpiexec -n P) on the same configuration, its own mpi_wtime per cycle.
 
@@ -87,7 +86,11 @@ def gpu_run(args, warmup=2):
     mg.ctx.call("set_profiling", 0)
     hi = mg.highest_lvl
     roof = None
-    for fam, bpu in (("smoother_gsrb", 24.0), ("smoother_gs", 24.0)):
+    # algorithmic bytes per cell update: phi read + write and rhs (24 B), plus
+    # every eps variable in full (both colours) per red-black substep, i.e.
+    # 16 B per variable per update (vlaplacian / vhelmholtz 1, ahelmholtz 3)
+    n_eps = {"vlpl": 1, "vhelm": 1, "ahelm": 3}.get(cfg["op"], 0)
+    for fam, bpu in (("smoother_gsrb", 24.0 + 16.0 * n_eps), ("smoother_gs", 24.0 + 8.0 * n_eps)):
         n, ms, upd = mg.ctx.kernel_stats(f"{fam}@{hi}")
         if n and ms > 0:
             # cells counts the updates of the launch (half a level per RB substep)
