@@ -881,6 +881,8 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
 // on this GPU, LDS-tiled box size, no refinement boundary, and every parent
 // with all its children here.  INT_MIN when not even the lowest level can.
 int tail_top(omg_ctx* c, int max_lvl) {
+  // (the variable-coefficient operators measured faster level by level:
+  // their single-workgroup program spills heavily)
   if (c->smoother != OMG_SMOOTHER_GSRB || (c->op != OP_LPL && c->op != OP_HELM)) return INT_MIN;
   if (max_lvl - c->lowest + 1 > kTailMaxLevels) max_lvl = c->lowest + kTailMaxLevels - 1;
   int top = INT_MIN;
