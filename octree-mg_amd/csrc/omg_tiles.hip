@@ -14,6 +14,19 @@
 #include "omg_gsrb.h"
 #include "omg_kernels.h"
 
+// k_prolong_smooth tuning: waves per SIMD it is compiled for; PRE issues the
+// substep's rhs loads before the correction phases (A/B builds only)
+#ifndef OMG_PS_WAVES
+#define OMG_PS_WAVES 8
+#endif
+#ifndef OMG_PS_PRE
+#define OMG_PS_PRE 0
+#endif
+// leaves per wave of the get_sum box sums (a wave per 64 threads)
+#ifndef OMG_SUMS_LPW
+#define OMG_SUMS_LPW 32
+#endif
+
 namespace omg {
 
 template <int NC, int OP, int BS>
@@ -290,6 +303,10 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     const int q2 = tid + BS * r;
     if (q2 < HV / 2) old[r] = ld_nt(u + 2 * q2);
   }
+#if OMG_PS_PRE
+  GsrbRhs<NC, BS> pre;
+  gsrb_load_rhs<NC, BS, 2>(F, 1, b, pre);
+#endif
   // ---- colour-0 ghost values from same-GPU neighbours: the neighbour's
   // old boundary value (still in our ghost slot) + its prolongation
   constexpr int NG = (6 * FH + BS - 1) / BS;
@@ -428,13 +445,14 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   }
   __syncthreads();
   // ---- substep 1: colour 1 from colour 0, then its ghost fill (push colour 1)
+#if OMG_PS_PRE
+  gsrb_box<NC, OP, BS, 2, true>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, &pre);
+#else
   gsrb_box<NC, OP, BS, 2, true>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds);
+#endif
 }
 
 template <int NC, int OP, int BS>
-#ifndef OMG_PS_WAVES
-#define OMG_PS_WAVES 8
-#endif
 // 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64
 __global__ void __launch_bounds__(BS, OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
@@ -464,24 +482,24 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
 
 // get_sum's per-leaf interior sums (m_multigrid.f90:286-290): one lane per
 // leaf, each summing its box sequentially in column-major order from +0.0
-// (amdflang -O2 emits a single accumulator).  A wave owns 32 leaves and
+// (amdflang -O2 emits a single accumulator).  A wave owns LPW leaves and
 // streams them through LDS in chunks of R rows: the loads are whole 256-B
 // colour segments shared by 64 lanes (coalesced), the next chunk is in flight
 // while the lanes run their add chains out of LDS.
 // SUB: subtract_mean fused in front (m_multigrid.f90:268-272, no ghosts): every
 // value is replaced by v - mean in HBM and the box sums are those of the new
 // values (what the next get_sum of this variable will need).
-template <int NC, bool SUB>
+template <int NC, bool SUB, int LPW = OMG_SUMS_LPW>
 __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
                                                   int n_leaves, double* __restrict__ out,
                                                   const double* __restrict__ mean) {
   constexpr int H = NC / 2, R = 4, SEG = R * H;   // doubles of one colour in a chunk
   constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
-  constexpr int PER = 32 * CH2 / 64;              // double2 per lane per chunk
+  constexpr int PER = LPW * CH2 / 64;             // double2 per lane per chunk
   constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
   constexpr int NCH = NC * NC / R;
-  __shared__ double lds[32 * P];
-  const int lane = threadIdx.x, b0 = blockIdx.x * 32;
+  __shared__ double lds[LPW * P];
+  const int lane = threadIdx.x, b0 = blockIdx.x * LPW;
   const long long hv = L.hv;
   double* src[PER];
   int dst[PER];
@@ -521,7 +539,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
 #pragma unroll
       for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r] + r1);
     }
-    if (lane < 32) {
+    if (lane < LPW) {
 #pragma unroll
       for (int rr = 0; rr < R; rr++) {
         const int ca = (1 + j0 + rr + k) & 1;   // colour of the odd-i cells of row j0+rr
@@ -535,7 +553,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
       }
     }
   }
-  if (lane < 32 && b0 + lane < n_leaves) out[b0 + lane] = acc;
+  if (lane < LPW && b0 + lane < n_leaves) out[b0 + lane] = acc;
 }
 
 // generic box size: one lane per leaf straight from HBM
@@ -724,7 +742,7 @@ bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int
 
 void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
   if (n == 0) return;
-  const dim3 g((n + 31) / 32);
+  const dim3 g((n + OMG_SUMS_LPW - 1) / OMG_SUMS_LPW);
   switch (L.nc) {
     case 16: k_box_sums3<16, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
     case 8: k_box_sums3<8, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
@@ -738,7 +756,7 @@ bool subtract_sums_nc(int nc) { return nc == 16 || nc == 8 || nc == 4; }
 void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
                           hipStream_t st) {
   if (n == 0) return;
-  const dim3 g((n + 31) / 32);
+  const dim3 g((n + OMG_SUMS_LPW - 1) / OMG_SUMS_LPW);
   switch (L.nc) {
     case 16: k_box_sums3<16, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
     case 8: k_box_sums3<8, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
