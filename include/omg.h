@@ -151,6 +151,20 @@ int omg_subtract_mean(omg_ctx *ctx, int iv, int include_ghostcells);
                                                       /* subtract_mean, m_multigrid.f90:245-276 */
 int omg_phi_bc_store(omg_ctx *ctx);                   /* mg_phi_bc_store, m_ghost_cells.f90:66-117 */
 
+/* m_diffusion (src/m_diffusion.f90).  omg_set_rhs: its set_rhs (:144-159),
+ * rhs = f1*phi + f2*rhs on the interior of this rank's leaves.
+ * omg_diffusion_solve: diffusion_solve (:19-57) for op = OMG_HELMHOLTZ,
+ * diffusion_solve_vcoeff (:63-101) for OMG_VHELMHOLTZ (coefficient in var 5),
+ * diffusion_solve_acoeff (:108-142) for OMG_AHELMHOLTZ (vars 5..7), which
+ * take diffusion_coeff = 1.  One implicit step of order 1 or 2 on phi: the
+ * context's operator and lambda are left as the reference leaves them, then
+ * FMG and up to 10 V-cycles until max_res.  *n_vcycles = V-cycles after the
+ * FMG, *res = the last max residual.  Errors: "order should be 1 or 2",
+ * "no convergence" (the reference's error stops). */
+int omg_set_rhs(omg_ctx *ctx, double f1, double f2);
+int omg_diffusion_solve(omg_ctx *ctx, int op, double dt, double diffusion_coeff, int order,
+                        double max_res, int *n_vcycles, double *res);
+
 /* The communication plan of level lvl as built by omg_tree_setup: transfer
  * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,
  * 3 refinement-boundary faces, 4 copies of the host's boxes of a replicated

@@ -1033,6 +1033,76 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
   return max_res;
 }
 
+// mg_set_methods' operator part + *_set_lambda (m_multigrid.f90:27-60,
+// m_helmholtz.f90:39-46, m_vhelmholtz.f90:51-58, m_ahelmholtz.f90:59-66)
+void set_operator(omg_ctx* c, int op, double lambda) {
+  if (op < OMG_LAPLACIAN || op > OMG_AHELMHOLTZ) throw OmgError("mg_set_methods: unknown operator");
+  if (lambda < 0) throw OmgError("helmholtz_set_lambda: lambda < 0 not allowed");
+  if (op == OMG_AHELMHOLTZ && c->n_vars < 7 && c->n_boxes > 0)
+    throw OmgError("ahelmholtz_set_methods: needs 3 extra variables");
+  if ((op == OMG_VLAPLACIAN || op == OMG_VHELMHOLTZ) && c->n_vars < 5 && c->n_boxes > 0)
+    throw OmgError("vlaplacian/vhelmholtz_set_methods: mg%n_extra_vars == 0");
+  if (op == OMG_VLAPLACIAN) lambda = 0.0;
+  c->op = op;
+  c->lambda = lambda;
+}
+
+// mg_apply_op (m_multigrid.f90:439-456): box_op on every box of every level
+void apply_op(omg_ctx* c, int i_out) {
+  enter(c);
+  if (i_out == 1) phi_dirty_all(c);
+  for (int l = c->lowest; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (L && L->n) launch_box_op(L->view(), c->op, c->lambda, i_out, c->stream);
+  }
+}
+
+// m_diffusion's set_rhs (m_diffusion.f90:144-159): rhs = f1*phi + f2*rhs on
+// the interior of this rank's leaves of levels 1..highest
+void set_rhs(omg_ctx* c, double f1, double f2) {
+  enter(c);
+  for (int l = 1; l <= c->highest; l++) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->leaves.empty()) continue;
+    launch_set_rhs(L->view(), L->d_leaves, (int)L->leaves.size(), f1, f2, c->stream);
+  }
+}
+
+// diffusion_solve / diffusion_solve_vcoeff / diffusion_solve_acoeff
+// (m_diffusion.f90:19-57, :63-101, :108-142): one implicit time step of
+// order 1 (backward Euler) or 2 (Crank-Nicolson) as a Helmholtz problem,
+// FMG first, then up to 10 V-cycles until max_res.  The three differ only in
+// the operator and in lambda = 1/(dt*D) vs 1/dt (D = 1 for the v/a forms).
+constexpr int kDiffusionMaxIts = 10;   // m_diffusion.f90:25
+void diffusion_solve(omg_ctx* c, int op, double dt, double coeff, int order, double max_res, int* n_vcycles,
+                     double* res_out) {
+  if (op != OMG_HELMHOLTZ && op != OMG_VHELMHOLTZ && op != OMG_AHELMHOLTZ)
+    throw OmgError("diffusion_solve: operator must be helmholtz, vhelmholtz or ahelmholtz");
+  if (order != 1 && order != 2) throw OmgError("diffusion_solve: order should be 1 or 2");
+  const double dtc = op == OMG_HELMHOLTZ ? dt * coeff : dt;
+  // helmholtz_set_methods / vhelmholtz_set_methods clear subtract_mean;
+  // ahelmholtz_set_methods leaves it as it was
+  set_operator(c, op, 0.0);
+  if (op != OMG_AHELMHOLTZ) c->subtract_mean = 0;
+  if (order == 1) {
+    set_operator(c, op, 1 / dtc);
+    set_rhs(c, -1 / dtc, 0.0);
+  } else {
+    apply_op(c, 2);   // lambda = 0: rhs = L(phi) on every level
+    set_operator(c, op, 2 / dtc);
+    set_rhs(c, -2 / dtc, -1.0);
+  }
+  double res = fas_fmg(c, true, true);
+  int n = 1;
+  for (; n <= kDiffusionMaxIts; n++) {
+    if (res <= max_res) break;
+    res = fas_vcycle(c, c->lowest - 1, true, true);
+  }
+  if (n_vcycles) *n_vcycles = n - 1;
+  if (res_out) *res_out = res;
+  if (n == kDiffusionMaxIts + 1) throw OmgError("diffusion_solve: no convergence");
+}
+
 // ---------------------------------------------------------------------------
 // Plan builder (device side of mg_allocate_storage, m_allocate_storage.f90:51-99,
 // and of the three buffer dry runs m_ghost_cells.f90:17-62, m_restrict.f90:
@@ -1551,17 +1621,7 @@ int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* pee
 }
 
 int omg_set_operator(omg_ctx* c, int op, double lambda) {
-  return guarded([&] {
-    if (op < OMG_LAPLACIAN || op > OMG_AHELMHOLTZ) throw OmgError("mg_set_methods: unknown operator");
-    if (lambda < 0) throw OmgError("helmholtz_set_lambda: lambda < 0 not allowed");
-    if (op == OMG_AHELMHOLTZ && c->n_vars < 7 && c->n_boxes > 0)
-      throw OmgError("ahelmholtz_set_methods: needs 3 extra variables");
-    if ((op == OMG_VLAPLACIAN || op == OMG_VHELMHOLTZ) && c->n_vars < 5 && c->n_boxes > 0)
-      throw OmgError("vlaplacian/vhelmholtz_set_methods: mg%n_extra_vars == 0");
-    if (op == OMG_VLAPLACIAN) lambda = 0.0;
-    c->op = op;
-    c->lambda = lambda;
-  });
+  return guarded([&] { set_operator(c, op, lambda); });
 }
 
 int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up, int max_coarse_cycles,
@@ -1742,14 +1802,16 @@ int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
 }
 
 int omg_apply_op(omg_ctx* c, int i_out) {
-  return guarded([&] {
-    enter(c);
-    if (i_out == 1) phi_dirty_all(c);
-    for (int l = c->lowest; l <= c->highest; l++) {
-      Level* L = level_ptr(c, l);
-      if (L && L->n) launch_box_op(L->view(), c->op, c->lambda, i_out, c->stream);
-    }
-  });
+  return guarded([&] { apply_op(c, i_out); });
+}
+
+int omg_set_rhs(omg_ctx* c, double f1, double f2) {
+  return guarded([&] { set_rhs(c, f1, f2); });
+}
+
+int omg_diffusion_solve(omg_ctx* c, int op, double dt, double diffusion_coeff, int order, double max_res,
+                        int* n_vcycles, double* res) {
+  return guarded([&] { diffusion_solve(c, op, dt, diffusion_coeff, order, max_res, n_vcycles, res); });
 }
 
 int omg_restrict(omg_ctx* c, int iv) {

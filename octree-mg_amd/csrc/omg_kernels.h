@@ -70,6 +70,7 @@ void launch_prolong_pack(const LevelView& C, const LevelView& F, int iv, const i
 void launch_prolong_unpack(const LevelView& F, int iv_to, int add, const int* items, int n,
                            const double* buf, hipStream_t st);
 void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts, hipStream_t st);
+void launch_set_rhs(const LevelView& L, const int* leaves, int n_leaves, double f1, double f2, hipStream_t st);
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st);
 void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t st);
 void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st);

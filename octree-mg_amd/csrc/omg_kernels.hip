@@ -372,6 +372,21 @@ __global__ void __launch_bounds__(256) k_subtract_even(LevelView L, int iv, cons
   }
 }
 
+// m_diffusion's set_rhs (src/m_diffusion.f90:144-159): rhs = f1*phi + f2*rhs
+// on the interior of the given leaves, one thread per cell.
+__global__ void __launch_bounds__(256) k_set_rhs(LevelView L, const int* __restrict__ leaves, int n_leaves,
+                                                 double f1, double f2) {
+  const long long per = 2LL * L.hv;
+  GRID_STRIDE(t, per * n_leaves) {
+    const int b = leaves[t / per], o = (int)(t % per);
+    int i, j, k;
+    if (!cell_of(L, o, i, j, k)) continue;
+    const double u = boxp(L, 1, b)[o];
+    double* f = boxp(L, 2, b) + o;
+    *f = f1 * u + f2 * *f;
+  }
+}
+
 // Whole-box copy / zero of one variable (FMG's old = phi and phi = 0).
 __global__ void __launch_bounds__(256) k_copy_var(LevelView L, int src, int dst) {
   GRID_STRIDE(t, (long long)L.n * L.stride) {
@@ -574,6 +589,12 @@ void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts,
     return;
   }
   k_subtract<<<grid_for(work), 256, 0, st>>>(L, iv, mean, ghosts);
+}
+
+void launch_set_rhs(const LevelView& L, const int* leaves, int n_leaves, double f1, double f2, hipStream_t st) {
+  const long long work = 2LL * L.hv * n_leaves;
+  if (work == 0) return;
+  k_set_rhs<<<grid_for(work), 256, 0, st>>>(L, leaves, n_leaves, f1, f2);
 }
 
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st) {

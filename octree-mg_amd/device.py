@@ -55,6 +55,8 @@ SIGNATURES = {
     "omg_get_sum": (_I, [_P, _I, C.POINTER(_D)]),
     "omg_subtract_mean": (_I, [_P, _I, _I]),
     "omg_phi_bc_store": (_I, [_P]),
+    "omg_set_rhs": (_I, [_P, _D, _D]),
+    "omg_diffusion_solve": (_I, [_P, _I, _D, _D, _I, _D, C.POINTER(_I), C.POINTER(_D)]),
     "omg_synchronize": (_I, [_P]),
     "omg_stream": (_P, [_P]),
     "omg_set_profiling": (_I, [_P, _I]),

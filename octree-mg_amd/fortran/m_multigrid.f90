@@ -56,6 +56,7 @@ module m_multigrid
   public :: mg_gpu_set_resident
   public :: mg_gpu_to_host
   public :: mg_gpu_to_device
+  public :: mg_gpu_diffusion_solve
 
 contains
 
@@ -189,6 +190,32 @@ contains
     call omg_ok(omg_apply_op(ctx, int(i_out, c_int)), "mg_apply_op")
     if (.not. resident) call copy_var_to_host(mg, i_out)
   end subroutine mg_apply_op
+
+  !> One implicit diffusion step on the GPU for the drop-in m_diffusion
+  !> (omg_diffusion_solve: lambda, set_rhs, FMG and the V-cycle loop of
+  !> src/m_diffusion.f90:19-142 without a host round trip).  converged is
+  !> .false. where the reference stops with "diffusion_solve: no convergence".
+  subroutine mg_gpu_diffusion_solve(mg, dt, diffusion_coeff, order, max_res, converged)
+    type(mg_t), intent(inout) :: mg
+    real(dp), intent(in)      :: dt, diffusion_coeff, max_res
+    integer, intent(in)       :: order
+    logical, intent(out)      :: converged
+    integer(c_int)            :: ierr, n_v
+    real(c_double)            :: res
+
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call sync_in(mg)
+    call mg_timer_start(mg%timers(timer_device_fmg))
+    ierr = omg_diffusion_solve(ctx, int(mg%operator_type, c_int), real(dt, c_double), &
+         real(diffusion_coeff, c_double), int(order, c_int), real(max_res, c_double), n_v, res)
+    converged = ierr == 0
+    if (.not. converged .and. omg_error_message() /= "diffusion_solve: no convergence") &
+         call omg_ok(ierr, "diffusion_solve")
+    call omg_ok(omg_synchronize(ctx), "synchronize")
+    call mg_timer_end(mg%timers(timer_device_fmg))
+    call sync_out(mg)
+  end subroutine mg_gpu_diffusion_solve
 
   !> Resident mode on/off.  When on, mg_fas_vcycle / mg_fas_fmg / mg_apply_op
   !> neither upload mg%boxes(:)%cc before nor download it after: the GPU copy

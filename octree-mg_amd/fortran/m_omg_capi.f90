@@ -17,7 +17,7 @@ module m_omg_capi
   public :: omg_set_subtract_mean, omg_set_bc, omg_set_bc_faces
   public :: omg_level_size, omg_upload_level, omg_download_level
   public :: omg_fas_vcycle, omg_fas_fmg, omg_apply_op, omg_phi_bc_store
-  public :: omg_synchronize
+  public :: omg_synchronize, omg_diffusion_solve
 
   interface
      function omg_last_error() bind(C, name="omg_last_error") result(p)
@@ -160,6 +160,17 @@ module m_omg_capi
        type(c_ptr), value :: ctx
        integer(c_int) :: ierr
      end function omg_phi_bc_store
+
+     function omg_diffusion_solve(ctx, op, dt, diffusion_coeff, order, max_res, n_vcycles, res) &
+          bind(C, name="omg_diffusion_solve") result(ierr)
+       import :: c_ptr, c_int, c_double
+       type(c_ptr), value          :: ctx
+       integer(c_int), value       :: op, order
+       real(c_double), value       :: dt, diffusion_coeff, max_res
+       integer(c_int), intent(out) :: n_vcycles
+       real(c_double), intent(out) :: res
+       integer(c_int) :: ierr
+     end function omg_diffusion_solve
 
      function omg_synchronize(ctx) bind(C, name="omg_synchronize") result(ierr)
        import :: c_ptr, c_int

@@ -16,13 +16,17 @@
 !
 ! Usage (positional):
 !   omg_golden box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres dump
-!     cycle    v | f
+!     cycle    v | f | d1 | d2  (d1/d2: one m_diffusion time step of order
+!              1/2 per iteration, dt = the lambda argument; op helm ->
+!              diffusion_solve with D = 0.5, vhelm -> diffusion_solve_vcoeff,
+!              ahelm -> diffusion_solve_acoeff; max_res 1e-8)
 !     smoother gs | gsrb
 !     op       lpl | helm | vlpl | vhelm   (v*: coefficient eps in var 5, solution in 6)
 !              | ahelm (eps1..3 in vars 5..7, solution in 8; the dump holds rhs)
 !     bc       sol (callback Dirichlet u) | d0 (Dirichlet 0) | per (periodic)
 !              | n0 (Neumann 0) | c0 (continuous)
-!     rhs      sol (rhs = L u) | one (rhs = 1)
+!     rhs      sol (rhs = L u) | one (rhs = 1) | phi (phi = u incl. ghosts,
+!              rhs = 0: the initial state of a diffusion run)
 !     n_levels 1 = uniform, >1 = test_refinement's AMR tree
 !     lb       lb (mg_load_balance) | lbp (+ mg_load_balance_parents)
 !     maxres   0 | 1  (request max_res from mg_fas_vcycle/mg_fas_fmg)
@@ -32,6 +36,7 @@
 program omg_golden
   use mpi
   use m_octree_mg
+  use m_diffusion
   implicit none
 
   integer, parameter  :: i8k = selected_int_kind(18)
@@ -41,8 +46,9 @@ program omg_golden
   logical             :: periodic(NDIM) = .false.
   real(dp), parameter :: pi = acos(-1.0_dp)
   character(len=64)   :: a_cycle, a_smoother, a_op, a_bc, a_rhs, a_lb, a_dump, arg
-  integer             :: n, ierr, maxres_flag, i_sol
+  integer             :: n, ierr, maxres_flag, i_sol, order
   real(dp)            :: max_res, t0, t1
+  real(dp), parameter :: diff_coeff = 0.5_dp, diff_tol = 1.0e-8_dp
   type(mg_t)          :: mg
 
   if (command_argument_count() < 15) error stop "omg_golden: need 15 args"
@@ -141,6 +147,9 @@ program omg_golden
   if (trim(a_rhs) == "sol") then
      call set_solution(mg, n_levels > 1)
      call compute_rhs_and_reset(mg)
+  else if (trim(a_rhs) == "phi") then
+     call set_solution(mg, n_levels > 1)
+     call copy_solution_to_phi(mg)
   else
      call set_rhs_one(mg)
   end if
@@ -149,7 +158,16 @@ program omg_golden
   t0 = mpi_wtime()
   do n = 1, n_its
      max_res = 0.0_dp
-     if (trim(a_cycle) == "f") then
+     if (a_cycle(1:1) == "d") then
+        read(a_cycle(2:2), *) order
+        if (mg%operator_type == mg_helmholtz) then
+           call diffusion_solve(mg, lambda, diff_coeff, order, diff_tol)
+        else if (mg%operator_type == mg_vhelmholtz) then
+           call diffusion_solve_vcoeff(mg, lambda, order, diff_tol)
+        else
+           call diffusion_solve_acoeff(mg, lambda, order, diff_tol)
+        end if
+     else if (trim(a_cycle) == "f") then
         if (maxres_flag == 1) then
            call mg_fas_fmg(mg, n > 1, max_res)
         else
@@ -256,6 +274,17 @@ contains
        end do
     end do
   end subroutine compute_rhs_and_reset
+
+  subroutine copy_solution_to_phi(mg)
+    type(mg_t), intent(inout) :: mg
+    integer                   :: n, id, lvl
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       do n = 1, size(mg%lvls(lvl)%my_ids)
+          id = mg%lvls(lvl)%my_ids(n)
+          mg%boxes(id)%cc(DTIMES(:), mg_iphi) = mg%boxes(id)%cc(DTIMES(:), i_sol)
+       end do
+    end do
+  end subroutine copy_solution_to_phi
 
   subroutine set_rhs_one(mg)
     type(mg_t), intent(inout) :: mg

@@ -804,3 +804,49 @@ void orc_fas_fmg(orc_mg *mg, int have_guess, int want_max_res, double *max_res) 
         else orc_fas_vcycle(mg, l, 0, NULL, 0);
     }
 }
+
+/* set_rhs of m_diffusion (reference: src/m_diffusion.f90:144-159):
+ * rhs = f1*phi + f2*rhs on the interior of the leaves of levels 1..highest. */
+void orc_set_rhs(orc_mg *mg, double f1, double f2) {
+    for (int l = 1; l <= mg->highest; l++) {
+        int nc = NCL(mg, l);
+        for (int n = 0; n < LV(mg, l).n_leaves; n++) {
+            int id = LV(mg, l).leaves[n];
+            for (int k = 1; k <= nc; k++)
+                for (int j = 1; j <= nc; j++)
+                    for (int i = 1; i <= nc; i++)
+                        CC(id, nc, i, j, k, 2) = f1 * CC(id, nc, i, j, k, 1) + f2 * CC(id, nc, i, j, k, 2);
+        }
+    }
+}
+
+/* diffusion_solve / _vcoeff / _acoeff (reference: src/m_diffusion.f90:19-57,
+ * :63-101, :108-142).  op selects the variant (helmholtz: lambda from
+ * 1/(dt*D); vhelmholtz / ahelmholtz: 1/dt, pass D = 1).  Returns 0, or
+ * 1 "no convergence" (after 10 V-cycles), 2 "order should be 1 or 2". */
+int orc_diffusion_solve(orc_mg *mg, int op, double dt, double coeff, int order, double max_res,
+                        int *n_vcycles, double *res_out) {
+    if (order != 1 && order != 2) return 2;                 /* :42-43 */
+    double dtc = op == ORC_HELMHOLTZ ? dt * coeff : dt;
+    mg->op = op;                                            /* :29-30, mg_set_methods */
+    if (op != ORC_AHELMHOLTZ) mg->subtract_mean = 0;        /* m_helmholtz.f90:21, m_vhelmholtz.f90:28 */
+    if (order == 1) {                                       /* :33-35 */
+        mg->lambda = 1 / dtc;
+        orc_set_rhs(mg, -1 / dtc, 0.0);
+    } else {                                                /* :36-40 */
+        mg->lambda = 0.0;
+        orc_apply_op(mg, 2);
+        mg->lambda = 2 / dtc;
+        orc_set_rhs(mg, -2 / dtc, -1.0);
+    }
+    double res = 0.0;
+    orc_fas_fmg(mg, 1, 1, &res);                            /* :47 */
+    int n;
+    for (n = 1; n <= 10; n++) {                             /* :50-53 */
+        if (res <= max_res) break;
+        orc_fas_vcycle(mg, mg->lowest - 1, 1, &res, 1);
+    }
+    if (n_vcycles) *n_vcycles = n - 1;
+    if (res_out) *res_out = res;
+    return n == 11 ? 1 : 0;                                 /* :55-58 */
+}

@@ -47,6 +47,9 @@ def lib():
         for f in ("orc_apply_op",):
             getattr(L, f).argtypes = [_P, _I]
         L.orc_box_op.argtypes = [_P, _I, _I]
+        L.orc_set_rhs.argtypes = [_P, _D, _D]
+        L.orc_diffusion_solve.restype = _I
+        L.orc_diffusion_solve.argtypes = [_P, _I, _D, _D, _I, _D, C.POINTER(_I), C.POINTER(_D)]
         L.orc_restrict.argtypes = [_P, _I]
         L.orc_restrict_lvl.argtypes = [_P, _I, _I]
         L.orc_fill_ghost_cells.argtypes = [_P, _I]
@@ -150,6 +153,12 @@ class Oracle:
         r = C.c_double(0.0)
         self.L.orc_fas_fmg(self.h, int(have_guess), int(want_max_res), C.byref(r))
         return r.value
+
+    def diffusion_solve(self, op, dt, coeff, order, max_res):
+        """m_diffusion's time step (orc_diffusion_solve): (status, n_vcycles, res)."""
+        n, r = C.c_int(0), C.c_double(0.0)
+        rc = self.L.orc_diffusion_solve(self.h, op, dt, coeff, order, max_res, C.byref(n), C.byref(r))
+        return rc, n.value, r.value
 
     def __getattr__(self, name):
         # thin pass-through: orc.<fn>(args) -> liboracle.orc_<fn>(h, args)

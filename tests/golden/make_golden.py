@@ -60,14 +60,35 @@ CONFIGS = {
     "ref3_gs_f": ("8 32 32 32 5 f gs lpl 0 sol sol 3 lb 1", True, [1, 3]),
     "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1, 3]),
     "c4_ref2_box16": ("16 128 128 128 4 v gs lpl 0 sol sol 2 lb 0", False, [1, 3, 4]),
+    # §8(f) row 1: m_diffusion — one implicit time step per iteration from
+    # phi = u (cycle d1 = backward Euler, d2 = Crank-Nicolson; the lambda
+    # field is dt; helm: diffusion_solve with D = 0.5, vhelm: _vcoeff)
+    "diff_helm_d1_n0": ("8 32 32 32 4 d1 gsrb helm 0.001 n0 phi 1 lb 0", True, [1, 2]),
+    "diff_helm_d2_d0": ("8 32 32 32 4 d2 gsrb helm 0.001 d0 phi 1 lb 0", True, [1]),
+    "diff_helm_d2_box16": ("16 64 64 64 2 d2 gsrb helm 0.0001 d0 phi 1 lb 0", True, [1]),
+    "diff_helm_d1_ref2": ("8 32 32 32 3 d1 gsrb helm 0.001 n0 phi 2 lb 0", True, [1, 3]),
+    "diff_vhelm_d1_per": ("8 32 32 32 3 d1 gsrb vhelm 0.01 per phi 1 lb 0", True, [1, 4]),
+    # the reference's error stop "diffusion_solve: no convergence" (10 V-cycles
+    # after the FMG without reaching max_res)
+    "diff_nonconv_helm_per_ref2": ("8 32 32 32 3 d2 gs helm 0.01 per phi 2 lb 0", False, [1], True),
+    "diff_nonconv_vhelm_sol": ("8 32 32 32 3 d2 gs vhelm 0.001 sol phi 1 lb 0", False, [1], True),
 }
 
 
-def run(args, ranks, dump):
+def run(args, ranks, dump, expect_error=False):
     cmd = [os.path.join(REF, "omg_golden")] + args.split() + [dump or "x"]
     if ranks > 1:
         cmd = [MPIEXEC, "-n", str(ranks)] + cmd
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    out, err = p.stdout, None
+    if expect_error:
+        assert p.returncode != 0, "expected an error stop"
+        for line in (p.stdout + p.stderr).splitlines():
+            if "ERROR STOP:" in line:
+                err = line.split("ERROR STOP:", 1)[1].strip()
+        assert err, p.stderr
+    elif p.returncode != 0:
+        raise subprocess.CalledProcessError(p.returncode, cmd, p.stdout, p.stderr)
     its, t = [], None
     for line in out.splitlines():
         f = line.split()
@@ -75,18 +96,31 @@ def run(args, ranks, dump):
             its.append({"it": int(f[1]), "err": f[2], "res": f[3], "max_res": f[4]})
         elif f and f[0] == "TIME":
             t = float(f[1])
-    return its, t
+    return (its, t, err) if expect_error else (its, t)
 
 
 def main():
+    """make_golden.py [name ...]: all configurations, or only the named ones
+    (merged into the existing golden.json)."""
     if not os.path.exists(os.path.join(REF, "omg_golden")):
         sys.exit("build the reference first: make -C oracle ref")
-    golden = {}
-    for name, (args, dump, ranks) in CONFIGS.items():
+    path = os.path.join(HERE, "golden.json")
+    only = sys.argv[1:]
+    golden = json.load(open(path))["configs"] if only else {}
+    for name, spec in CONFIGS.items():
+        if only and name not in only:
+            continue
+        args, dump, ranks = spec[:3]
+        expect_error = len(spec) > 3 and spec[3]
         entry = {"args": args, "runs": {}}
         for r in ranks:
             with tempfile.TemporaryDirectory() as td:
                 fn = os.path.join(td, "phi.bin") if (dump and r == 1) else None
+                if expect_error:
+                    its, t, err = run(args, r, fn, True)
+                    entry["runs"][str(r)] = {"history": its, "error": err}
+                    print(name, r, err, file=sys.stderr)
+                    continue
                 its, t = run(args, r, fn)
                 run_entry = {"history": its, "ref_seconds_per_cycle": t}
                 if fn:
@@ -98,7 +132,7 @@ def main():
             entry["runs"][str(r)] = run_entry
             print(name, r, its[-1]["err"], its[-1]["res"], file=sys.stderr)
         golden[name] = entry
-    with open(os.path.join(HERE, "golden.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference": "FermiQ/octree-mg @ 2025-06-14, amdflang -O2, MPICH 3.3.2",
                    "configs": golden}, f, indent=1)

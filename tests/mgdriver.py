@@ -97,6 +97,14 @@ def n_vars(cfg):
 
 OPS = {"lpl": 1, "vlpl": 2, "helm": 3, "vhelm": 4, "ahelm": 5}
 
+# omg_golden's diffusion runs (cycle d1 / d2): max_res of every step, and the
+# coefficient D of diffusion_solve (the v/a forms take none: 1)
+DIFF_TOL = 1.0e-8
+
+
+def diffusion_coeff(cfg):
+    return 0.5 if cfg["op"] == "helm" else 1.0
+
 
 class OracleBackend:
     def __init__(self, cfg, n_ranks=1):
@@ -143,6 +151,15 @@ class OracleBackend:
 
     def fmg(self, have_guess, want):
         return self.o.fas_fmg(have_guess, bool(want))
+
+    def diffusion(self, order, dt):
+        op = OPS[self.cfg["op"]]
+        rc, n, res = self.o.diffusion_solve(op, dt, diffusion_coeff(self.cfg), order, DIFF_TOL)
+        if rc == 2:
+            raise RuntimeError("diffusion_solve: order should be 1 or 2")
+        if rc == 1:
+            raise RuntimeError("diffusion_solve: no convergence")
+        return res
 
 
 class DeviceBackend:
@@ -207,6 +224,14 @@ class DeviceBackend:
     def fmg(self, have_guess, want):
         return omg.mg_fas_fmg(self.mg, have_guess, max_res=bool(want)) or 0.0
 
+    def diffusion(self, order, dt):
+        op = self.cfg["op"]
+        if op == "helm":
+            return omg.diffusion_solve(self.mg, dt, diffusion_coeff(self.cfg), order, DIFF_TOL)
+        if op == "vhelm":
+            return omg.diffusion_solve_vcoeff(self.mg, dt, order, DIFF_TOL)
+        return omg.diffusion_solve_acoeff(self.mg, dt, order, DIFF_TOL)
+
 
 def _apply_bc(cfg, tree, set_bc, set_faces):
     bc = cfg["bc"]
@@ -245,7 +270,16 @@ def setup_problem(be):
                     put(lvl, I_EPS + d - 1, lambda ids: e * float(d))
             else:
                 put(lvl, I_EPS, lambda ids: e)
-    if cfg["rhs"] == "sol":
+    if cfg["rhs"] == "phi":
+        # copy_solution_to_phi: phi = u incl. ghosts, rhs stays 0
+        for lvl in be.levels():
+            put(lvl, I_SOL, lambda ids: P.level_solution(tree, lvl, ids))
+        if cfg["n_levels"] > 1:
+            be.restrict(I_SOL)
+            be.fill_ghost_cells(I_SOL)
+        for lvl in be.levels():
+            put(lvl, T.MG_IPHI, lambda ids: be.get_level(lvl, I_SOL))
+    elif cfg["rhs"] == "sol":
         for lvl in be.levels():
             put(lvl, I_SOL, lambda ids: P.level_solution(tree, lvl, ids))
         if cfg["n_levels"] > 1:
@@ -302,6 +336,15 @@ def phi_digest(be, iv=None):
     return h.hexdigest()
 
 
+class StepError(RuntimeError):
+    """A step that failed the way the reference's error stop does; .history
+    holds what was printed before it."""
+
+    def __init__(self, msg, history):
+        super().__init__(msg)
+        self.history = history
+
+
 def _cycles(be, cfg, reduce=None):
     hist = []
 
@@ -313,6 +356,14 @@ def _cycles(be, cfg, reduce=None):
 
     record(0, 0.0)
     for n in range(1, cfg["n_its"] + 1):
+        if cfg["cycle"] in ("d1", "d2"):
+            # one m_diffusion time step; omg_golden prints max_res = 0
+            try:
+                be.diffusion(int(cfg["cycle"][1]), cfg["lam"])
+            except RuntimeError as ex:
+                raise StepError(str(ex), hist) from ex
+            record(n, 0.0)
+            continue
         if cfg["cycle"] == "f":
             m = be.fmg(n > 1, cfg["maxres"])
         else:
@@ -330,7 +381,10 @@ def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None)
         cfg["n_its"] = n_its
     be = OracleBackend(cfg, n_ranks) if backend == "oracle" else DeviceBackend(cfg)
     setup_problem(be)
-    hist = _cycles(be, cfg, reduce)
+    try:
+        hist = _cycles(be, cfg, reduce)
+    except StepError as ex:   # the reference's error stop: what it printed + the message
+        return {"history": ex.history, "error": str(ex), "backend": be}
     out = {"history": hist, "phi_sha256": phi_digest(be), "backend": be}
     if cfg["op"] == "ahelm":
         out["rhs_sha256"] = phi_digest(be, T.MG_IRHS)

@@ -63,6 +63,11 @@ def test_dropin_golden(name):
     with tempfile.TemporaryDirectory() as td:
         dump = os.path.join(td, "dump.bin") if key else None   # phi, or rhs for ahelm
         p = run_driver(cfg["args"], dump)
+        if "error" in ref:   # the reference's error stop, after the same printed lines
+            assert p.returncode != 0
+            assert "ERROR STOP: " + ref["error"] in p.stdout + p.stderr
+            assert parse(p.stdout) == ref["history"]
+            return
         assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
         assert parse(p.stdout) == ref["history"]
         if dump:
@@ -92,7 +97,7 @@ def test_reference_programs_unchanged(name):
 
 RESIDENT = os.path.join(BUILD, "omg_golden_gpu_resident")
 RESIDENT_CASES = ["c1_gsrb_f_maxres", "per32_gsrb_v", "helm32_gs_c0", "ref3_gsrb_v", "vlpl32_gsrb_v",
-                  "u32_gs_d0_one"]
+                  "u32_gs_d0_one", "diff_helm_d2_d0", "diff_helm_d1_ref2", "diff_vhelm_d1_per"]
 
 
 @pytest.mark.gpu

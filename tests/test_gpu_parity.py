@@ -23,6 +23,7 @@ def test_device_matches_reference_golden(name):
     run = e["runs"]["1"]
     out = run_problem(e["args"], backend="device")
     assert out["history"] == run["history"]
+    assert out.get("error") == run.get("error")
     if "phi_sha256" in run:
         assert out["phi_sha256"] == run["phi_sha256"]
     if "rhs_sha256" in run:   # aniso operator pinned through rhs = L(u)
@@ -97,6 +98,8 @@ def test_per_operation_bitwise(args):
     assert c.scalar("get_sum", 1) == orc.o.get_sum(1)
     c.call("subtract_mean", 1, 1); orc.o.subtract_mean(1, 1)
     _assert_same(dev, orc)
+    c.call("set_rhs", 0.3, -1.7); orc.o.set_rhs(0.3, -1.7)   # m_diffusion's set_rhs
+    _assert_same(dev, orc)
 
 
 @pytest.mark.parametrize("args", [OPS_CASES[0], OPS_CASES[1], "16 64 64 64 1 v gsrb helm 2 d0 sol 1 lb 0"])
@@ -125,3 +128,29 @@ def test_ahelm_smoother_matches_oracle(args):
     orc = run_problem(args, backend="oracle")
     assert dev["history"] == orc["history"]
     assert dev["phi_sha256"] == orc["phi_sha256"]
+
+
+@pytest.mark.parametrize("args", ["8 32 32 32 2 d1 gsrb ahelm 0.01 n0 phi 1 lb 0",
+                                  "8 32 32 32 2 d2 gs ahelm 0.001 d0 phi 2 lb 0"])
+def test_ahelm_diffusion_matches_oracle(args):
+    """diffusion_solve_acoeff (m_diffusion.f90:108-142): like the aniso
+    V-cycle, held to the oracle's restatement (reference NaN, unpinned)."""
+    dev = run_problem(args, backend="device")
+    orc = run_problem(args, backend="oracle")
+    assert dev.get("error") == orc.get("error")
+    assert dev["history"] == orc["history"]
+    if "phi_sha256" in orc:
+        assert dev["phi_sha256"] == orc["phi_sha256"]
+
+
+def test_diffusion_bad_order_fails_like_reference():
+    """order 3: the reference's error stop (m_diffusion.f90:42-43) as an error,
+    with phi untouched."""
+    from tests.mgdriver import omg, phi_digest
+    cfg = parse("8 16 16 16 1 d1 gsrb helm 0.01 n0 phi 1 lb 0")
+    be = DeviceBackend(cfg)
+    setup_problem(be)
+    before = phi_digest(be)
+    with pytest.raises(omg.device.OmgError, match="order should be 1 or 2"):
+        be.mg.ctx.call("diffusion_solve", 3, 0.01, 1.0, 3, 1e-8, None, None)
+    assert phi_digest(be) == before

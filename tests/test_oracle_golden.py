@@ -24,6 +24,7 @@ def test_oracle_matches_reference(name, ranks):
     run = e["runs"][ranks]
     out = run_problem(e["args"], backend="oracle", n_ranks=int(ranks))
     assert out["history"] == run["history"]
+    assert out.get("error") == run.get("error")
     if "phi_sha256" in run:
         assert out["phi_sha256"] == run["phi_sha256"]
     if "rhs_sha256" in run:   # aniso operator pinned through rhs = L(u)
