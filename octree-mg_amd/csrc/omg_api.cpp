@@ -616,15 +616,35 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
   Level* C = level_ptr(c, lvl);
   if (c->no_fuse_up || !F || !C || !F->prolong_smooth_ok || c->smoother != OMG_SMOOTHER_GSRB ||
       (c->op != OP_LPL && c->op != OP_HELM) ||
-      c->n_cycle_up < 1 || F->has_rb || F->has_remote || !gs_tiled(F->nc, c->op, F->has_rb) ||
+      c->n_cycle_up < 1 || F->has_rb || (F->has_remote && !F->n_int) || !gs_tiled(F->nc, c->op, F->has_rb) ||
       !((size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc) ||
       (c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv)))
     return false;
   if (F->shift_pending) materialize_level(c, F);
+  const bool split = F->has_remote;
   {
-    Prof p(c, "prolong_smooth", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
+    const int n = split ? F->n_int : F->n;
+    Prof p(c, "prolong_smooth", (double)n * F->nc * F->nc * F->nc, lvl + 1);
     launch_prolong_smooth(C->view(), F->view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
-                          bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, c->stream);
+                          bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, split ? F->d_int : nullptr, n,
+                          split ? F->d_push0 : nullptr, c->stream);
+  }
+  if (split) {
+    // multi-GPU: boxes with a face on another GPU take the unfused pair,
+    // correct + fill (their faces travel), then the colour-1 substep; their
+    // same-GPU neighbours above pushed them the corrected colour 0 (push0)
+    {
+      Prof p(c, "prolong_fill", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl + 1);
+      launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
+                          F->d_sendbuf, true, !c->no_skip1, c->stream, F->d_bnd, F->n_bnd);
+    }
+    finish_halo(c, F, 1);
+    {
+      Prof p(c, "smoother_gsrb", 0.5 * F->n_bnd * F->nc * F->nc * F->nc, lvl + 1);
+      launch_gs_substep(F->view(), c->op, c->lambda, 1, 1 << 1, view_of(c, lvl), F->d_rb, F->has_rb,
+                        bc_for(c, lvl + 1, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd);
+    }
+    finish_halo(c, F, 1);
   }
   // colour-0 ghost halves hold pre-correction values, but the next substep
   // reads only colour 1 and pushes colour 0 itself
@@ -1113,7 +1133,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
-    dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int);
+    dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
@@ -1292,6 +1312,12 @@ void build_plan(omg_ctx* c) {
         L.n_int = (int)in.size();
         L.d_bnd = to_device(bnd);
         L.d_int = to_device(in);
+        std::vector<uint8_t> isb(L.n, 0), push0(L.n, 0);
+        for (int b : bnd) isb[b] = 1;
+        for (int b : in)
+          for (int nb = 0; nb < 6; nb++)
+            if (L.h_nbk[(size_t)b * 6 + nb] == NB_LOCAL && isb[L.h_nba[(size_t)b * 6 + nb]]) push0[b] |= 1u << nb;
+        L.d_push0 = to_device(push0);
       }
     }
     L.d_phi = L.d_data;
@@ -1369,10 +1395,14 @@ void build_plan(omg_ctx* c) {
     F.d_parent_local = to_device(F.parent_local);
     F.d_dix = to_device(F.dix_packed);
     // k_prolong_smooth needs, for every same-GPU fine face whose neighbour has
-    // another parent, that parent on this GPU as the coarse neighbour
+    // another parent, that parent on this GPU as the coarse neighbour (boxes
+    // with a face on another GPU are not fused)
     F.prolong_smooth_ok = F.n > 0 && F.n_pairs == F.n;
     const bool one_child = C.nc * 2 == F.nc;
     for (int b = 0; b < F.n && F.prolong_smooth_ok; b++) {
+      bool remote = false;
+      for (int nb = 0; nb < 6; nb++) remote |= F.h_nbk[(size_t)b * 6 + nb] == NB_REMOTE;
+      if (remote) continue;   // takes correct + fill + the substep (prolong_smooth())
       int d[3];
       T.child_offset(F.ids[b], d);
       for (int nb = 1; nb <= 6; nb++) {

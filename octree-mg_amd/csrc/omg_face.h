@@ -87,9 +87,11 @@ __device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc,
 // boundary cells of the colours in `colours` go to the neighbour's ghost
 // half, two consecutive slots of the half per thread as one 16-B store (the
 // half of colour e on the opposite face lists exactly our colour-e boundary
-// cells, in the same order).  get(i, j, k) reads our (final) interior value.
+// cells, in the same order).  get(i, j, k) reads our (final) interior value;
+// `faces` (bit f = face f+1) limits the push to some faces.
 template <int NC, class Get>
-__device__ __forceinline__ void face_push_local(const LevelView& L, int b, int colours, Get get) {
+__device__ __forceinline__ void face_push_local(const LevelView& L, int b, int colours, Get get,
+                                                unsigned faces = 0x3f) {
   using TL = Tl<NC>;
   constexpr int H = TL::H, PF = TL::FH / 2;   // 16-B pairs per face half
   const int ncol = (colours & 1) + ((colours >> 1) & 1);
@@ -98,7 +100,7 @@ __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int c
     const int f = p / (PF * ncol), rem = p % (PF * ncol);
     const int col = ncol == 2 ? rem / PF : c_first, r = rem % PF;
     const long long fidx = (long long)b * 6 + f;
-    if (L.nbk[fidx] != NB_LOCAL) continue;
+    if (L.nbk[fidx] != NB_LOCAL || !(faces >> f & 1)) continue;
     const int nb = f + 1;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, x1 = low ? 1 : NC;

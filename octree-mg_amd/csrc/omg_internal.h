@@ -134,6 +134,9 @@ struct Level {
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
   int* d_int = nullptr;
   int n_bnd = 0, n_int = 0;
+  // [n]: for a box without remote faces, the faces (bit f = face f+1) whose
+  // same-GPU neighbour has one (k_prolong_smooth pushes colour 0 there)
+  uint8_t* d_push0 = nullptr;
   double* d_rbsend = nullptr;
   double* d_rbrecv = nullptr;
   double* d_sendbuf = nullptr;

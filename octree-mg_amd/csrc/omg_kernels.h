@@ -112,11 +112,13 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 // red-black substep follows, so all-local boxes correct and push colour 0 only
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
-                         hipStream_t st);
+                         hipStream_t st, const int* list = nullptr, int n_list = 0);
 // correct_children + fill + the first up-smoothing substep (colour 1) in one
-// pass; every fine box with its parent here and no remote / refinement faces
+// pass; fine boxes with their parent here and no remote / refinement faces
+// (all, or the `list`); push0: per box, faces to push the corrected colour 0 to
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
-                           const int* dixp, const GcBC& bc, int one_child, hipStream_t st);
+                           const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
+                           const uint8_t* push0, hipStream_t st);
 // update_coarse's parent loop, LDS-tiled; false when the box size / operator
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,

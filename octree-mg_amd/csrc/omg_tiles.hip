@@ -26,6 +26,10 @@
 #ifndef OMG_SUMS_LPW
 #define OMG_SUMS_LPW 32
 #endif
+// rows of a box per chunk of the get_sum box sums
+#ifndef OMG_SUMS_R
+#define OMG_SUMS_R 4
+#endif
 
 namespace omg {
 
@@ -234,10 +238,10 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
 template <int NC, int BS, bool SUB>
 __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
                                                      const int* parent_local, const int* dixp, GcBC bc,
-                                                     double* sendbuf, int skip1) {
+                                                     double* sendbuf, int skip1, const int* list) {
   __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
-  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, xcd_box(blockIdx.x, gridDim.x), lds,
-                                skip1 != 0);
+  const int t = xcd_box(blockIdx.x, gridDim.x);
+  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, list ? list[t] : t, lds, skip1 != 0);
 }
 
 // correct_children + fill + the first up-smoothing substep in one pass
@@ -276,7 +280,7 @@ constexpr int prolong_smooth_lds() {
 template <int NC, int OP, int BS>
 __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const LevelView& F, double lambda,
                                                    const int* parent_local, const int* dixp, const GcBC& bc,
-                                                   int one_child, int b, double* lds) {
+                                                   int one_child, const uint8_t* push0, int b, double* lds) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, FH = TL::FH, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
   double* sb = lds;                     // both colours of the corrected interior (so | se of gsrb_box)
@@ -418,6 +422,11 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     gv[g] = gv[g] + (f0 + fx + fy + fz);
   }
   __syncthreads();
+  // next to boxes the caller runs unfused (multi-GPU: those with a face on
+  // another GPU, push0 = the faces toward them): they read our corrected
+  // colour 0 from their ghost halves
+  if (push0 && push0[b])
+    face_push_local<NC>(F, b, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; }, push0[b]);
   // ---- colour-0 ghost values the substep reads (physical faces from the
   // corrected boundary cells: bc_to_gc)
 #pragma unroll
@@ -456,21 +465,25 @@ template <int NC, int OP, int BS>
 // 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64
 __global__ void __launch_bounds__(BS, OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
-                                                       int one_child) {
+                                                       int one_child, const int* list, const uint8_t* push0) {
   __shared__ double lds[prolong_smooth_lds<NC>()];
-  prolong_smooth_box<NC, OP, BS>(Cv, F, lambda, parent_local, dixp, bc, one_child,
-                                 xcd_box(blockIdx.x, gridDim.x), lds);
+  const int t = xcd_box(blockIdx.x, gridDim.x);
+  prolong_smooth_box<NC, OP, BS>(Cv, F, lambda, parent_local, dixp, bc, one_child, push0, list ? list[t] : t, lds);
 }
 
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
-                           const int* dixp, const GcBC& bc, int one_child, hipStream_t st) {
-  if (F.n == 0) return;
-  const dim3 g(F.n);
+                           const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
+                           const uint8_t* push0, hipStream_t st) {
+  const int n = list ? n_list : F.n;
+  if (n == 0) return;
+  const dim3 g(n);
 #define OMG_PS(NC, BS)                                                                                \
   if (op == OP_HELM)                                                                                  \
-    k_prolong_smooth<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child); \
+    k_prolong_smooth<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child, \
+                                                        list, push0);                                 \
   else                                                                                                \
-    k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child);
+    k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
+                                                       list, push0);
   switch (F.nc) {
     case 16: OMG_PS(16, 512) break;
     case 8: OMG_PS(8, 256) break;
@@ -493,7 +506,7 @@ template <int NC, bool SUB, int LPW = OMG_SUMS_LPW>
 __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
                                                   int n_leaves, double* __restrict__ out,
                                                   const double* __restrict__ mean) {
-  constexpr int H = NC / 2, R = 4, SEG = R * H;   // doubles of one colour in a chunk
+  constexpr int H = NC / 2, R = OMG_SUMS_R < NC ? OMG_SUMS_R : NC, SEG = R * H;   // doubles of one colour in a chunk
   constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
   constexpr int PER = LPW * CH2 / 64;             // double2 per lane per chunk
   constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
@@ -641,14 +654,15 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
-                         hipStream_t st) {
-  if (F.n == 0) return;
-  const dim3 g(F.n);
-#define OMG_PF(NC, BS)                                                                                \
-  if (sub)                                                                                            \
-    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1); \
-  else                                                                                                \
-    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1);
+                         hipStream_t st, const int* list, int n_list) {
+  const int n = list ? n_list : F.n;
+  if (n == 0) return;
+  const dim3 g(n);
+#define OMG_PF(NC, BS)                                                                                      \
+  if (sub)                                                                                                  \
+    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list);  \
+  else                                                                                                      \
+    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list);
   switch (F.nc) {
     case 16: OMG_PF(16, 512) break;
     case 8: OMG_PF(8, 256) break;

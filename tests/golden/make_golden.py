@@ -37,6 +37,11 @@ CONFIGS = {
     # C3-like periodic GSRB (subtract_mean), rank counts pin the allreduce order
     "per32_gsrb_v": ("8 32 32 32 10 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 3, 4, 5, 6, 8]),
     "per32_gs_f": ("8 32 32 32 5 f gs lpl 0 per sol 1 lb 1", True, [1, 4]),
+    # multi-rank levels that also have boxes without a face on another rank
+    # (the fused prolongation + substep runs on those, the unfused pair on the
+    # others)
+    "per64_gsrb_v": ("8 64 64 64 4 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
+    "helm128_box16_d0": ("16 128 128 128 3 v gsrb helm 10 d0 sol 1 lb 1", True, [1, 2, 4]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),
