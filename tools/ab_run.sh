@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OP=${1:-vcycle}; REPS=${2:-5}
 R=$PWD
-for lib in default $(ls $R/octree-mg_amd/_variants/libomg_v*.so 2>/dev/null); do
+for lib in default $(ls $R/octree-mg_amd/_variants/libomg_*.so 2>/dev/null); do
   name=$(basename "$lib" .so)
   if [ "$lib" = default ]; then unset OMG_LIB; else export OMG_LIB=$lib; fi
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab/$name" -o run --output-format csv \
