@@ -903,7 +903,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
 int tail_top(omg_ctx* c, int max_lvl) {
   // (the variable-coefficient operators measured faster level by level:
   // their single-workgroup program spills heavily)
-  if (c->smoother != OMG_SMOOTHER_GSRB || (c->op != OP_LPL && c->op != OP_HELM)) return INT_MIN;
+  if (c->op != OP_LPL && c->op != OP_HELM) return INT_MIN;
   if (max_lvl - c->lowest + 1 > kTailMaxLevels) max_lvl = c->lowest + kTailMaxLevels - 1;
   int top = INT_MIN;
   for (int l = c->lowest; l <= max_lvl; l++) {
@@ -947,6 +947,7 @@ void run_tail(omg_ctx* c, int top) {
   A.res_rel = c->res_rel;
   A.maxbits = (unsigned long long*)c->d_scalar;
   A.coarse_its = (int*)(c->d_scalar + 1);
+  A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
   {
     Prof p(c, "coarse_tail", 0.0, top);
     launch_coarse_tail(A, c->op, c->stream);

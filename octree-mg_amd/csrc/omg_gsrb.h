@@ -294,4 +294,56 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   }
 }
 
+// Lexicographic Gauss-Seidel on one box with the box in LDS (the reference's
+// mg_smoother_gs, m_laplacian.f90:67-81): phi with its ghost faces and rhs are
+// read once, hyperplanes i+j+k = d run in increasing d on LDS (all updates of
+// a plane are independent and see planes < d updated, planes > d old: the
+// values the i-fastest loop nest reads), the interior is written back.
+template <int NC>
+constexpr int gs_lex_lds() { return (NC + 2) * (NC + 2) * (NC + 2) + NC * NC * NC; }
+
+template <int OP, int NC>
+__device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, int b, double* lds) {
+  constexpr int S = NC + 2, S3 = S * S * S, N3 = NC * NC * NC;
+  double* P = lds;         // phi(0:nc+1)^3, i fastest (edges and corners unused)
+  double* R = lds + S3;    // rhs(1:nc)^3
+  const OpCoef<OP> K(L, lambda);
+  double* u = boxp(L, 1, b);
+  const double* f = boxp(L, 2, b);
+  for (int q = threadIdx.x; q < S3; q += blockDim.x) {
+    const int i = q % S, j = (q / S) % S, k = q / (S * S);
+    const int nbd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
+    P[q] = nbd <= 1 ? u[off_cell(L, i, j, k)] : 0.0;
+  }
+  for (int q = threadIdx.x; q < N3; q += blockDim.x)
+    R[q] = f[off_int(L, q % NC + 1, (q / NC) % NC + 1, q / (NC * NC) + 1)];
+  __syncthreads();
+  for (int d = 3; d <= 3 * NC; d++) {
+    for (int p = threadIdx.x; p < NC * NC; p += blockDim.x) {
+      const int j = p % NC + 1, k = p / NC + 1, i = d - j - k;
+      if (i < 1 || i > NC) continue;
+      const int c = i + S * (j + S * k);
+      Nbr7 st;
+      st.c = P[c];
+      st.xm = P[c - 1];
+      st.xp = P[c + 1];
+      st.ym = P[c - S];
+      st.yp = P[c + S];
+      st.zm = P[c - S * S];
+      st.zp = P[c + S * S];
+      const double fv = R[(i - 1) + NC * ((j - 1) + NC * (k - 1))];
+      if constexpr (is_varop(OP))
+        P[c] = ags_value<OP>(K, st, load_eps<OP>(L, b, i, j, k), fv);
+      else
+        P[c] = gs_value<OP>(K, st, fv);
+    }
+    __syncthreads();
+  }
+  for (int q = threadIdx.x; q < N3; q += blockDim.x) {
+    const int i = q % NC + 1, j = (q / NC) % NC + 1, k = q / (NC * NC) + 1;
+    u[off_int(L, i, j, k)] = P[i + S * (j + S * k)];
+  }
+  __syncthreads();
+}
+
 }  // namespace omg

@@ -99,6 +99,7 @@ struct TailArgs {
   double res_abs, res_rel;
   unsigned long long* maxbits;   // device scratch
   int* coarse_its;               // device: sweeps the coarse solve took
+  int gs_lex;                    // smoother: lexicographic GS (else red-black)
 };
 void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st);
 

@@ -8,6 +8,7 @@
 // are cited as path:line of FermiQ/octree-mg.
 #include "omg_device.h"
 #include "omg_face.h"
+#include "omg_gsrb.h"
 #include "omg_kernels.h"
 
 namespace omg {
@@ -150,6 +151,13 @@ __global__ void __launch_bounds__(256) k_gs_lex(LevelView L, double lambda) {
       __syncthreads();
     }
   }
+}
+
+// The same sweep with the box in LDS (gs_lex_box, omg_gsrb.h): bit-identical.
+template <int OP, int NC>
+__global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) {
+  __shared__ double lds[gs_lex_lds<NC>()];
+  for (int b = blockIdx.x; b < L.n; b += gridDim.x) gs_lex_box<OP, NC>(L, lambda, b, lds);
 }
 
 template <int OP>
@@ -467,10 +475,30 @@ void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours
   OP_SWITCH(op, k_gs_sub, g, 256, st, L, lambda, e, colours, C, rb, bc, sendbuf);
 }
 
+template <int OP>
+static void gs_lex_lds(const LevelView& L, double lambda, unsigned g, int block, hipStream_t st) {
+  switch (L.nc) {
+    case 16: k_gs_lex_lds<OP, 16><<<g, block, 0, st>>>(L, lambda); break;
+    case 8: k_gs_lex_lds<OP, 8><<<g, block, 0, st>>>(L, lambda); break;
+    case 4: k_gs_lex_lds<OP, 4><<<g, block, 0, st>>>(L, lambda); break;
+    default: k_gs_lex_lds<OP, 2><<<g, block, 0, st>>>(L, lambda); break;
+  }
+}
+
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st) {
   if (L.n == 0) return;
   const unsigned g = (unsigned)std::min(L.n, 65535 * 8);
   const int block = L.nc * L.nc >= 256 ? 256 : ((L.nc * L.nc + 63) / 64) * 64;
+  if (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2) {
+    switch (op) {
+      case OP_HELM: gs_lex_lds<OP_HELM>(L, lambda, g, block, st); break;
+      case OP_AHELM: gs_lex_lds<OP_AHELM>(L, lambda, g, block, st); break;
+      case OP_VLPL: gs_lex_lds<OP_VLPL>(L, lambda, g, block, st); break;
+      case OP_VHELM: gs_lex_lds<OP_VHELM>(L, lambda, g, block, st); break;
+      default: gs_lex_lds<OP_LPL>(L, lambda, g, block, st); break;
+    }
+    return;
+  }
   OP_SWITCH(op, k_gs_lex, g, block, st, L, lambda);
 }
 

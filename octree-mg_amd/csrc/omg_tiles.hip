@@ -22,6 +22,10 @@
 #ifndef OMG_PS_PRE
 #define OMG_PS_PRE 0
 #endif
+// threads per 16^3 box
+#ifndef OMG_PS_BS16
+#define OMG_PS_BS16 512
+#endif
 // leaves per wave of the get_sum box sums (a wave per 64 threads)
 #ifndef OMG_SUMS_LPW
 #define OMG_SUMS_LPW 32
@@ -485,7 +489,7 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
     k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
                                                        list, push0);
   switch (F.nc) {
-    case 16: OMG_PS(16, 512) break;
+    case 16: OMG_PS(16, OMG_PS_BS16) break;
     case 8: OMG_PS(8, 256) break;
     case 4: OMG_PS(4, 256) break;
     default: OMG_PS(2, 256) break;
@@ -803,11 +807,33 @@ void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStr
 // ---------------------------------------------------------------------------
 // The coarse end of mg_fas_vcycle (m_multigrid.f90:185-229) in one workgroup.
 constexpr int kTailBS = 512;
-constexpr int kTailLds = Tl<16>::NST;   // the largest box program (16^3 residual / coarse rhs)
+// LDS of the largest box program: 16^3 residual / coarse rhs, and with LEX
+// (lexicographic GS) the 16^3 sweep
+template <bool LEX>
+constexpr int tail_lds() {
+  return LEX && gs_lex_lds<16>() > Tl<16>::NST ? gs_lex_lds<16>() : Tl<16>::NST;
+}
 
-template <int OP>
+__device__ void tail_fill(const TailArgs& A, int li);
+
+template <int OP, bool LEX>
 __device__ void tail_smooth(const TailArgs& A, int li, int n_cycle, double* lds) {
   const TailLevel& T = A.lv[li];
+  if constexpr (LEX) {
+    // smooth_boxes with mg_smoother_gs: a sweep of every box, then the fill
+    for (int n = 1; n <= n_cycle; n++) {
+      for (int b = 0; b < T.L.n; b++) {
+        switch (T.L.nc) {
+          case 16: gs_lex_box<OP, 16>(T.L, A.lambda, b, lds); break;
+          case 8: gs_lex_box<OP, 8>(T.L, A.lambda, b, lds); break;
+          case 4: gs_lex_box<OP, 4>(T.L, A.lambda, b, lds); break;
+          default: gs_lex_box<OP, 2>(T.L, A.lambda, b, lds); break;
+        }
+      }
+      tail_fill(A, li);
+    }
+    return;
+  }
   for (int n = 1; n <= 2 * n_cycle; n++) {
     const int e = n & 1;
     for (int b = 0; b < T.L.n; b++) {
@@ -892,12 +918,12 @@ __device__ void tail_correct(const TailArgs& A, int li, double* lds) {
   }
 }
 
-template <int OP>
+template <int OP, bool LEX>
 __global__ void __launch_bounds__(kTailBS) k_coarse_tail(TailArgs A) {
-  __shared__ double lds[kTailLds];
+  __shared__ double lds[tail_lds<LEX>()];
   const int top = A.n_lvls - 1;
   for (int li = top; li >= 1; li--) {
-    tail_smooth<OP>(A, li, A.n_down, lds);
+    tail_smooth<OP, LEX>(A, li, A.n_down, lds);
     tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
     tail_fill(A, li - 1);
     tail_coarse_rhs<OP>(A, li - 1, lds);
@@ -906,23 +932,30 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(TailArgs A) {
   const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
   int its = 0;
   for (int i = 1; i <= A.max_coarse; i++) {
-    tail_smooth<OP>(A, 0, A.n_up + A.n_down, lds);
+    tail_smooth<OP, LEX>(A, 0, A.n_up + A.n_down, lds);
     its = i;
     const double res = tail_residual<OP>(A, 0, 0, true, lds);
     if (res < A.res_rel * init_res || res < A.res_abs) break;
   }
   for (int li = 1; li <= top; li++) {
     tail_correct(A, li, lds);
-    tail_smooth<OP>(A, li, A.n_up, lds);
+    tail_smooth<OP, LEX>(A, li, A.n_up, lds);
   }
   if (threadIdx.x == 0) *A.coarse_its = its;
 }
 
 void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st) {
-  if (op == OP_HELM)
-    k_coarse_tail<OP_HELM><<<1, kTailBS, 0, st>>>(A);
-  else
-    k_coarse_tail<OP_LPL><<<1, kTailBS, 0, st>>>(A);
+  if (op == OP_HELM) {
+    if (A.gs_lex)
+      k_coarse_tail<OP_HELM, true><<<1, kTailBS, 0, st>>>(A);
+    else
+      k_coarse_tail<OP_HELM, false><<<1, kTailBS, 0, st>>>(A);
+  } else {
+    if (A.gs_lex)
+      k_coarse_tail<OP_LPL, true><<<1, kTailBS, 0, st>>>(A);
+    else
+      k_coarse_tail<OP_LPL, false><<<1, kTailBS, 0, st>>>(A);
+  }
 }
 
 }  // namespace omg
