@@ -923,7 +923,8 @@ int tail_top(omg_ctx* c, int max_lvl) {
 // Levels lowest..top of the V-cycle (down-smoothing of top .. up-smoothing of
 // top) in one launch, bit-identical to the level-by-level path.
 void run_tail(omg_ctx* c, int top) {
-  TailArgs A{};
+  TailArgs A;
+  std::memset(&A, 0, sizeof(A));   // padding too: compared bytewise below
   A.n_lvls = top - c->lowest + 1;
   for (int l = c->lowest; l <= top; l++) {
     Level* L = level_ptr(c, l);
@@ -948,9 +949,19 @@ void run_tail(omg_ctx* c, int top) {
   A.maxbits = (unsigned long long*)c->d_scalar;
   A.coarse_its = (int*)(c->d_scalar + 1);
   A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
+  if (!c->d_tail) {
+    HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
+    c->h_tail = new TailArgs;
+    std::memset(c->h_tail, 0xff, sizeof(TailArgs));
+  }
+  if (std::memcmp(&A, c->h_tail, sizeof(TailArgs)) != 0) {
+    *c->h_tail = A;
+    // pageable source: the copy is staged before the call returns
+    HIPCHK(hipMemcpyAsync(c->d_tail, c->h_tail, sizeof(TailArgs), hipMemcpyHostToDevice, c->stream));
+  }
   {
     Prof p(c, "coarse_tail", 0.0, top);
-    launch_coarse_tail(A, c->op, c->stream);
+    launch_coarse_tail(c->d_tail, A.gs_lex, c->op, c->stream);
   }
   for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
 }
@@ -1555,6 +1566,8 @@ int omg_ctx_destroy(omg_ctx* c) {
     (void)hipStreamSynchronize(c->stream_comm);
     free_levels(c);
     dfree(c->d_scalar);
+    if (c->d_tail) (void)hipFree(c->d_tail);
+    delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_stage);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);

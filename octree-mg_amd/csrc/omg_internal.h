@@ -183,6 +183,10 @@ struct KStat {
 
 struct omg_loop;   // in-process loopback transport (omg_api.cpp)
 
+namespace omg {
+struct TailArgs;   // omg_kernels.h
+}
+
 struct omg_ctx {
   int device = 0, rank = 0, n_ranks = 1;
   bool host_only = false;                   // plan-only context (OMG_DEVICE_NONE)
@@ -225,6 +229,11 @@ struct omg_ctx {
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch
+  // arguments of the coarse-tail kernel in device memory (a by-value kernel
+  // argument indexed by level is copied to scratch per lane); uploaded when
+  // they change
+  omg::TailArgs* d_tail = nullptr;
+  omg::TailArgs* h_tail = nullptr;   // the last uploaded copy (host)
   double* h_scalar = nullptr;          // pinned host scratch
   double* d_stage = nullptr;           // upload/download staging (reference layout)
   size_t stage_n = 0;

@@ -101,7 +101,7 @@ struct TailArgs {
   int* coarse_its;               // device: sweeps the coarse solve took
   int gs_lex;                    // smoother: lexicographic GS (else red-black)
 };
-void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st);
+void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 
 // LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16
 bool tiled_nc(int nc);

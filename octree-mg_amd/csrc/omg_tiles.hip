@@ -919,8 +919,9 @@ __device__ void tail_correct(const TailArgs& A, int li, double* lds) {
 }
 
 template <int OP, bool LEX>
-__global__ void __launch_bounds__(kTailBS) k_coarse_tail(TailArgs A) {
+__global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restrict__ dA) {
   __shared__ double lds[tail_lds<LEX>()];
+  const TailArgs& A = *dA;
   const int top = A.n_lvls - 1;
   for (int li = top; li >= 1; li--) {
     tail_smooth<OP, LEX>(A, li, A.n_down, lds);
@@ -944,17 +945,17 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(TailArgs A) {
   if (threadIdx.x == 0) *A.coarse_its = its;
 }
 
-void launch_coarse_tail(const TailArgs& A, int op, hipStream_t st) {
+void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st) {
   if (op == OP_HELM) {
-    if (A.gs_lex)
-      k_coarse_tail<OP_HELM, true><<<1, kTailBS, 0, st>>>(A);
+    if (gs_lex)
+      k_coarse_tail<OP_HELM, true><<<1, kTailBS, 0, st>>>(dA);
     else
-      k_coarse_tail<OP_HELM, false><<<1, kTailBS, 0, st>>>(A);
+      k_coarse_tail<OP_HELM, false><<<1, kTailBS, 0, st>>>(dA);
   } else {
-    if (A.gs_lex)
-      k_coarse_tail<OP_LPL, true><<<1, kTailBS, 0, st>>>(A);
+    if (gs_lex)
+      k_coarse_tail<OP_LPL, true><<<1, kTailBS, 0, st>>>(dA);
     else
-      k_coarse_tail<OP_LPL, false><<<1, kTailBS, 0, st>>>(A);
+      k_coarse_tail<OP_LPL, false><<<1, kTailBS, 0, st>>>(dA);
   }
 }
 
