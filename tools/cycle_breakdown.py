@@ -10,7 +10,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    marker = sys.argv[2] if len(sys.argv) > 2 else "k_box_sums3<16, true>"
+    marker = sys.argv[2] if len(sys.argv) > 2 else "k_box_sums3<16, true"
     back = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
