@@ -414,8 +414,10 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (iv == 1) L->phi_gc_ok = true;
   if (L->n) {
     Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc, lvl);
-    launch_fill_gc(L->view(), iv, 3, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_sendbuf,
-                   c->stream);
+    if (iv != 1 || L->has_rb || c->no_fill_tile ||
+        !launch_fill_tile(L->view(), bc_for(c, lvl, iv), L->d_sendbuf, c->stream))
+      launch_fill_gc(L->view(), iv, 3, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_sendbuf,
+                     c->stream);
   }
   finish_halo(c, L, iv);
 }
@@ -1510,6 +1512,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
     c->no_fuse_up = getenv("OMG_NO_FUSE_UP") != nullptr;
     c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
+    c->no_fill_tile = getenv("OMG_NO_FILL_TILE") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));

@@ -105,6 +105,9 @@ void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);
 
 // LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16
 bool tiled_nc(int nc);
+// the ghost fill of phi for a level without refinement boundaries, box sizes
+// 4, 8, 16 (false: use launch_fill_gc)
+bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st);

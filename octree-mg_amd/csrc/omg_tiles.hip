@@ -636,6 +636,33 @@ __global__ void __launch_bounds__(64) k_seq_sum3(const double* __restrict__ box_
   if (lane == 0) *acc = a;
 }
 
+// mg_fill_ghost_cells_lvl of phi (m_ghost_cells.f90:131-175) for a level
+// without refinement boundaries: the box's interior is read once, whole and
+// coalesced, into LDS, then tile_face_fill pushes its boundary cells to the
+// same-GPU neighbours as 16-B pairs, packs remote faces and forms physical
+// ghosts (k_fill_gc reads and writes every face cell with its own 8-B access).
+template <int NC, int BS>
+__global__ void __launch_bounds__(BS) k_fill_tile(LevelView L, GcBC bc, double* sendbuf) {
+  constexpr int HV = Tl<NC>::HV;
+  __shared__ double sb[2 * HV];
+  const int b = xcd_box(blockIdx.x, gridDim.x);
+  const double* u = L.phi + (long long)b * L.stride;
+  for (int q = threadIdx.x; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
+  __syncthreads();
+  tile_face_fill<NC>(L, b, sb, 3, bc, sendbuf);
+}
+
+bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipStream_t st) {
+  if (L.n == 0) return true;
+  const dim3 g(L.n);
+  switch (L.nc) {
+    case 16: k_fill_tile<16, 512><<<g, 512, 0, st>>>(L, bc, sendbuf); return true;
+    case 8: k_fill_tile<8, 256><<<g, 256, 0, st>>>(L, bc, sendbuf); return true;
+    case 4: k_fill_tile<4, 64><<<g, 64, 0, st>>>(L, bc, sendbuf); return true;
+    default: return false;
+  }
+}
+
 bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }
 
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
