@@ -739,13 +739,15 @@ void leaf_box_sums(omg_ctx* c, int iv, int ch, hipStream_t st) {
 
 void leaf_chain(omg_ctx* c, int ch, hipStream_t st) {
   double* acc = red_acc(c, ch);
-  HIPCHK(hipMemsetAsync(acc, 0, 8, st));
+  bool first = true;   // get_sum = 0 (:283): the first chain starts from +0.0 itself
   for (int l = 1; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     Prof p(c, "seq_sum", (double)L->leaves.size(), l);
-    launch_seq_sum(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, st);
+    launch_seq_sum(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, first, st);
+    first = false;
   }
+  if (first) HIPCHK(hipMemsetAsync(acc, 0, 8, st));
 }
 
 void leaf_sum_device(omg_ctx* c, int iv, int ch) {

@@ -132,6 +132,7 @@ bool subtract_sums_nc(int nc);
 void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
                           hipStream_t st);
 void launch_mean(const double* all, int n, double volume, double* mean, hipStream_t st);
-void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st);
+// init: start from +0.0 instead of *acc
+void launch_seq_sum(const double* box_sums, int n, double w, double* acc, bool init, hipStream_t st);
 
 }  // namespace omg

@@ -591,11 +591,11 @@ __global__ void __launch_bounds__(64) k_box_sums_any(LevelView L, int iv, const 
 // stage in flight in registers), every lane runs the same add chain reading
 // LDS a group ahead, and the products are formed off the chain.
 __global__ void __launch_bounds__(64) k_seq_sum3(const double* __restrict__ box_sums, int n, double w,
-                                                 double* __restrict__ acc) {
+                                                 double* __restrict__ acc, int init) {
   constexpr int CH = 1024, PL = CH / 128, G = 16;
   __shared__ double st[CH];
   const int lane = threadIdx.x;
-  double a = *acc;
+  double a = init ? 0.0 : *acc;
   double2 pre[PL];
   auto fetch = [&](int base) {
 #pragma unroll
@@ -814,8 +814,8 @@ void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, 
 // m_multigrid.f90:255-262): the per-rank sums combined in MPICH's one-node
 // binomial order, ((a0+a1)+(a2+a3))+..., then the division.
 __global__ void k_mean(const double* all, int n, double volume, double* mean) {
+  __shared__ double t[64];   // (a per-lane array indexed by r would live in scratch)
   if (threadIdx.x || blockIdx.x) return;
-  double t[64];
   for (int r = 0; r < n; r++) t[r] = all[r];
   for (int w = 1; w < n; w *= 2)
     for (int r = 0; r + w < n; r += 2 * w) t[r] = t[r] + t[r + w];
@@ -826,9 +826,9 @@ void launch_mean(const double* all, int n, double volume, double* mean, hipStrea
   k_mean<<<1, 64, 0, st>>>(all, n, volume, mean);
 }
 
-void launch_seq_sum(const double* box_sums, int n, double w, double* acc, hipStream_t st) {
+void launch_seq_sum(const double* box_sums, int n, double w, double* acc, bool init, hipStream_t st) {
   if (n == 0) return;
-  k_seq_sum3<<<1, 64, 0, st>>>(box_sums, n, w, acc);
+  k_seq_sum3<<<1, 64, 0, st>>>(box_sums, n, w, acc, init);
 }
 
 // ---------------------------------------------------------------------------
