@@ -34,6 +34,17 @@
 #ifndef OMG_SUMS_R
 #define OMG_SUMS_R 4
 #endif
+// non-temporal loads in the get_sum box sums; loads / stores of the fused
+// rhs subtract
+#ifndef OMG_SUMS_NT
+#define OMG_SUMS_NT 1
+#endif
+#ifndef OMG_SUB_NT_LD
+#define OMG_SUB_NT_LD 0
+#endif
+#ifndef OMG_SUB_NT_ST
+#define OMG_SUB_NT_ST 0
+#endif
 
 namespace omg {
 
@@ -506,11 +517,29 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
 // SUB: subtract_mean fused in front (m_multigrid.f90:268-272, no ghosts): every
 // value is replaced by v - mean in HBM and the box sums are those of the new
 // values (what the next get_sum of this variable will need).
+// NT: non-temporal streams (the level is read once per pass)
+template <bool NT>
+__device__ __forceinline__ double2 sums_ld(const double* p) {
+  if (NT) {
+    const v2d t = ld_nt(p);
+    return make_double2(t.x, t.y);
+  }
+  return *reinterpret_cast<const double2*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void sums_st(double* p, double2 v) {
+  if (NT)
+    st_nt(p, v.x, v.y);
+  else
+    *reinterpret_cast<double2*>(p) = v;
+}
+
 template <int NC, bool SUB, int LPW = OMG_SUMS_LPW>
 __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
                                                   int n_leaves, double* __restrict__ out,
                                                   const double* __restrict__ mean) {
   constexpr int H = NC / 2, R = OMG_SUMS_R < NC ? OMG_SUMS_R : NC, SEG = R * H;   // doubles of one colour in a chunk
+  constexpr bool NTL = SUB ? OMG_SUB_NT_LD : OMG_SUMS_NT;
   constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
   constexpr int PER = LPW * CH2 / 64;             // double2 per lane per chunk
   constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
@@ -532,7 +561,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
   const double m = SUB ? *mean : 0.0;
   double2 v[PER];
 #pragma unroll
-  for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r]);
+  for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r]);
   double acc = 0.0;
   const double* my = lds + lane * P;
   for (int c = 0; c < NCH; c++) {
@@ -543,7 +572,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
       if (SUB) {
         v[r].x = v[r].x - m;
         v[r].y = v[r].y - m;
-        if (own[r]) *reinterpret_cast<double2*>(src[r] + rc) = v[r];
+        if (own[r]) sums_st<OMG_SUB_NT_ST>(src[r] + rc, v[r]);
       }
       lds[dst[r]] = v[r].x;
       lds[dst[r] + 1] = v[r].y;
@@ -554,7 +583,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
       const int k1 = (c + 1) / (NC / R) + 1, j1 = ((c + 1) % (NC / R)) * R + 1;
       const int r1 = H * ((j1 - 1) + NC * (k1 - 1));
 #pragma unroll
-      for (int r = 0; r < PER; r++) v[r] = *reinterpret_cast<const double2*>(src[r] + r1);
+      for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r] + r1);
     }
     if (lane < LPW) {
 #pragma unroll
