@@ -735,7 +735,9 @@ void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const i
 // update_coarse's parent loop (m_multigrid.f90:364-383) for one parent box
 // per workgroup: rhs = L(phi) + res over the interior (box_op, then the sum),
 // old = phi over the whole stored box.
-template <int NC, int OP, int BS>
+// NT: non-temporal streams (a whole level per launch; the coarse tail's
+// levels are re-read right away and keep the default policy)
+template <int NC, int OP, int BS, bool NT = false>
 __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambda, int b, double* sb) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, H = NC / 2;
@@ -747,15 +749,18 @@ __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambd
   double* __restrict__ old = Cv.data + 2 * Cv.vstride + boff;
   const double* __restrict__ res = Cv.data + 3 * Cv.vstride + boff;
   for (int q = tid; q < NST / 2; q += BS) {
-    const v2d x = reinterpret_cast<const v2d*>(u)[q];
+    const v2d x = NT ? ld_nt(u + 2 * q) : reinterpret_cast<const v2d*>(u)[q];
     reinterpret_cast<v2d*>(sb)[q] = x;
-    reinterpret_cast<v2d*>(old)[q] = x;
+    if (NT)
+      st_nt(old + 2 * q, x.x, x.y);
+    else
+      reinterpret_cast<v2d*>(old)[q] = x;
   }
   v2d rr[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < HV) rr[r] = reinterpret_cast<const v2d*>(res)[q2];
+    if (q2 < HV) rr[r] = NT ? ld_nt(res + 2 * q2) : reinterpret_cast<const v2d*>(res)[q2];
   }
   __syncthreads();
   const OpCoef<OP> K(Cv, lambda);
@@ -786,14 +791,17 @@ __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambd
     v2d out;
     out.x = l0 + rr[r].x;
     out.y = l1 + rr[r].y;
-    reinterpret_cast<v2d*>(rhs)[q2] = out;
+    if (NT)
+      st_nt(rhs + 2 * q2, out.x, out.y);
+    else
+      reinterpret_cast<v2d*>(rhs)[q2] = out;
   }
 }
 
 template <int NC, int OP, int BS>
 __global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
   __shared__ double sb[Tl<NC>::NST];
-  coarse_rhs_box<NC, OP, BS>(Cv, lambda, parents[xcd_box(blockIdx.x, gridDim.x)], sb);
+  coarse_rhs_box<NC, OP, BS, true>(Cv, lambda, parents[xcd_box(blockIdx.x, gridDim.x)], sb);
 }
 
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
