@@ -7,6 +7,9 @@
 namespace omg {
 
 typedef double v2d __attribute__((ext_vector_type(2)));
+// pointer types of __builtin_amdgcn_global_load_lds (LDS-DMA)
+typedef __attribute__((address_space(1))) void glb_void;
+typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ v2d ld_nt(const double* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));

@@ -22,6 +22,10 @@
 #ifndef OMG_PS_PRE
 #define OMG_PS_PRE 0
 #endif
+// old ghost values by LDS-DMA (boxes without a physical face)
+#ifndef OMG_PS_OGLDS
+#define OMG_PS_OGLDS 1
+#endif
 // threads per 16^3 box
 #ifndef OMG_PS_BS16
 #define OMG_PS_BS16 512
@@ -326,11 +330,21 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   GsrbRhs<NC, BS> pre;
   gsrb_load_rhs<NC, BS, 2>(F, 1, b, pre);
 #endif
+  // The old values in our colour-0 ghost halves (og below) go by LDS-DMA into
+  // the colour-1 half of the tile, unused until the substep in a box without
+  // a physical face: no registers held across the parent's loads.
+  const bool og_lds = OMG_PS_OGLDS && !phys && 6 * FH <= HV;   // fits the colour-1 half (NC >= 8)
+  if (og_lds && tid < 3 * FH) {   // 16-B chunks of the six face halves
+    const int q = 2 * tid;
+    __builtin_amdgcn_global_load_lds((glb_void*)(u + 2 * HV + (q / FH) * TL::FS + q % FH),
+                                     (lds_void*)(sb + HV + 2 * (tid & ~63)), 16, 0, 0);
+  }
   // ---- colour-0 ghost values from same-GPU neighbours: the neighbour's
   // old boundary value (still in our ghost slot) + its prolongation
   constexpr int NG = (6 * FH + BS - 1) / BS;
   double gv[NG], rva[NG], rvc[NG];
   unsigned defm = 0, rima = 0, rimc = 0;   // from the tile after it is loaded; rim taps
+  unsigned ocm = 0;                        // one_child faces: og added after the barrier
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     const int q = tid + BS * g;
@@ -349,7 +363,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     if (d == 1) { fi = xn; fj = a; fk = c; }
     else if (d == 2) { fi = a; fj = xn; fk = c; }
     else { fi = a; fj = c; fk = xn; }
-    const double og = u[TL::ogh(nb, a, c)];
+    const double og = og_lds ? 0.0 : u[TL::ogh(nb, a, c)];
     if (!one_child) {
       // From the tile once it is loaded: a sibling's cells are the parent's
       // own; a neighbour parent's boundary layer is our parent's ghost layer
@@ -382,7 +396,12 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     int nd[3] = {dix[0], dix[1], dix[2]};
     const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
     nd[d - 1] = 0;
-    gv[g] = og + prolong_at<NC>(Cv, pn, nd, fi, fj, fk);
+    if (og_lds) {
+      gv[g] = prolong_at<NC>(Cv, pn, nd, fi, fj, fk);
+      ocm |= 1u << g;
+    } else {
+      gv[g] = og + prolong_at<NC>(Cv, pn, nd, fi, fj, fk);
+    }
   }
   // ---- parent's res = phi - old on its octant + face layer (stored by owner)
   load_parent_octant<NC, BS, true, true>(Cv, 4, pb, dix[0], dix[1], dix[2], cb);
@@ -434,8 +453,11 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     const double fx = 0.25 * (d == 1 ? tn : ta);
     const double fy = 0.25 * (d == 1 ? ta : (d == 2 ? tn : tc));
     const double fz = 0.25 * (d == 3 ? tn : tc);
-    gv[g] = gv[g] + (f0 + fx + fy + fz);
+    gv[g] = (og_lds ? sb[HV + q] : gv[g]) + (f0 + fx + fy + fz);
   }
+#pragma unroll
+  for (int g = 0; g < NG; g++)
+    if (ocm >> g & 1) gv[g] = sb[HV + tid + BS * g] + gv[g];
   __syncthreads();
   // next to boxes the caller runs unfused (multi-GPU: those with a face on
   // another GPU, push0 = the faces toward them): they read our corrected
