@@ -953,6 +953,11 @@ void run_tail(omg_ctx* c, int top) {
   A.maxbits = (unsigned long long*)c->d_scalar;
   A.coarse_its = (int*)(c->d_scalar + 1);
   A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
+  const bool tail_timing = c->tail_timing;
+  if (tail_timing) {
+    if (!c->d_tail_stamps) HIPCHK(hipMalloc(&c->d_tail_stamps, 8 * 64));
+    A.stamps = c->d_tail_stamps;
+  }
   if (!c->d_tail) {
     HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
     c->h_tail = new TailArgs;
@@ -966,6 +971,15 @@ void run_tail(omg_ctx* c, int top) {
   {
     Prof p(c, "coarse_tail", 0.0, top);
     launch_coarse_tail(c->d_tail, A.gs_lex, c->op, c->stream);
+  }
+  if (tail_timing) {   // diagnostics: phase times of the tail (100 MHz wall clock)
+    long long h[64];
+    HIPCHK(hipMemcpyAsync(h, c->d_tail_stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int n = 4 * (A.n_lvls - 1) + 2 + 2 * (A.n_lvls - 1);
+    std::fprintf(stderr, "tail us:");
+    for (int i = 1; i < n; i++) std::fprintf(stderr, " %.1f", (h[i] - h[i - 1]) * 0.01);
+    std::fprintf(stderr, "\n");
   }
   for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
 }
@@ -1514,6 +1528,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
     c->no_fuse_up = getenv("OMG_NO_FUSE_UP") != nullptr;
     c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
+    c->tail_timing = getenv("OMG_TAIL_TIMING") != nullptr;
     c->no_fill_tile = getenv("OMG_NO_FILL_TILE") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1572,6 +1587,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     free_levels(c);
     dfree(c->d_scalar);
     if (c->d_tail) (void)hipFree(c->d_tail);
+    if (c->d_tail_stamps) (void)hipFree(c->d_tail_stamps);
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_stage);

@@ -235,6 +235,8 @@ struct omg_ctx {
   // they change
   omg::TailArgs* d_tail = nullptr;
   omg::TailArgs* h_tail = nullptr;   // the last uploaded copy (host)
+  bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
+  long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch
   double* d_stage = nullptr;           // upload/download staging (reference layout)
   size_t stage_n = 0;

@@ -100,6 +100,7 @@ struct TailArgs {
   unsigned long long* maxbits;   // device scratch
   int* coarse_its;               // device: sweeps the coarse solve took
   int gs_lex;                    // smoother: lexicographic GS (else red-black)
+  long long* stamps;             // OMG_TAIL_TIMING: wall clock per phase (thread 0), or null
 };
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 

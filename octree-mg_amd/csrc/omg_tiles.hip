@@ -1009,11 +1009,21 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
   __shared__ double lds[tail_lds<LEX>()];
   const TailArgs& A = *dA;
   const int top = A.n_lvls - 1;
+  int ns = 0;
+  auto stamp = [&]() {
+    if (A.stamps && threadIdx.x == 0) A.stamps[ns] = (long long)wall_clock64();
+    ns++;
+  };
+  stamp();
   for (int li = top; li >= 1; li--) {
     tail_smooth<OP, LEX>(A, li, A.n_down, lds);
+    stamp();
     tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
+    stamp();
     tail_fill(A, li - 1);
+    stamp();
     tail_coarse_rhs<OP>(A, li - 1, lds);
+    stamp();
   }
   // coarse solve (m_multigrid.f90:197-208)
   const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
@@ -1024,9 +1034,12 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
     const double res = tail_residual<OP>(A, 0, 0, true, lds);
     if (res < A.res_rel * init_res || res < A.res_abs) break;
   }
+  stamp();
   for (int li = 1; li <= top; li++) {
     tail_correct(A, li, lds);
+    stamp();
     tail_smooth<OP, LEX>(A, li, A.n_up, lds);
+    stamp();
   }
   if (threadIdx.x == 0) *A.coarse_its = its;
 }
