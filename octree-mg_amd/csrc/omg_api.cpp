@@ -428,14 +428,14 @@ double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
 
 // smooth_boxes (m_multigrid.f90:404-424)
-void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1) {
+void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0) {
   Level* L = level_ptr(c, lvl);
-  const int n_sub = n_cycle * c->n_substeps;
+  const int n_sub = n_cycle * c->n_substeps - skip_last;
   if (!L) return;
   // a pending phi shift is subtracted by the first tiled substep while it
   // loads (the values it reads are dead afterwards); otherwise applied now
   // (not next to refinement boundaries: their ghosts read the coarse level)
-  const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 2 && L->phi_gc_ok &&
+  const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 1 && L->phi_gc_ok &&
                       !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
@@ -567,8 +567,21 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
   }
 }
 
-// update_coarse (m_multigrid.f90:347-384)
-void update_coarse(omg_ctx* c, int lvl) {
+// Whether the down-smoothing of level lvl can end in k_smooth_resid (its last
+// substep fused with update_coarse's residual + restriction): red-black with
+// an even substep count, Laplacian / Helmholtz, 16^3 or 8^3 boxes, every face
+// a same-GPU box (the recomputed ghosts read the neighbour directly).
+bool smooth_resid_ok(omg_ctx* c, int lvl) {
+  const Level* F = level_ptr(c, lvl);
+  const Level* C = level_ptr(c, lvl - 1);
+  return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_down >= 1 &&
+         (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) && !F->has_rb &&
+         !F->has_remote && !F->has_phys;
+}
+
+// update_coarse (m_multigrid.f90:347-384); fused: the level's last down
+// substep is still to do (smooth_resid_ok), k_smooth_resid runs it
+void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
   Level* F = level_ptr(c, lvl);
   if (Level* Cl = level_ptr(c, lvl - 1)) {
     // restriction overwrites every box of an all-parents level (interior), and
@@ -579,7 +592,12 @@ void update_coarse(omg_ctx* c, int lvl) {
   if (F && F->n && tiled_level(c, F)) {
     // residual + restriction of phi and res in one pass (omg_tiles.hip)
     phi_dirty(c, lvl - 1);
-    {
+    if (fused) {
+      Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
+      if (!launch_smooth_resid(F->view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
+                               F->d_dix, c->stream))
+        throw OmgError("smooth_resid: not available for this level");
+    } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
       launch_resid_restrict(F->view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
                             F->d_dix, c->stream);
@@ -1016,8 +1034,9 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   const bool tail = top >= min_lvl && !c->no_tail;
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
-    smooth_boxes(c, l, c->n_cycle_down);
-    update_coarse(c, l);
+    const bool fused = smooth_resid_ok(c, l);
+    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
+    update_coarse(c, l, fused);
   }
   if (tail) {
     run_tail(c, top);
@@ -1530,6 +1549,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
     c->tail_timing = getenv("OMG_TAIL_TIMING") != nullptr;
     c->no_fill_tile = getenv("OMG_NO_FILL_TILE") != nullptr;
+    c->no_fuse_down = getenv("OMG_NO_FUSE_DOWN") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));

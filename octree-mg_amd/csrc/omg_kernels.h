@@ -109,6 +109,10 @@ bool tiled_nc(int nc);
 // the ghost fill of phi for a level without refinement boundaries, box sizes
 // 4, 8, 16 (false: use launch_fill_gc)
 bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipStream_t st);
+// the last down-smoothing substep (colour 0) + residual + restriction in one
+// pass (k_smooth_resid); false: not available for this op / box size
+bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
+                         const int* parent_local, const int* dixp, hipStream_t st);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st);

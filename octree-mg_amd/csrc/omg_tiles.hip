@@ -53,16 +53,21 @@
 namespace omg {
 
 template <int NC, int OP, int BS>
+__device__ __forceinline__ void resid_restrict_core(const LevelView& F, const LevelView& Cv, double lambda,
+                                                    unsigned long long* maxbits, int restrict_on,
+                                                    const int* parent_local, const int* dixp, int b, double* sb,
+                                                    const v2d* fr);
+
+template <int NC, int OP, int BS>
 __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const LevelView& Cv, double lambda,
                                                    unsigned long long* maxbits, int restrict_on,
                                                    const int* parent_local, const int* dixp, int b, double* sb) {
   using TL = Tl<NC>;
-  constexpr int NST = TL::NST, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, HN = NC / 2;
+  constexpr int NST = TL::NST, HV = TL::HV, NR = (HV + BS - 1) / BS;
   const int tid = threadIdx.x;
   const long long boff = (long long)b * F.stride;
   const double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
-  double* __restrict__ res = F.data + 3 * F.vstride + boff;
   for (int q = tid; q < NST / 2; q += BS) reinterpret_cast<v2d*>(sb)[q] = ld_nt(u + 2 * q);
   v2d fr[NR];
 #pragma unroll
@@ -71,6 +76,20 @@ __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const Lev
     if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
   }
   __syncthreads();
+  resid_restrict_core<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp, b, sb, fr);
+}
+
+// The residual and the restriction of box b from its tile in LDS (phi with
+// its ghost faces, Tl<NC> layout) and rhs in registers (pairs q2 = tid + BS*r).
+template <int NC, int OP, int BS>
+__device__ __forceinline__ void resid_restrict_core(const LevelView& F, const LevelView& Cv, double lambda,
+                                                    unsigned long long* maxbits, int restrict_on,
+                                                    const int* parent_local, const int* dixp, int b, double* sb,
+                                                    const v2d* fr) {
+  using TL = Tl<NC>;
+  constexpr int HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS, HN = NC / 2;
+  const int tid = threadIdx.x;
+  double* __restrict__ res = F.data + 3 * F.vstride + (long long)b * F.stride;
 
   // residual_box (m_multigrid.f90:426-436) with box_lpl / box_helmh, two
   // same-colour cells per thread and step (pair q2: colour q2 / (HV/2))
@@ -149,6 +168,128 @@ __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv
   __shared__ double sb[Tl<NC>::NST];
   resid_restrict_box<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp,
                                  xcd_box(blockIdx.x, gridDim.x), sb);
+}
+
+// Tile offset of the cell at layer v along axis d and tangential (a, c)
+// (the two other axes in increasing order)
+template <int NC>
+__device__ __forceinline__ int sr_int(int d, int v, int a, int c) {
+  return d == 0 ? Tl<NC>::oint(v, a, c) : (d == 1 ? Tl<NC>::oint(a, v, c) : Tl<NC>::oint(a, c, v));
+}
+// Tile offset of the ghost of the neighbour cell (layer nl along d, (a, c))
+// past tangential axis t (0: a's axis, 1: c's axis), on the low side if lo
+template <int NC>
+__device__ __forceinline__ int sr_edge(int d, int t, bool lo, int nl, int a, int c) {
+  const int t1 = d == 0 ? 1 : 0, t2 = d == 2 ? 1 : 2, ax = t == 0 ? t1 : t2;
+  const int fn = 2 * ax + (lo ? 1 : 2);
+  // (i, j, k) of the cell, then its coordinates on face fn
+  const int i = d == 0 ? nl : a, j = d == 1 ? nl : (d == 0 ? a : c), k = d == 2 ? nl : c;
+  return ax == 0 ? Tl<NC>::ogh(fn, j, k) : (ax == 1 ? Tl<NC>::ogh(fn, i, k) : Tl<NC>::ogh(fn, i, j));
+}
+
+// The last down-smoothing substep of a level fused with update_coarse's
+// residual + restriction (k_smooth_resid).  The substep updates colour 0
+// from colour 1, which it does not change, so the colour-0 ghost values the
+// residual needs (the neighbours' new boundary cells) are recomputed here from
+// colour-1 data that is final: our boundary layer, the neighbour's second
+// layer, the neighbour's rhs and, at face edges, the neighbour's own ghosts.
+// Same operands, same gs_value: bit-identical to the neighbour's own update.
+// Levels whose faces are all same-GPU boxes, Laplacian / Helmholtz, NC 16/8.
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, double lambda, int restrict_on,
+                                                     const int* parent_local, const int* dixp) {
+  using TL = Tl<NC>;
+  constexpr int H = NC / 2, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS;
+  constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
+  __shared__ double sb[TL::NST];
+  const int tid = threadIdx.x, b = xcd_box(blockIdx.x, gridDim.x);
+  const long long boff = (long long)b * F.stride;
+  double* __restrict__ u = F.phi + boff;
+  const double* __restrict__ f = F.data + F.vstride + boff;
+  // colour 1 and the colour-1 halves of the ghost faces
+  for (int q = tid; q < HV / 2; q += BS)
+    reinterpret_cast<v2d*>(sb + HV)[q] = ld_nt(u + HV + 2 * q);
+  for (int q = tid; q < 3 * FH; q += BS) {
+    const int nb = q / (FH / 2), r = q % (FH / 2);
+    reinterpret_cast<v2d*>(sb + 2 * HV + nb * FS + FH)[r] = ld_nt(u + 2 * HV + nb * FS + FH + 2 * r);
+  }
+  v2d fr[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
+  }
+  // the neighbour-side operands of our colour-0 ghost cells: N's cell X at
+  // (layer nl, a, c) has neighbours deep (N's second layer), across (our
+  // boundary layer, LDS), and tangentially N's boundary cells (our colour-1
+  // ghosts, LDS) or, past the face edge, N's ghosts on its side faces
+  double gdeep[NG], grhs[NG], gedge[NG][2];
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    const int p = tid + BS * g;
+    if (p >= 6 * FH) continue;
+    const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
+    const bool low = nb & 1;
+    const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
+    const int d = (nb - 1) >> 1, nl = low ? NC : 1;
+    const long long noff = (long long)F.nba[(long long)b * 6 + nb - 1] * F.stride;
+    const double* un = F.phi + noff;
+    gdeep[g] = un[sr_int<NC>(d, low ? NC - 1 : 2, a, c)];
+    grhs[g] = F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)];
+    // a tangential neighbour outside N's face (edges; two at corners)
+    gedge[g][0] = gedge[g][1] = 0.0;
+    const bool ea = a == 1 || a == NC, ec = c == 1 || c == NC;
+    if (ea) gedge[g][0] = un[sr_edge<NC>(d, 0, a == 1, nl, a, c)];
+    if (ec) {
+      const double e = un[sr_edge<NC>(d, 1, c == 1, nl, a, c)];
+      if (ea) gedge[g][1] = e; else gedge[g][0] = e;
+    }
+  }
+  __syncthreads();
+
+  const OpCoef<OP> K(F, lambda);
+  // ---- colour-0 update (the substep), pairs q2 < HV/2 ----
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 >= HV / 2) continue;
+    Nbr7 s0, s1;
+    pair_stencil<NC>(sb + HV, sb + 2 * HV + FH, FS, 0, 2 * q2, s0, s1);
+    const double v0 = gs_value<OP>(K, s0, fr[r].x), v1 = gs_value<OP>(K, s1, fr[r].y);
+    reinterpret_cast<double2*>(sb)[q2] = make_double2(v0, v1);
+    st_nt(u + 2 * q2, v0, v1);
+  }
+  // ---- the neighbours' new colour-0 boundary cells = our colour-0 ghosts ----
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    const int p = tid + BS * g;
+    if (p >= 6 * FH) continue;
+    const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
+    const bool low = nb & 1;
+    const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
+    const int d = (nb - 1) >> 1;
+    const double across = sb[sr_int<NC>(d, low ? 1 : NC, a, c)];
+    const bool ea = a == 1 || a == NC;
+    // along the face normal, then the two tangential axes (t1 < t2)
+    const double dm = low ? gdeep[g] : across, dp = low ? across : gdeep[g];
+    const double am = a == 1 ? gedge[g][0] : sb[TL::ogh(nb, a - 1, c)];
+    const double ap = a == NC ? gedge[g][0] : sb[TL::ogh(nb, a + 1, c)];
+    const double ce = ea ? gedge[g][1] : gedge[g][0];
+    const double cm = c == 1 ? ce : sb[TL::ogh(nb, a, c - 1)];
+    const double cp = c == NC ? ce : sb[TL::ogh(nb, a, c + 1)];
+    Nbr7 s;
+    s.xm = d == 0 ? dm : am;
+    s.xp = d == 0 ? dp : ap;
+    s.ym = d == 1 ? dm : (d == 0 ? am : cm);
+    s.yp = d == 1 ? dp : (d == 0 ? ap : cp);
+    s.zm = d == 2 ? dm : cm;
+    s.zp = d == 2 ? dp : cp;
+    sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, grhs[g]);
+  }
+  __syncthreads();
+  // our new colour-0 boundary cells to the neighbours' colour-0 ghost halves
+  face_push_local<NC>(F, b, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
+  resid_restrict_core<NC, OP, BS>(F, Cv, lambda, nullptr, restrict_on, parent_local, dixp, b, sb, fr);
 }
 
 // SUB: correct_children's `res = phi - old` on the parent (m_multigrid.f90:
@@ -712,6 +853,24 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
     case 4: k_fill_tile<4, 64><<<g, 64, 0, st>>>(L, bc, sendbuf); return true;
     default: return false;
   }
+}
+
+bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
+                         const int* parent_local, const int* dixp, hipStream_t st) {
+  if (F.n == 0) return true;
+  const dim3 g(F.n);
+  if (op != OP_LPL && op != OP_HELM) return false;
+#define OMG_SR(NC, BS)                                                                                   \
+  if (op == OP_LPL)                                                                                      \
+    k_smooth_resid<NC, OP_LPL, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp);   \
+  else                                                                                                   \
+    k_smooth_resid<NC, OP_HELM, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp);
+  switch (F.nc) {
+    case 16: OMG_SR(16, 512) return true;
+    case 8: OMG_SR(8, 256) return true;
+    default: return false;
+  }
+#undef OMG_SR
 }
 
 bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }

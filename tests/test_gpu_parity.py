@@ -154,3 +154,19 @@ def test_diffusion_bad_order_fails_like_reference():
     with pytest.raises(omg.device.OmgError, match="order should be 1 or 2"):
         be.mg.ctx.call("diffusion_solve", 3, 0.01, 1.0, 3, 1e-8, None, None)
     assert phi_digest(be) == before
+
+
+@pytest.mark.parametrize("args", ["16 64 64 64 2 v gsrb lpl 0 per sol 1 lb 0",
+                                  "16 64 64 64 2 f gsrb lpl 0 per sol 1 lb 0",
+                                  "16 64 64 64 2 v gsrb helm 2 per sol 1 lb 0",
+                                  "8 64 64 64 2 v gsrb helm 2 per sol 1 lb 0"])
+def test_fused_down_substep_matches_oracle(args):
+    """Levels whose faces are all same-GPU boxes end their down-smoothing in
+    k_smooth_resid (last substep + residual + restriction, the neighbours'
+    new boundary cells recomputed): box sizes 16 and 8, Laplacian (with the
+    periodic subtract_mean) and Helmholtz, V-cycles and FMG, bit for bit
+    against the oracle."""
+    dev = run_problem(args, backend="device")
+    orc = run_problem(args, backend="oracle")
+    assert dev["history"] == orc["history"]
+    assert dev["phi_sha256"] == orc["phi_sha256"]
