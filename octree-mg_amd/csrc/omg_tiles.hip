@@ -187,6 +187,28 @@ __device__ __forceinline__ int sr_edge(int d, int t, bool lo, int nl, int a, int
   return ax == 0 ? Tl<NC>::ogh(fn, j, k) : (ax == 1 ? Tl<NC>::ogh(fn, i, k) : Tl<NC>::ogh(fn, i, j));
 }
 
+// k_smooth_resid: non-temporal loads of colour 1 and rhs (measured 85 us
+// slower at 512^3: the neighbours' loads of the same lines then miss L2);
+// EARLY: neighbour loads issued before the bulk loads (10 us faster); timing-only
+// switches (wrong results): no neighbour loads / no ghost recompute
+#ifndef OMG_SR_NT
+#define OMG_SR_NT 0
+#endif
+#ifndef OMG_SR_EARLY
+#define OMG_SR_EARLY 1
+#endif
+#ifndef OMG_SR_NOLOAD
+#define OMG_SR_NOLOAD 0
+#endif
+#ifndef OMG_SR_NOGHOST
+#define OMG_SR_NOGHOST 0
+#endif
+template <bool NT>
+__device__ __forceinline__ v2d sr_ld(const double* p) {
+  if (NT) return ld_nt(p);
+  return *reinterpret_cast<const v2d*>(p);
+}
+
 // The last down-smoothing substep of a level fused with update_coarse's
 // residual + restriction (k_smooth_resid).  The substep updates colour 0
 // from colour 1, which it does not change, so the colour-0 ghost values the
@@ -206,28 +228,31 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   const long long boff = (long long)b * F.stride;
   double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
-  // colour 1 and the colour-1 halves of the ghost faces
-  for (int q = tid; q < HV / 2; q += BS)
-    reinterpret_cast<v2d*>(sb + HV)[q] = ld_nt(u + HV + 2 * q);
-  for (int q = tid; q < 3 * FH; q += BS) {
-    const int nb = q / (FH / 2), r = q % (FH / 2);
-    reinterpret_cast<v2d*>(sb + 2 * HV + nb * FS + FH)[r] = ld_nt(u + 2 * HV + nb * FS + FH + 2 * r);
-  }
   v2d fr[NR];
+  auto bulk_loads = [&]() {
+    // colour 1 and the colour-1 halves of the ghost faces
+    for (int q = tid; q < HV / 2; q += BS)
+      reinterpret_cast<v2d*>(sb + HV)[q] = sr_ld<OMG_SR_NT>(u + HV + 2 * q);
+    for (int q = tid; q < 3 * FH; q += BS) {
+      const int nb = q / (FH / 2), r = q % (FH / 2);
+      reinterpret_cast<v2d*>(sb + 2 * HV + nb * FS + FH)[r] = sr_ld<OMG_SR_NT>(u + 2 * HV + nb * FS + FH + 2 * r);
+    }
 #pragma unroll
-  for (int r = 0; r < NR; r++) {
-    const int q2 = tid + BS * r;
-    if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
-  }
+    for (int r = 0; r < NR; r++) {
+      const int q2 = tid + BS * r;
+      if (q2 < HV) fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
+    }
+  };
+  if (!OMG_SR_EARLY) bulk_loads();
   // the neighbour-side operands of our colour-0 ghost cells: N's cell X at
   // (layer nl, a, c) has neighbours deep (N's second layer), across (our
   // boundary layer, LDS), and tangentially N's boundary cells (our colour-1
   // ghosts, LDS) or, past the face edge, N's ghosts on its side faces
-  double gdeep[NG], grhs[NG], gedge[NG][2];
+  double gdeep[NG] = {}, grhs[NG] = {}, gedge[NG][2] = {};
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     const int p = tid + BS * g;
-    if (p >= 6 * FH) continue;
+    if (p >= 6 * FH || OMG_SR_NOLOAD) continue;
     const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
@@ -245,6 +270,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
       if (ea) gedge[g][1] = e; else gedge[g][0] = e;
     }
   }
+  if (OMG_SR_EARLY) bulk_loads();
   __syncthreads();
 
   const OpCoef<OP> K(F, lambda);
@@ -263,7 +289,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     const int p = tid + BS * g;
-    if (p >= 6 * FH) continue;
+    if (p >= 6 * FH || OMG_SR_NOGHOST) continue;
     const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
