@@ -576,7 +576,7 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
   const Level* C = level_ptr(c, lvl - 1);
   return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_down >= 1 &&
          (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) && !F->has_rb &&
-         !F->has_remote && !F->has_phys;
+         !F->has_phys && (!F->has_remote || F->n_int);
 }
 
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down
@@ -592,7 +592,34 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
   if (F && F->n && tiled_level(c, F)) {
     // residual + restriction of phi and res in one pass (omg_tiles.hip)
     phi_dirty(c, lvl - 1);
-    if (fused) {
+    if (fused && F->has_remote) {
+      // multi-GPU: boxes with a face on another GPU take the unfused pair (the
+      // substep, its halo on the comm stream, then the residual); the others
+      // run fused meanwhile.  They read the neighbours' ghosts only at face
+      // edges, colour 1, which the unpack rewrites with the values they hold.
+      {
+        Prof p(c, "smoother_gsrb", 0.5 * F->n_bnd * F->nc * F->nc * F->nc, lvl);
+        launch_gs_substep(F->view(), c->op, c->lambda, 0, 1, view_of(c, lvl - 1), F->d_rb, F->has_rb,
+                          bc_for(c, lvl, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd);
+      }
+      HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
+      exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm);
+      launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm);
+      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
+      {
+        Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
+        if (!launch_smooth_resid(F->view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
+                                 F->d_dix, c->stream, F->d_int, F->n_int))
+          throw OmgError("smooth_resid: not available for this level");
+      }
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+      {
+        Prof p(c, "resid_restrict", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl);
+        launch_resid_restrict(F->view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+                              F->d_dix, c->stream, F->d_bnd, F->n_bnd);
+      }
+    } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
                                F->d_dix, c->stream))

@@ -112,10 +112,11 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
 // the last down-smoothing substep (colour 0) + residual + restriction in one
 // pass (k_smooth_resid); false: not available for this op / box size
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
-                         const int* parent_local, const int* dixp, hipStream_t st);
+                         const int* parent_local, const int* dixp, hipStream_t st, const int* list = nullptr,
+                         int n_list = 0);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
-                           const int* dixp, hipStream_t st);
+                           const int* dixp, hipStream_t st, const int* list = nullptr, int n_list = 0);
 // sub: form the parent's res = phi - old on the fly (and store it) instead of
 // reading it (correct_children's parent loop fused in); skip1: a colour-1
 // red-black substep follows, so all-local boxes correct and push colour 0 only

@@ -164,10 +164,11 @@ __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const Le
 template <int NC, int OP, int BS>
 __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv, double lambda,
                                                        unsigned long long* maxbits, int restrict_on,
-                                                       const int* parent_local, const int* dixp) {
+                                                       const int* parent_local, const int* dixp,
+                                                       const int* list) {
   __shared__ double sb[Tl<NC>::NST];
-  resid_restrict_box<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp,
-                                 xcd_box(blockIdx.x, gridDim.x), sb);
+  const int q = xcd_box(blockIdx.x, gridDim.x);
+  resid_restrict_box<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp, list ? list[q] : q, sb);
 }
 
 // Tile offset of the cell at layer v along axis d and tangential (a, c)
@@ -219,12 +220,13 @@ __device__ __forceinline__ v2d sr_ld(const double* p) {
 // Levels whose faces are all same-GPU boxes, Laplacian / Helmholtz, NC 16/8.
 template <int NC, int OP, int BS>
 __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, double lambda, int restrict_on,
-                                                     const int* parent_local, const int* dixp) {
+                                                     const int* parent_local, const int* dixp,
+                                                     const int* list) {
   using TL = Tl<NC>;
   constexpr int H = NC / 2, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS;
   constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
   __shared__ double sb[TL::NST];
-  const int tid = threadIdx.x, b = xcd_box(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x, bq = xcd_box(blockIdx.x, gridDim.x), b = list ? list[bq] : bq;
   const long long boff = (long long)b * F.stride;
   double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
@@ -882,15 +884,17 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
 }
 
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
-                         const int* parent_local, const int* dixp, hipStream_t st) {
-  if (F.n == 0) return true;
-  const dim3 g(F.n);
+                         const int* parent_local, const int* dixp, hipStream_t st, const int* list,
+                         int n_list) {
   if (op != OP_LPL && op != OP_HELM) return false;
+  const int n = list ? n_list : F.n;
+  if (n == 0) return true;
+  const dim3 g(n);
 #define OMG_SR(NC, BS)                                                                                   \
   if (op == OP_LPL)                                                                                      \
-    k_smooth_resid<NC, OP_LPL, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp);   \
+    k_smooth_resid<NC, OP_LPL, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list);   \
   else                                                                                                   \
-    k_smooth_resid<NC, OP_HELM, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp);
+    k_smooth_resid<NC, OP_HELM, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list);
   switch (F.nc) {
     case 16: OMG_SR(16, 512) return true;
     case 8: OMG_SR(8, 256) return true;
@@ -903,11 +907,12 @@ bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }
 
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
-                           const int* dixp, hipStream_t st) {
-  if (F.n == 0) return;
-  const dim3 g(F.n);
+                           const int* dixp, hipStream_t st, const int* list, int n_list) {
+  const int n = list ? n_list : F.n;
+  if (n == 0) return;
+  const dim3 g(n);
 #define OMG_RR_OP(NC, BS, OPV) \
-  k_resid_restrict<NC, OPV, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, dixp);
+  k_resid_restrict<NC, OPV, BS><<<g, dim3(BS), 0, st>>>(F, C, lambda, maxbits, restrict_on, parent_local, dixp, list);
 #define OMG_RR(NC, BS) OMG_FOR_OP(op, OMG_RR_OP, NC, BS)
   switch (F.nc) {
     case 16: OMG_RR(16, 512) break;
