@@ -170,3 +170,23 @@ def test_fused_down_substep_matches_oracle(args):
     orc = run_problem(args, backend="oracle")
     assert dev["history"] == orc["history"]
     assert dev["phi_sha256"] == orc["phi_sha256"]
+
+
+@pytest.mark.parametrize("down,up", [(1, 1), (3, 2)])
+def test_fused_down_substep_other_cycle_counts(down, up):
+    """k_smooth_resid with n_cycle_down 1 (the pending mean shift is absorbed
+    by the only unfused substep) and 3: V-cycles bit for bit against the
+    oracle, every stored variable."""
+    from tests.mgdriver import setup_problem
+    cfg = parse("16 64 64 64 3 v gsrb lpl 0 per sol 1 lb 0")
+    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+    import pyoracle  # on sys.path once OracleBackend exists (checker only)
+    dev.mg.n_cycle_down, dev.mg.n_cycle_up = down, up
+    dev.mg._push_methods()
+    orc.o.configure(op=pyoracle.LAPLACIAN, lam=0.0, smoother=pyoracle.GSRB, n_cycle_down=down,
+                    n_cycle_up=up, subtract_mean=True)
+    for be in (dev, orc):
+        setup_problem(be)
+    for _ in range(3):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc, ivs=(1, 2, 3, 4))
