@@ -42,9 +42,11 @@ REPLICATE_CELLS = int(os.environ.get("OMG_REPLICATE_CELLS", 64 * 16 ** 3))
 CPU_CYCLES = 12
 
 
-KERNEL_FAMILIES = ("smoother_gsrb", "fill_gc", "resid_restrict", "residual", "restrict",
-                   "prolong_fill", "prolong", "sub_parents", "coarse_rhs", "box_sums",
-                   "seq_sum", "subtract")
+# every Prof name the library records (omg_api.cpp); the per-cycle breakdown
+# also reports what these do not account for
+KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
+                   "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
+                   "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract")
 
 
 def pmc_traffic():
@@ -180,15 +182,26 @@ def main():
     if not a.no_profile_pass:
         mg.ctx.call("reset_stats")
         mg.ctx.call("set_profiling", 1)
+        barrier()
+        tp = time.perf_counter()
         omg.mg_fas_vcycle(mg)
+        barrier()
+        tp = time.perf_counter() - tp
         mg.ctx.call("set_profiling", 0)
         hi = mg.highest_lvl
+        total = 0.0
         for name in KERNEL_FAMILIES:
             n, ms, c = mg.ctx.kernel_stats(name)
             if n:
+                total += ms
                 n1, ms1, _ = mg.ctx.kernel_stats(f"{name}@{hi}")
                 kern[name] = {"launches": n, "ms": round(ms, 4), f"launches_lvl{hi}": n1,
                               f"ms_lvl{hi}": round(ms1, 4)}
+        # wall time of the profiled cycle (event pairs add a little) and what
+        # the families above do not account for (launch gaps, RCCL, host
+        # waits; side-stream work overlaps and can make it negative)
+        kern["profiled_cycle_ms"] = round(tp * 1e3, 4)
+        kern["unaccounted_ms"] = round(tp * 1e3 - total, 4)
         # dominant kernel: the red-black substep on the finest level
         n, ms, upd = mg.ctx.kernel_stats(f"smoother_gsrb@{hi}")
         if n and ms > 0:

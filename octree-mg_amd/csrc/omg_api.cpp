@@ -462,8 +462,9 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     if (n == 1) L->shift_pending = false;
     if (L->n_bnd && L->n_int && !odd && gs_tiled(L->nc, c->op, L->has_rb)) {
       // boxes with faces on other GPUs first; their halo travels on the comm
-      // stream while the interior boxes run (interior boxes never touch a
-      // remote ghost face, the unpack touches nothing else)
+      // stream while the interior boxes run (the substep reads only its own
+      // box's ghost faces, and an interior box has no remote one; the unpack
+      // writes remote faces only)
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_bnd * L->nc * L->nc * L->nc, lvl);
         launch_gs_substep(L->view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
@@ -568,13 +569,17 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
 }
 
 // Whether the down-smoothing of level lvl can end in k_smooth_resid (its last
-// substep fused with update_coarse's residual + restriction): red-black with
-// an even substep count, Laplacian / Helmholtz, 16^3 or 8^3 boxes, every face
-// a same-GPU box (the recomputed ghosts read the neighbour directly).
+// substep, colour 0, fused with update_coarse's residual + restriction):
+// red-black (two substeps per cycle, so the last one is colour 0),
+// Laplacian / Helmholtz, 16^3 or 8^3 boxes, no physical or refinement-boundary
+// face on the level (the recomputed ghosts read the neighbour box directly).
+// On a level with faces on other GPUs only the boxes without such a face fuse
+// (n_int > 0); the others take the unfused substep + residual.
 bool smooth_resid_ok(omg_ctx* c, int lvl) {
   const Level* F = level_ptr(c, lvl);
   const Level* C = level_ptr(c, lvl - 1);
-  return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_down >= 1 &&
+  return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_substeps == 2 &&
+         c->n_cycle_down >= 1 &&
          (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) && !F->has_rb &&
          !F->has_phys && (!F->has_remote || F->n_int);
 }
@@ -595,8 +600,10 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     if (fused && F->has_remote) {
       // multi-GPU: boxes with a face on another GPU take the unfused pair (the
       // substep, its halo on the comm stream, then the residual); the others
-      // run fused meanwhile.  They read the neighbours' ghosts only at face
-      // edges, colour 1, which the unpack rewrites with the values they hold.
+      // run fused meanwhile.  Those read their neighbours' colour-1 ghosts at
+      // face edges, and some of those faces are remote: the unpack therefore
+      // writes the colour-0 halves only (the colour this substep changed;
+      // colour 1 is consistent since the previous substep's exchange).
       {
         Prof p(c, "smoother_gsrb", 0.5 * F->n_bnd * F->nc * F->nc * F->nc, lvl);
         launch_gs_substep(F->view(), c->op, c->lambda, 0, 1, view_of(c, lvl - 1), F->d_rb, F->has_rb,
@@ -605,7 +612,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
       exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm);
-      launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm);
+      launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm, 1);
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       {
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);

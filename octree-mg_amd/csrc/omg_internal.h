@@ -226,7 +226,7 @@ struct omg_ctx {
   bool no_tail = false;                // OMG_NO_TAIL: level-by-level coarse end (A/B checks)
   bool no_fuse_up = false;             // OMG_NO_FUSE_UP: separate prolongation and first up-substep
   bool no_skip1 = false;               // OMG_NO_SKIP1: correct colour 1 before the up-smoothing too
-  bool no_fuse_down = false;
+  bool no_fuse_down = false;           // OMG_NO_FUSE_DOWN: last down-substep and residual + restriction apart
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending

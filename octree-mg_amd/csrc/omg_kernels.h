@@ -49,7 +49,7 @@ void launch_residual(const LevelView& L, int op, double lambda, unsigned long lo
 void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C, const RBRec* rb,
                     const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, const double* recv,
-                         hipStream_t st);
+                         hipStream_t st, int colours = 3);
 void launch_rb_pack(const LevelView& C, int iv, const int* items, int n, int nc, double* buf, hipStream_t st);
 void launch_rb_unpack(const LevelView& L, int iv, const int* items, int n, const double* recv, hipStream_t st);
 void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* pairs, int n_pairs,

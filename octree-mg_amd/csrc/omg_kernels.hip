@@ -35,13 +35,17 @@ __global__ void __launch_bounds__(256) k_fill_gc(LevelView L, int iv, int colour
 }
 
 // fill_buffered_nb (m_ghost_cells.f90:424-454): received faces -> ghosts.
+// colours: bit e set = write the ghosts of colour e (the sender packs whole
+// faces; a caller that knows only colour e changed writes that half only).
 __global__ void __launch_bounds__(256) k_unpack_faces(LevelView L, int iv, const int* items, int n_items,
-                                                      const double* recv) {
+                                                      const double* recv, int colours) {
   const int nc = L.nc, nc2 = nc * nc;
   GRID_STRIDE(t, (long long)n_items * nc2) {
     const int q = (int)(t / nc2), cell = (int)(t % nc2);
     const int it = items[q], b = it / 6, nb = it % 6 + 1;
-    boxp(L, iv, b)[off_gh(L, nb, cell % nc + 1, cell / nc + 1)] = recv[t];
+    const int a = cell % nc + 1, c = cell / nc + 1, g = (nb & 1) ? 0 : nc + 1;
+    if (!((colours >> ((g + a + c) & 1)) & 1)) continue;
+    boxp(L, iv, b)[off_gh(L, nb, a, c)] = recv[t];
   }
 }
 
@@ -534,10 +538,10 @@ void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C,
 }
 
 void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, const double* recv,
-                         hipStream_t st) {
+                         hipStream_t st, int colours) {
   const long long work = (long long)n * L.nc * L.nc;
   if (work == 0) return;
-  k_unpack_faces<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, recv);
+  k_unpack_faces<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, recv, colours);
 }
 
 void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* pairs, int n_pairs,

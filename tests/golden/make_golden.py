@@ -42,6 +42,13 @@ CONFIGS = {
     # others)
     "per64_gsrb_v": ("8 64 64 64 4 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
     "helm128_box16_d0": ("16 128 128 128 3 v gsrb helm 10 d0 sol 1 lb 1", True, [1, 2, 4]),
+    # box-16 periodic levels with boxes both with and without a face on
+    # another rank (the multi-GPU bench's level kind): the fused down-step
+    # (k_smooth_resid over a box list) next to the unfused substep + residual;
+    # at 6 ranks the 128x128x64 tree leaves ranks 1 and 4 with no box free of
+    # remote faces, so they stay unfused while their peers fuse
+    "per128_box16_gsrb_v": ("16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 8]),
+    "per128x64_box16_mixed": ("16 128 128 64 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 6]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),

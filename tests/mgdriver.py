@@ -391,12 +391,31 @@ def run_problem(args: str, backend="device", n_ranks=1, n_its=None, reduce=None)
     return out
 
 
+def _owned_phi(be):
+    """{(lvl, id): interior phi bytes} of the boxes this rank owns (a
+    replicated coarse level: every box, each rank holds them all)."""
+    out = {}
+    for lvl in be.levels():
+        ids = be.my_ids(lvl)
+        n, nc = be.mg.ctx.level_size(lvl)
+        if lvl <= be.rep_lvl and n == len(be.tree.lvls[lvl].ids):
+            ids = be.tree.lvls[lvl].ids
+        if not n:
+            continue
+        phi = be.mg.get_level(lvl, T.MG_IPHI)[:, 1:nc + 1, 1:nc + 1, 1:nc + 1]
+        for q, id_ in enumerate(ids):
+            out[(lvl, int(id_))] = np.ascontiguousarray(phi[q]).tobytes()
+    return out
+
+
 def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0):
     """The same configuration on n_ranks device contexts of this process (one
     thread per rank, all on GPU 0), exchanging through the loopback transport
     (omg_loopback_unique_id): the multi-rank path of libomg.so (plans, packing,
     MPICH-order reductions) on a single GPU.  Returns the history with err /
-    res reduced by max over ranks, as omg_golden's MPI_Reduce(MAX)."""
+    res reduced by max over ranks, as omg_golden's MPI_Reduce(MAX), and the
+    sha256 of the final phi of every box gathered from its owner, in the
+    order phi_digest uses for a one-rank run (ids per level, lowest first)."""
     import threading
     cfg = parse(args)
     if n_its is not None:
@@ -405,6 +424,8 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
     bar = threading.Barrier(n_ranks)
     slots = [None] * n_ranks
     out = [None] * n_ranks
+    phis = [None] * n_ranks
+    trees = [None] * n_ranks
     errors = []
 
     def worker(rank):
@@ -420,6 +441,8 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
             setup_problem(be)
             out[rank] = _cycles(be, cfg, reduce)
             be.mg.ctx.call("synchronize")
+            phis[rank] = _owned_phi(be)
+            trees[rank] = be.tree
             omg.mg_deallocate_storage(be.mg)
         except BaseException as ex:  # noqa: BLE001  (re-raised in the caller)
             errors.append((rank, ex))
@@ -437,4 +460,11 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
     if any(t.is_alive() for t in th):
         raise TimeoutError("loopback run did not finish")
     assert all(h == out[0] for h in out)
-    return {"history": out[0]}
+    tree = trees[0]
+    h = hashlib.sha256()
+    for lvl in range(tree.lowest_lvl, tree.highest_lvl + 1):
+        for id_ in tree.lvls[lvl].ids:
+            key = (lvl, int(id_))
+            owner = int(tree.rank[id_])
+            h.update(phis[owner][key] if key in phis[owner] else phis[0][key])
+    return {"history": out[0], "phi_sha256": h.hexdigest()}

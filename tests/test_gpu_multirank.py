@@ -9,7 +9,7 @@ import os
 
 import pytest
 
-from tests.mgdriver import run_problem_loopback
+from tests.mgdriver import run_problem, run_problem_loopback
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
 MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) for r in e["runs"] if int(r) > 1]
@@ -34,3 +34,23 @@ def test_multirank_replicated_coarse_matches_golden(name, ranks, rep):
     e = GOLDEN[name]
     out = run_problem_loopback(e["args"], ranks, rep_cells=rep)
     assert out["history"] == e["runs"][str(ranks)]["history"]
+
+
+# Box-16 periodic levels where only the boxes without a face on another rank
+# take the fused last down-substep (k_smooth_resid over a box list) and the
+# others the unfused substep + residual, with the colour-0 halo unpacked
+# while the fused boxes run; per128x64 at 6 ranks leaves ranks 1 and 4 with
+# no such box (they stay unfused, their peers fuse).  History against the
+# reference, final phi of every box against the oracle at the same rank
+# count (the reference dumps phi at one rank only).
+FUSED = [("per128_box16_gsrb_v", 2), ("per128_box16_gsrb_v", 8), ("per128x64_box16_mixed", 6)]
+
+
+@pytest.mark.parametrize("name,ranks", FUSED)
+def test_multirank_fused_down_step_phi_matches_oracle(name, ranks):
+    e = GOLDEN[name]
+    out = run_problem_loopback(e["args"], ranks)
+    assert out["history"] == e["runs"][str(ranks)]["history"]
+    orc = run_problem(e["args"], backend="oracle", n_ranks=ranks)
+    assert orc["history"] == out["history"]
+    assert out["phi_sha256"] == orc["phi_sha256"]
