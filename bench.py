@@ -46,7 +46,7 @@ CPU_CYCLES = 12
 # also reports what these do not account for
 KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
-                   "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract")
+                   "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
 
 
 def pmc_traffic():

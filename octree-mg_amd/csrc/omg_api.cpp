@@ -905,7 +905,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       Level* L = level_ptr(c, l);
       if (!L || !L->n) continue;
       if (mode == kInCycle && L->all_parents) continue;
-      Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, l);
+      Prof p(c, "subtract_rhs", (double)L->n * L->nc * L->nc * L->nc, l);
       if (l >= 1 && (int)L->leaves.size() == L->n && subtract_sums_nc(L->nc))
         launch_subtract_sums(L->view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
       else {

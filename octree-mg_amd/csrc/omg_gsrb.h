@@ -136,6 +136,12 @@ __device__ __forceinline__ void op_pair(const OpCoef<OP>& K, const LevelView& L,
   }
 }
 
+// timing-only switch (wrong results; tools/ab_variants.sh): bit 0 = no
+// pushes to y/z neighbours, bit 1 = no y/z ghost-half loads
+#ifndef OMG_T_YZ
+#define OMG_T_YZ 0
+#endif
+
 // RB: the level has refinement-boundary faces (a separate instantiation keeps
 // their interpolation out of the plain kernels)
 template <int NC, int OP, int BS, int NT, bool PRE = false, bool RB = false>
@@ -168,6 +174,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     }
     for (int q = tid; q < 3 * FH; q += BS) {   // 6 faces x FH/2 double2
       const int nb = q / (FH / 2), r = q % (FH / 2);
+      if ((OMG_T_YZ & 2) && nb >= 2) continue;
       const v2d* gp = reinterpret_cast<const v2d*>(u + 2 * HV + nb * FS + o * FH) + r;
       v2d x = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
       if (shift) {
@@ -265,7 +272,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     const int idx = ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
     return ((i + j + k) & 1) == e ? se[idx] : so[idx];
   };
-  face_push_local<NC>(L, b, colours, cellv);
+  face_push_local<NC>(L, b, colours, cellv, (OMG_T_YZ & 1) ? 0x3u : 0x3fu);
   for (int p = tid; p < 6 * NC * NC; p += BS) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
     const long long fidx = (long long)b * 6 + nb - 1;
