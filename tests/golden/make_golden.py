@@ -22,6 +22,9 @@ REF = os.path.join(HERE, "..", "..", "oracle", "_ref")
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 # name: (box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres), dump?, ranks
+# BIG: too large for the CPU oracle in the quick CPU suite (the device is
+# compared with the reference's numbers directly; tests/test_gpu_parity.py)
+BIG = {"c3_per512_box16"}
 CONFIGS = {
     # tests/test_uniform_grid 8 64 64 64 10 f, as shipped (GS)
     "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
@@ -49,6 +52,9 @@ CONFIGS = {
     # remote faces, so they stay unfused while their peers fuse
     "per128_box16_gsrb_v": ("16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 8]),
     "per128x64_box16_mixed": ("16 128 128 64 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 6]),
+    # SURVEY §8(d) C3 at the bench's own size: 512^3 per GPU, box 16,
+    # periodic, GSRB (the reference takes ~40 s on one core)
+    "c3_per512_box16": ("16 512 512 512 3 v gsrb lpl 0 per sol 1 lb 0", True, [1]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),
@@ -125,6 +131,8 @@ def main():
         args, dump, ranks = spec[:3]
         expect_error = len(spec) > 3 and spec[3]
         entry = {"args": args, "runs": {}}
+        if name in BIG:
+            entry["big"] = True
         for r in ranks:
             with tempfile.TemporaryDirectory() as td:
                 fn = os.path.join(td, "phi.bin") if (dump and r == 1) else None
