@@ -309,6 +309,11 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
 template <int NC>
 constexpr int gs_lex_lds() { return (NC + 2) * (NC + 2) * (NC + 2) + NC * NC * NC; }
 
+// timing-only switch (wrong results): 1 = no sweep (load + store only),
+// 2 = no loads (sweep + store)
+#ifndef OMG_T_LEX
+#define OMG_T_LEX 0
+#endif
 template <int OP, int NC>
 __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, int b, double* lds) {
   constexpr int S = NC + 2, S3 = S * S * S, N3 = NC * NC * NC;
@@ -317,15 +322,15 @@ __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, in
   const OpCoef<OP> K(L, lambda);
   double* u = boxp(L, 1, b);
   const double* f = boxp(L, 2, b);
-  for (int q = threadIdx.x; q < S3; q += blockDim.x) {
+  for (int q = threadIdx.x; q < S3 && OMG_T_LEX != 2; q += blockDim.x) {
     const int i = q % S, j = (q / S) % S, k = q / (S * S);
     const int nbd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
     P[q] = nbd <= 1 ? u[off_cell(L, i, j, k)] : 0.0;
   }
-  for (int q = threadIdx.x; q < N3; q += blockDim.x)
+  for (int q = threadIdx.x; q < N3 && OMG_T_LEX != 2; q += blockDim.x)
     R[q] = f[off_int(L, q % NC + 1, (q / NC) % NC + 1, q / (NC * NC) + 1)];
   __syncthreads();
-  for (int d = 3; d <= 3 * NC; d++) {
+  for (int d = 3; d <= 3 * NC && OMG_T_LEX != 1; d++) {
     for (int p = threadIdx.x; p < NC * NC; p += blockDim.x) {
       const int j = p % NC + 1, k = p / NC + 1, i = d - j - k;
       if (i < 1 || i > NC) continue;

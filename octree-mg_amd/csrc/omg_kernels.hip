@@ -11,6 +11,9 @@
 #include "omg_gsrb.h"
 #include "omg_kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace omg {
 
 static inline unsigned grid_for(long long work, int block = 256) {
@@ -162,6 +165,169 @@ template <int OP, int NC>
 __global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) {
   __shared__ double lds[gs_lex_lds<NC>()];
   for (int b = blockIdx.x; b < L.n; b += gridDim.x) gs_lex_box<OP, NC>(L, lambda, b, lds);
+}
+
+// Lexicographic GS with one wave per box (64-thread workgroups, so the
+// plane-to-plane barrier is free) and the box dense in LDS, (NC+2)^3 with i
+// fastest: 46.6 KB for 16^3, so three boxes share a CU.  The stored box
+// (colour-split interior + face ghosts, omg_device.h) comes in and the
+// interior goes back as whole 16-B rows.  Hyperplanes i+j+k = d in increasing
+// d as in gs_lex_box, same operands and gs_value: bit-identical to the
+// reference's i-fastest loop.  Lane l owns the lines (j, k) = l + 64 r; rhs of
+// its cells is read from L2 GS_PF planes ahead (one wave per box hides no
+// latency by itself).
+#ifndef OMG_GS_PF
+#define OMG_GS_PF 8
+#endif
+// timing-only (wrong results): 1 = no sweep, 2 = no rhs loads, 3 = no box load
+#ifndef OMG_T_LEXW
+#define OMG_T_LEXW 0
+#endif
+template <int NC>
+constexpr int gs_wave_lds() { return (NC + 2) * (NC + 2) * (NC + 2); }
+
+// WPS: waves per SIMD the register budget must allow (the LDS-bound
+// workgroups per CU x T/64 / 4)
+template <int OP, int NC, int T, int WPS>
+__global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lambda) {
+  using TL = Tl<NC>;
+  constexpr int S = NC + 2, NL = (NC * NC + T - 1) / T, H = TL::H, HV = TL::HV, FS = TL::FS;
+  constexpr int D0 = 3, D1 = 3 * NC, PF = OMG_GS_PF, NQ = (TL::NST / 2 + T - 1) / T;
+  __shared__ double P[gs_wave_lds<NC>()];
+  const int tid = threadIdx.x, G = gridDim.x;
+  const OpCoef<OP> K(L, lambda);
+  // stored slot q -> dense index (edges and corners are neither stored nor read)
+  auto dense = [&](int q) {
+    int i, j, k;
+    if (q < 2 * HV) {
+      TL::decode(q, i, j, k);
+    } else {
+      const int r0 = q - 2 * HV, nb = r0 / FS + 1, r1 = r0 % FS;
+      const int e = r1 >= H * NC, r = r1 - e * H * NC, ah = r % H, c = r / H + 1;
+      const int g = (nb & 1) ? 0 : NC + 1;
+      const int a = 2 * ah + 1 + ((1 + g + c + e) & 1);
+      const int d = (nb + 1) >> 1;
+      if (d == 1) { i = g; j = a; k = c; }
+      else if (d == 2) { i = a; j = g; k = c; }
+      else { i = a; j = c; k = g; }
+    }
+    return i + S * (j + S * k);
+  };
+  // per line: j + k, its dense base (c - i) and its row offset in rhs
+  int jk[NL], cbase[NL], roff[NL];
+#pragma unroll
+  for (int r = 0; r < NL; r++) {
+    const int p = tid + T * r, j = p % NC + 1, k = p / NC + 1;
+    jk[r] = p < NC * NC ? j + k : 1 << 20;   // lanes past the last line never fall in range
+    cbase[r] = S * (j + S * k);
+    roff[r] = H * ((j - 1) + NC * (k - 1));
+  }
+  auto rhs_plane = [&](const double* f, int d, double* out) {
+#pragma unroll
+    for (int r = 0; r < NL; r++) {
+      const int i = min(max(d - jk[r], 1), NC);   // off-plane lanes load a valid dummy
+      if (OMG_T_LEXW != 2) out[r] = f[(d & 1) * HV + ((i - 1) >> 1) + roff[r]];
+      else out[r] = 0.0;
+    }
+  };
+  // Persistent workgroups: box sequence q = blockIdx.x + G t (G a multiple of
+  // 8, so every box of one workgroup sits on its XCD's run, xcd_box).  The
+  // next box's stored data and first rhs planes are loaded into registers
+  // while this box sweeps.
+  double ring[PF][NL], ringn[PF][NL];
+  v2d buf[NQ];
+  auto issue = [&](int q, double (*rg)[NL]) {
+    const int b = xcd_box(q, L.n);
+    const double* f = boxp(L, 2, b);
+#pragma unroll
+    for (int s = 0; s < PF; s++) rhs_plane(f, D0 + s, rg[s]);
+    const double* u = boxp(L, 1, b);
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      const int q2 = tid + T * r;
+      if (q2 < TL::NST / 2 && OMG_T_LEXW != 3) buf[r] = *reinterpret_cast<const v2d*>(u + 2 * q2);
+    }
+  };
+  int q = blockIdx.x;
+  if (q >= L.n) return;
+  issue(q, ring);
+  for (; q < L.n; q += G) {
+    const int b = xcd_box(q, L.n);
+    double* __restrict__ u = boxp(L, 1, b);
+    const double* __restrict__ f = boxp(L, 2, b);
+    // tid made opaque per box: the scatter / gather addresses are recomputed
+    // instead of being hoisted out of the box loop (~40 VGPRs)
+    int tv = tid;
+    asm volatile("" : "+v"(tv));
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      const int q2 = tv + T * r;
+      if (q2 < TL::NST / 2 && OMG_T_LEXW != 3) {
+        P[dense(2 * q2)] = buf[r].x;
+        P[dense(2 * q2 + 1)] = buf[r].y;
+      }
+    }
+    if (q + G < L.n) issue(q + G, ringn);
+    __syncthreads();
+#pragma unroll 1
+    for (int d0 = D0; d0 <= D1 && OMG_T_LEXW != 1; d0 += PF) {
+#pragma unroll
+      for (int s = 0; s < PF; s++) {
+        const int d = d0 + s;
+        if (d > D1) break;
+        // all stencil reads of the plane first, then the updates: the cells of
+        // a plane are independent, and a store between them would order every
+        // later read behind it
+        Nbr7 st[NL];
+        int w[NL];
+#pragma unroll
+        for (int r = 0; r < NL; r++) {
+          const int i0 = d - jk[r], i = min(max(i0, 1), NC);
+          const int c = cbase[r] + i;
+          st[r].c = P[c];
+          st[r].xm = P[c - 1];
+          st[r].xp = P[c + 1];
+          st[r].ym = P[c - S];
+          st[r].yp = P[c + S];
+          st[r].zm = P[c - S * S];
+          st[r].zp = P[c + S * S];
+          w[r] = (i0 >= 1 && i0 <= NC) ? c : -1;
+        }
+        double nv[NL];
+#pragma unroll
+        for (int r = 0; r < NL; r++) {
+          if constexpr (is_varop(OP)) {
+            const int i = min(max(d - jk[r], 1), NC), j = (cbase[r] / S) % S, k = cbase[r] / (S * S);
+            nv[r] = ags_value<OP>(K, st[r], load_eps<OP>(L, b, i, j, k), ring[s][r]);
+          } else {
+            nv[r] = gs_value<OP>(K, st[r], ring[s][r]);
+          }
+        }
+        // off-plane lanes store nothing (a shared dummy slot would serialise
+        // their stores on one bank)
+#pragma unroll
+        for (int r = 0; r < NL; r++)
+          if (w[r] >= 0) P[w[r]] = nv[r];
+        if (d + PF <= D1) rhs_plane(f, d + PF, ring[s]);
+        __syncthreads();
+      }
+    }
+    asm volatile("" : "+v"(tv));
+#pragma unroll
+    for (int r = 0; r < (HV + T - 1) / T; r++) {
+      const int q2 = tv + T * r;
+      if (q2 >= HV) break;
+      v2d v;
+      v.x = P[dense(2 * q2)];
+      v.y = P[dense(2 * q2 + 1)];
+      *reinterpret_cast<v2d*>(u + 2 * q2) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PF; s++)
+#pragma unroll
+      for (int r = 0; r < NL; r++) ring[s][r] = ringn[s][r];
+  }
 }
 
 template <int OP>
@@ -489,8 +655,46 @@ static void gs_lex_lds(const LevelView& L, double lambda, unsigned g, int block,
   }
 }
 
+#ifndef OMG_GS_T16
+#define OMG_GS_T16 256
+#endif
+// persistent grid: `per_cu` workgroups per CU (the LDS limit), a multiple of 8
+static unsigned gs_grid(int n, int per_cu) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const long long g = std::min<long long>(n, (long long)cus * per_cu);
+  return (unsigned)(g < 8 ? g : g & ~7LL);
+}
+
+template <int OP>
+static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
+  switch (L.nc) {
+    case 16:
+      // 46.6 KB of LDS per box: 3 workgroups per CU
+      k_gs_lex_wave<OP, 16, OMG_GS_T16, (3 * OMG_GS_T16 / 64 + 3) / 4>
+          <<<gs_grid(L.n, 3), OMG_GS_T16, 0, st>>>(L, lambda);
+      break;
+    default: k_gs_lex_wave<OP, 8, 64, 4><<<gs_grid(L.n, 16), 64, 0, st>>>(L, lambda); break;
+  }
+}
+
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st) {
   if (L.n == 0) return;
+  static const bool wg = getenv("OMG_GS_LEX_WG") != nullptr;
+  if ((L.nc == 16 || L.nc == 8) && (op == OP_LPL || op == OP_HELM) && !wg) {
+    // persistent, software-pipelined (k_gs_lex_wave); OMG_GS_LEX_WG: the
+    // one-box-per-workgroup kernel (which the variable-coefficient operators
+    // keep: their eps loads would spill the pipelined kernel)
+    if (op == OP_HELM)
+      gs_lex_wave<OP_HELM>(L, lambda, st);
+    else
+      gs_lex_wave<OP_LPL>(L, lambda, st);
+    return;
+  }
   const unsigned g = (unsigned)std::min(L.n, 65535 * 8);
   const int block = L.nc * L.nc >= 256 ? 256 : ((L.nc * L.nc + 63) / 64) * 64;
   if (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2) {

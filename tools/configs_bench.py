@@ -40,6 +40,11 @@ CONFIGS = {
            "3D Poisson 256^3, box 16, Dirichlet 0, GSRB"),
     "C3": ("16 512 512 512 10 v gsrb lpl 0 per sol 1 lb 0", 1,
            "3D Poisson 512^3, box 16, periodic, GSRB (bench.py's workload)"),
+    "C2-gs": ("16 256 256 256 10 v gs lpl 0 d0 sol 1 lb 0", 3,
+              "C2 with the tests' default lexicographic GS"),
+    "perf-gs": ("16 512 512 512 5 v gs lpl 0 d0 one 1 lbp 0", 1,
+                "tests/test_performance as shipped at 512^3: lexicographic GS, rhs = 1, Dirichlet 0, "
+                "mg_load_balance_parents"),
     "C4": ("16 128 128 128 10 v gsrb lpl 0 sol sol 2 lb 0", 3,
            "one-level-refined octree, 128^3 base, box 16, Dirichlet u, GSRB"),
     "C5-helm": ("16 256 256 256 10 v gsrb helm 10 d0 sol 1 lb 0", 3,

@@ -24,7 +24,8 @@ def main():
     if which == "vcycle_nofuse":
         os.environ["OMG_NO_FUSE_UP"] = "1"
     mg = omg.MG()
-    mg.smoother_type = T.MG_SMOOTHER_GSRB
+    # *_gs: the lexicographic Gauss-Seidel smoother (the reference tests' default)
+    mg.smoother_type = T.MG_SMOOTHER_GS if which.endswith("_gs") else T.MG_SMOOTHER_GSRB
     omg.mg_set_methods(mg)
     omg.mg_comm_init(mg)
     d = np.array([n, n, n])
@@ -39,6 +40,8 @@ def main():
     hi = mg.highest_lvl
     ops = {
         "smooth": lambda: c.call("smooth_boxes", hi, 1),
+        "smooth_gs": lambda: c.call("smooth_boxes", hi, 1),
+        "vcycle_gs": lambda: omg.mg_fas_vcycle(mg),
         "residual": lambda: c.call("residual_lvl", hi),
         "fill": lambda: c.call("fill_ghost_cells_lvl", hi, 1),
         "update_coarse": lambda: c.call("update_coarse", hi),
