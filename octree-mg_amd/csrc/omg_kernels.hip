@@ -177,14 +177,17 @@ __global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) 
 // its cells is read from L2 GS_PF planes ahead (one wave per box hides no
 // latency by itself).
 #ifndef OMG_GS_PF
-#define OMG_GS_PF 8
+#define OMG_GS_PF 4
 #endif
 // timing-only (wrong results): 1 = no sweep, 2 = no rhs loads, 3 = no box load
 #ifndef OMG_T_LEXW
 #define OMG_T_LEXW 0
 #endif
-template <int NC>
-constexpr int gs_wave_lds() { return (NC + 2) * (NC + 2) * (NC + 2); }
+// + one dummy slot per thread: off-plane lanes store there, so the sweep is
+// branch-free and the same every plane (the compiler then keeps the rhs
+// prefetch in flight instead of draining it at each plane)
+template <int NC, int T>
+constexpr int gs_wave_lds() { return (NC + 2) * (NC + 2) * (NC + 2) + T; }
 
 // WPS: waves per SIMD the register budget must allow (the LDS-bound
 // workgroups per CU x T/64 / 4)
@@ -193,7 +196,9 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
   using TL = Tl<NC>;
   constexpr int S = NC + 2, NL = (NC * NC + T - 1) / T, H = TL::H, HV = TL::HV, FS = TL::FS;
   constexpr int D0 = 3, D1 = 3 * NC, PF = OMG_GS_PF, NQ = (TL::NST / 2 + T - 1) / T;
-  __shared__ double P[gs_wave_lds<NC>()];
+  // planes D0 .. D1 padded to whole groups of PF (the padding planes update nothing)
+  constexpr int DP = D0 + ((D1 - D0 + PF) / PF) * PF - 1;
+  __shared__ double P[gs_wave_lds<NC, T>()];
   const int tid = threadIdx.x, G = gridDim.x;
   const OpCoef<OP> K(L, lambda);
   // stored slot q -> dense index (edges and corners are neither stored nor read)
@@ -234,6 +239,20 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
   // 8, so every box of one workgroup sits on its XCD's run, xcd_box).  The
   // next box's stored data and first rhs planes are loaded into registers
   // while this box sweeps.
+  // this thread's LDS slots for the scatter (stored slot 2 q2, 2 q2 + 1) and
+  // the gather (interior slots), as 16-bit pairs: the same for every box
+  constexpr int NG2 = (HV + T - 1) / T;
+  unsigned scat[NQ], gath[NG2];
+#pragma unroll
+  for (int r = 0; r < NQ; r++) {
+    const int q2 = min(tid + T * r, TL::NST / 2 - 1);
+    scat[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
+  }
+#pragma unroll
+  for (int r = 0; r < NG2; r++) {
+    const int q2 = min(tid + T * r, HV - 1);
+    gath[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
+  }
   double ring[PF][NL], ringn[PF][NL];
   v2d buf[NQ];
   auto issue = [&](int q, double (*rg)[NL]) {
@@ -255,26 +274,21 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
     const int b = xcd_box(q, L.n);
     double* __restrict__ u = boxp(L, 1, b);
     const double* __restrict__ f = boxp(L, 2, b);
-    // tid made opaque per box: the scatter / gather addresses are recomputed
-    // instead of being hoisted out of the box loop (~40 VGPRs)
-    int tv = tid;
-    asm volatile("" : "+v"(tv));
 #pragma unroll
     for (int r = 0; r < NQ; r++) {
-      const int q2 = tv + T * r;
+      const int q2 = tid + T * r;
       if (q2 < TL::NST / 2 && OMG_T_LEXW != 3) {
-        P[dense(2 * q2)] = buf[r].x;
-        P[dense(2 * q2 + 1)] = buf[r].y;
+        P[scat[r] & 0xffff] = buf[r].x;
+        P[scat[r] >> 16] = buf[r].y;
       }
     }
     if (q + G < L.n) issue(q + G, ringn);
     __syncthreads();
 #pragma unroll 1
-    for (int d0 = D0; d0 <= D1 && OMG_T_LEXW != 1; d0 += PF) {
+    for (int d0 = D0; d0 <= DP && OMG_T_LEXW != 1; d0 += PF) {
 #pragma unroll
       for (int s = 0; s < PF; s++) {
         const int d = d0 + s;
-        if (d > D1) break;
         // all stencil reads of the plane first, then the updates: the cells of
         // a plane are independent, and a store between them would order every
         // later read behind it
@@ -291,7 +305,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
           st[r].yp = P[c + S];
           st[r].zm = P[c - S * S];
           st[r].zp = P[c + S * S];
-          w[r] = (i0 >= 1 && i0 <= NC) ? c : -1;
+          w[r] = (i0 >= 1 && i0 <= NC) ? c : S * S * S + tid;
         }
         double nv[NL];
 #pragma unroll
@@ -303,23 +317,19 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
             nv[r] = gs_value<OP>(K, st[r], ring[s][r]);
           }
         }
-        // off-plane lanes store nothing (a shared dummy slot would serialise
-        // their stores on one bank)
 #pragma unroll
-        for (int r = 0; r < NL; r++)
-          if (w[r] >= 0) P[w[r]] = nv[r];
-        if (d + PF <= D1) rhs_plane(f, d + PF, ring[s]);
+        for (int r = 0; r < NL; r++) P[w[r]] = nv[r];
+        rhs_plane(f, d + PF, ring[s]);   // past the last plane: clamped, unused
         __syncthreads();
       }
     }
-    asm volatile("" : "+v"(tv));
 #pragma unroll
-    for (int r = 0; r < (HV + T - 1) / T; r++) {
-      const int q2 = tv + T * r;
+    for (int r = 0; r < NG2; r++) {
+      const int q2 = tid + T * r;
       if (q2 >= HV) break;
       v2d v;
-      v.x = P[dense(2 * q2)];
-      v.y = P[dense(2 * q2 + 1)];
+      v.x = P[gath[r] & 0xffff];
+      v.y = P[gath[r] >> 16];
       *reinterpret_cast<v2d*>(u + 2 * q2) = v;
     }
     __syncthreads();
