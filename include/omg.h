@@ -165,6 +165,31 @@ int omg_set_rhs(omg_ctx *ctx, double f1, double f2);
 int omg_diffusion_solve(omg_ctx *ctx, int op, double dt, double diffusion_coeff, int order,
                         double max_res, int *n_vcycles, double *res);
 
+/* m_free_space (src/m_free_space.f90).  omg_poisson_free_3d is
+ * mg_poisson_free_3d (:36-214): on the first call (new_rhs must be set) and
+ * whenever the FFT level changes, rhs is restricted down to the highest
+ * uniform level with at most max_fft_frac of the unknowns and the free-space
+ * Green's function of that grid is built (PSolver's createKernel, geocode
+ * 'F', poisson_3d_fft/build_kernel.f90:55-199); with new_rhs the Poisson
+ * problem is solved there by FFT convolution (PSolver, psolver_main.f90:
+ * 91-556), phi gets Dirichlet values interpolated from that solution on every
+ * physical face of every level (ghost_cells_free_bc + mg_phi_bc_store) and
+ * the solution as initial guess (restricted down, prolonged up); then one FMG
+ * (fmgcycle) or V-cycle runs unless the FFT level is the highest.  r_min:
+ * mg%r_min of the domain (3 doubles); box_r_min: mg%boxes(id)%r_min, 3 per
+ * box indexed by id-1, or NULL (then r_min + (ix-1)*nc*dr).  Operators other
+ * than the Laplacian are refused ("mg_poisson_free_3d: laplacian operator
+ * required"), as is a first call without new_rhs.  The transforms run on the
+ * device (hipFFT); results agree with the reference at round-off.
+ * omg_free_planes: the FFT level, nx (3 ints: the FFT level's domain + 2) and,
+ * if planes is not NULL, the six boundary planes bc_x0, bc_x1 (nx2*nx3 each),
+ * bc_y0, bc_y1 (nx1*nx3), bc_z0, bc_z1 (nx1*nx2), first index fastest
+ * (m_free_space.f90:163-171), for host copies of the boundary callback. */
+int omg_poisson_free_3d(omg_ctx *ctx, int new_rhs, double max_fft_frac, int fmgcycle,
+                        int want_max_res, double *max_res, const double *r_min,
+                        const double *box_r_min);
+int omg_free_planes(omg_ctx *ctx, int *fft_lvl, int *nx, double *planes);
+
 /* The communication plan of level lvl as built by omg_tree_setup: transfer
  * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,
  * 3 refinement-boundary faces, 4 copies of the host's boxes of a replicated

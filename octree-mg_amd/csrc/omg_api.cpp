@@ -7,6 +7,7 @@
 // exchange of the reference (m_communication.f90:37-66) is one grouped RCCL
 // send/recv round over xGMI carrying device-packed buffers.
 #include <hip/hip_runtime.h>
+#include <hipfft/hipfft.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -24,6 +25,8 @@
 #include <vector>
 
 #include "../../include/omg.h"
+#include "omg_free.h"
+#include "omg_free_gequad.h"
 #include "omg_kernels.h"
 
 using namespace omg;
@@ -194,6 +197,32 @@ struct omg_loop {
   std::map<Key, hipEvent_t> acks;               // (receiver, sender, seq) -> copies done
   std::map<long long, std::vector<double>> vals;
   std::map<long long, int> n_in, n_out;
+};
+
+// m_free_space's free_bc (src/m_free_space.f90:9-24) on the device: the FFT
+// grid, the kernel spectrum, the boundary planes and the gather plan of the
+// FFT level's right-hand side.
+struct omg_free_state {
+  bool initialized = false;
+  int fft_lvl = INT_MIN;
+  omg::FreeGrid G{};
+  double r_min[3] = {0, 0, 0};       // mg%r_min of the domain
+  double* d_R = nullptr;             // real padded grid [N3][N2][N1] (density, then potential)
+  double2* d_Z = nullptr;            // its D2Z spectrum [N3][N2][N1/2+1]
+  double* d_karray = nullptr;        // kernel spectrum * scal, same shape, real
+  double* d_planes = nullptr;        // bc_x0, bc_x1, bc_y0, bc_y1, bc_z0, bc_z1
+  hipfftHandle fwd = 0, inv = 0;
+  bool have_plans = false;
+  // my boxes at the FFT level: local index and ix
+  int n_my = 0;
+  int* d_my = nullptr;
+  int* d_my_ix = nullptr;
+  // the other ranks' boxes (multi-rank, FFT level not replicated)
+  omg::Transfer gather;
+  double* d_send = nullptr;
+  double* d_recv = nullptr;
+  int* d_recv_ix = nullptr;
+  omg::FreePlaneGeom P{};
 };
 
 namespace {
@@ -1207,10 +1236,344 @@ void diffusion_solve(omg_ctx* c, int op, double dt, double coeff, int order, dou
 }
 
 // ---------------------------------------------------------------------------
+// mg_phi_bc_store (m_ghost_cells.f90:66-117): the bc values of phi go into
+// the rhs ghost cells and the bc type into the neighbour slot.
+void phi_bc_store(omg_ctx* c) {
+  phi_dirty_all(c);
+  for (auto& kv : c->levels) {
+    Level& L = kv.second;
+    if (!L.n) continue;
+    GcBC g = bc_for(c, kv.first, 1);
+    g.phi_stored = 0;
+    launch_phi_bc_store(L.view(), g, L.d_nba, c->stream);
+    HIPCHK(hipMemcpyAsync(L.h_nba.data(), L.d_nba, sizeof(int) * L.h_nba.size(), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int b = 0; b < L.n; b++)
+      for (int nb = 1; nb <= 6; nb++)
+        if (L.h_nbk[(size_t)b * 6 + nb - 1] == NB_PHYS)
+          c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = L.h_nba[(size_t)b * 6 + nb - 1];
+  }
+  c->phi_bc_data_stored = 1;
+}
+
+// ---------------------------------------------------------------------------
+// Free-space boundary conditions: mg_poisson_free_3d (m_free_space.f90:36-214)
+// with PSolver's solve on the device (omg_free.hip).
+
+#define FFTCHK(x)                                                                          \
+  do {                                                                                     \
+    hipfftResult r_ = (x);                                                                 \
+    if (r_ != HIPFFT_SUCCESS) throw OmgError(std::string(#x) + ": hipFFT error " + std::to_string((int)r_)); \
+  } while (0)
+
+// smallest even n >= m whose prime factors are 2, 3, 5, 7 (the transform
+// length of one padded axis; any n >= 2*nx gives the same linear convolution)
+int fft_length(int m) {
+  for (int n = std::max(m, 2);; n++) {
+    if (n & 1) continue;
+    int r = n;
+    for (int f : {2, 3, 5, 7})
+      while (r % f == 0) r /= f;
+    if (r == 1) return n;
+  }
+}
+
+void free_grid_release(omg_free_state* S) {
+  dfree(S->d_R);
+  dfree(S->d_Z);
+  dfree(S->d_karray);
+  dfree(S->d_planes);
+  dfree(S->d_my);
+  dfree(S->d_my_ix);
+  dfree(S->d_send);
+  dfree(S->d_recv);
+  dfree(S->d_recv_ix);
+  dfree(S->gather.d_send_items);
+  dfree(S->gather.d_recv_items);
+  S->gather = Transfer();
+  if (S->have_plans) {
+    (void)hipfftDestroy(S->fwd);
+    (void)hipfftDestroy(S->inv);
+    S->have_plans = false;
+  }
+  S->initialized = false;
+  S->fft_lvl = INT_MIN;
+}
+
+void free_state_destroy(omg_ctx* c) {
+  if (!c->free_state) return;
+  free_grid_release(c->free_state);
+  delete c->free_state;
+  c->free_state = nullptr;
+}
+
+// createKernel(geocode 'F', nx(1), nx(3), nx(3), dr, itype_scf = 8)
+// (m_free_space.f90:118-120, build_kernel.f90:55-199, 884-1164): the kernel
+// spectrum * scal on the grid S->G.
+void free_create_kernel(omg_ctx* c, omg_free_state* S, const double h[3]) {
+  const FreeGrid& G = S->G;
+  // the reference creates the kernel for (nx(1), nx(3), nx(3)); the extents
+  // of the tables are the grid's own (equal whenever ny == nz)
+  const int n0k[3] = {G.nx[0], G.nx[2], G.nx[2]};
+  int n_range = 2 * kFreeItype;
+  for (int d = 0; d < 3; d++) n_range = std::max(n_range, G.n0[d]);
+  if (n_range > kFreeMaxRange) throw OmgError("mg_poisson_free_3d: FFT grid too large for the kernel tables");
+  double a[3];
+  for (int d = 0; d < 3; d++) a[d] = h[d] * (double)n0k[d];
+  const double factor = 1.0 / std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  const double factor2 = 1.0 / (a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  const bool cube = h[0] == h[1] && h[1] == h[2];
+  // per Gaussian in the order the reference sums them (i_gauss = 89 .. 1):
+  // weight, starting exponent and number of scf_recursion passes per axis
+  std::vector<double> w(kFreeNGauss), p0(3 * kFreeNGauss);
+  std::vector<int> nit(3 * kFreeNGauss);
+  for (int g = 0; g < kFreeNGauss; g++) {
+    const int ig = kFreeNGauss - 1 - g;
+    const double pg = factor2 * kGequadP[ig];
+    w[g] = factor * kGequadW[ig];
+    for (int d = 0; d < 3; d++) {
+      const double pref = 1.0 / (cube ? h[0] * h[0] : h[d] * h[d]);
+      long n = std::lround((std::log(pg) - std::log(pref)) / std::log(4.0));
+      if (n <= 0) n = 0;
+      nit[3 * g + d] = (int)n;
+      p0[3 * g + d] = n == 0 ? pg : pg / std::pow(4.0, (double)n);
+    }
+  }
+  int n0max = std::max(G.n0[0], std::max(G.n0[1], G.n0[2]));
+  double *d_p0 = nullptr, *d_w = nullptr, *d_tab = nullptr, *d_work = nullptr, *d_F = nullptr;
+  int* d_nit = nullptr;
+  const int fmax = std::max(G.N[0], std::max(G.N[1], G.N[2])) / 2 + 1;
+  d_p0 = to_device(p0);
+  d_w = to_device(w);
+  d_nit = to_device(nit);
+  dmalloc(&d_tab, sizeof(double) * 3 * kFreeNGauss * (size_t)n0max, true);
+  dmalloc(&d_work, sizeof(double) * 3 * kFreeNGauss * (size_t)(n_range + 1), true);
+  dmalloc(&d_F, sizeof(double) * 3 * kFreeNGauss * (size_t)fmax, true);
+  FreeTabArgs A;
+  A.p0 = d_p0;
+  A.n_iter = d_nit;
+  for (int d = 0; d < 3; d++) {
+    A.h[d] = cube ? h[0] : h[d];
+    A.n0[d] = G.n0[d];
+  }
+  A.cube = cube;
+  A.n_range = n_range;
+  A.n0max = n0max;
+  A.tab = d_tab;
+  A.work = d_work;
+  launch_free_tables(A, c->stream);
+  launch_free_dft(d_tab, n0max, G, d_F, fmax, c->stream);
+  const size_t nk = (size_t)(G.N[0] / 2 + 1) * G.N[1] * G.N[2];
+  dmalloc(&S->d_karray, sizeof(double) * nk);
+  // PSolver's scal = hx*hy*hz/(n1*n2*n3) (psolver_main.f90:297)
+  const double scal = h[0] * h[1] * h[2] / ((double)G.N[0] * (double)G.N[1] * (double)G.N[2]);
+  launch_free_karray(d_F, fmax, d_w, G, scal, S->d_karray, c->stream);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dfree(d_p0);
+  dfree(d_w);
+  dfree(d_nit);
+  dfree(d_tab);
+  dfree(d_work);
+  dfree(d_F);
+}
+
+// the FFT grid, its plans and the gather plan of the FFT level
+void free_new_grid(omg_ctx* c, omg_free_state* S, int fft_lvl, const int nx[3], const double h[3]) {
+  FreeGrid& G = S->G;
+  for (int d = 0; d < 3; d++) {
+    G.nx[d] = nx[d];
+    G.n0[d] = nx[d];
+    G.N[d] = fft_length(2 * nx[d]);
+  }
+  free_create_kernel(c, S, h);
+  const size_t nr = (size_t)G.N[0] * G.N[1] * G.N[2], nz = (size_t)(G.N[0] / 2 + 1) * G.N[1] * G.N[2];
+  dmalloc(&S->d_R, sizeof(double) * nr);
+  dmalloc(&S->d_Z, sizeof(double2) * nz);
+  dmalloc(&S->d_planes, sizeof(double) * 2 *
+                            ((size_t)nx[1] * nx[2] + (size_t)nx[0] * nx[2] + (size_t)nx[0] * nx[1]));
+  FFTCHK(hipfftPlan3d(&S->fwd, G.N[2], G.N[1], G.N[0], HIPFFT_D2Z));
+  FFTCHK(hipfftPlan3d(&S->inv, G.N[2], G.N[1], G.N[0], HIPFFT_Z2D));
+  S->have_plans = true;
+  FFTCHK(hipfftSetStream(S->fwd, c->stream));
+  FFTCHK(hipfftSetStream(S->inv, c->stream));
+  // my boxes at the FFT level (a replicated level holds all of them)
+  Level* L = level_ptr(c, fft_lvl);
+  std::vector<int> my, my_ix;
+  if (L)
+    for (int b = 0; b < L->n; b++) {
+      my.push_back(b);
+      for (int d = 0; d < 3; d++) my_ix.push_back(c->ix[(size_t)(L->ids[b] - 1) * 3 + d]);
+    }
+  S->n_my = (int)my.size();
+  S->d_my = to_device(my);
+  S->d_my_ix = to_device(my_ix);
+  // every other rank's boxes, unless the level is replicated: my rhs goes to
+  // every peer (one packed copy, m_free_space.f90:152-153's allreduce)
+  if (c->n_ranks > 1 && !(L && L->replicated)) {
+    const int nc = c->bsl[fft_lvl];
+    Transfer& T = S->gather;
+    T.item_doubles = nc * nc * nc;
+    std::vector<Rec> snd, rcv;
+    for (int id : c->ids[fft_lvl]) {
+      const int r = c->rank_of[id - 1];
+      if (r == c->rank) {
+        for (int q = 0; q < c->n_ranks; q++)
+          if (q != c->rank) snd.push_back({q, (long long)id, c->local_index[id], 0});
+      } else {
+        rcv.push_back({r, (long long)id, id, 0});
+      }
+    }
+    T.send = group(snd, 1);
+    T.recv = group(rcv, 1);
+    finalize_transfer(T);
+    for (auto& p : T.send) p.offset = 0;   // the same packed boxes for every peer
+    std::vector<int> rix;
+    for (auto& p : T.recv)
+      for (int id : p.items)
+        for (int d = 0; d < 3; d++) rix.push_back(c->ix[(size_t)(id - 1) * 3 + d]);
+    S->d_recv_ix = to_device(rix);
+    dmalloc(&S->d_send, sizeof(double) * (size_t)S->n_my * T.item_doubles);
+    dmalloc(&S->d_recv, sizeof(double) * (size_t)T.n_recv * T.item_doubles);
+  }
+  S->fft_lvl = fft_lvl;
+}
+
+// the interpolated Dirichlet values of phi on every physical face of every
+// box here (ghost_cells_free_bc via mg_phi_bc_store, m_free_space.f90:174,
+// 216-270) as phi's boundary table, then mg_phi_bc_store itself
+void free_store_bc(omg_ctx* c, omg_free_state* S, const double* box_r_min) {
+  const int k = 0;   // phi
+  for (auto& kv : c->d_face_off_lvl[k]) dfree(kv.second);
+  for (auto& kv : c->d_face_type_lvl[k]) dfree(kv.second);
+  c->d_face_off_lvl[k].clear();
+  c->d_face_type_lvl[k].clear();
+  dfree(c->d_face_data[k]);
+  std::vector<FreeFace> faces;
+  long long n_data = 0;
+  for (auto& kv : c->levels) {
+    Level& L = kv.second;
+    if (!L.n) continue;
+    const std::vector<double>& dr = c->drl[kv.first];
+    std::vector<long long> off(L.n * 6, -1);
+    std::vector<int> typ(L.n * 6, 0);
+    for (int b = 0; b < L.n; b++)
+      for (int nb = 1; nb <= 6; nb++) {
+        if (L.h_nbk[(size_t)b * 6 + nb - 1] != NB_PHYS) continue;
+        const int id = L.ids[b];
+        FreeFace f;
+        for (int d = 0; d < 3; d++) {
+          f.rmin[d] = box_r_min ? box_r_min[(size_t)(id - 1) * 3 + d]
+                                : S->r_min[d] + (double)((c->ix[(size_t)(id - 1) * 3 + d] - 1) * L.nc) * dr[d];
+          f.dr[d] = dr[d];
+        }
+        f.off = n_data;
+        f.nb = nb;
+        f.nc = L.nc;
+        faces.push_back(f);
+        off[(size_t)b * 6 + nb - 1] = n_data;
+        typ[(size_t)b * 6 + nb - 1] = OMG_BC_DIRICHLET;
+        n_data += (long long)L.nc * L.nc;
+      }
+    c->d_face_off_lvl[k][kv.first] = to_device(off);
+    c->d_face_type_lvl[k][kv.first] = to_device(typ);
+  }
+  for (int nb = 0; nb < 6; nb++) {
+    c->bc[k].type[nb] = OMG_BC_DIRICHLET;
+    c->bc[k].value[nb] = 0.0;
+  }
+  dmalloc(&c->d_face_data[k], sizeof(double) * std::max(n_data, 1LL));
+  FreeFace* d_faces = to_device(faces);
+  launch_free_bc_faces(d_faces, (int)faces.size(), S->d_planes, S->G, S->P, c->d_face_data[k], c->stream);
+  phi_bc_store(c);   // synchronises the stream
+  dfree(d_faces);
+}
+
+// mg_poisson_free_3d (m_free_space.f90:36-214)
+double poisson_free_3d(omg_ctx* c, bool new_rhs, double max_fft_frac, bool fmgcycle, bool want_max_res,
+                       const double* r_min, const double* box_r_min) {
+  if (!c->free_state) c->free_state = new omg_free_state;
+  omg_free_state* S = c->free_state;
+  if (!S->initialized && !new_rhs)
+    throw OmgError("mg_poisson_free_3d: first call requires new_rhs = .true.");
+  if (c->op != OP_LPL) throw OmgError("mg_poisson_free_3d: laplacian operator required");
+  // mg_number_of_unknowns (m_data_structures.f90:482-492)
+  long long n_total = 0;
+  for (int l = c->first_normal; l <= c->highest; l++) n_total += (long long)c->leaves[l].size();
+  n_total *= (long long)c->box_size * c->box_size * c->box_size;
+  // mg_highest_uniform_lvl (m_data_structures.f90:469-479)
+  int lvl = c->first_normal;
+  for (; lvl <= c->highest - 1; lvl++)
+    if (!c->leaves[lvl].empty() && !c->parents[lvl].empty()) break;
+  // the highest level small enough for the FFT solve (:83-90)
+  for (; lvl >= c->lowest + 1; lvl--) {
+    const long long n_lvl = (long long)c->ids[lvl].size() * c->box_size * c->box_size * c->box_size;
+    if ((double)n_lvl <= max_fft_frac * (double)n_total) break;
+  }
+  const int fft_lvl = lvl;
+  const bool new_grid = !S->initialized || S->fft_lvl != fft_lvl;
+  // domain_size_lvl(:, fft_lvl) + 2 (:95)
+  int nx[3] = {0, 0, 0};
+  const int nc_f = c->bsl[fft_lvl];
+  for (int id : c->ids[fft_lvl])
+    for (int d = 0; d < 3; d++) nx[d] = std::max(nx[d], c->ix[(size_t)(id - 1) * 3 + d] * nc_f);
+  for (int d = 0; d < 3; d++) nx[d] += 2;
+  const double h[3] = {c->drl[fft_lvl][0], c->drl[fft_lvl][1], c->drl[fft_lvl][2]};
+  if (S->initialized && new_grid) free_grid_release(S);
+  for (int d = 0; d < 3; d++) S->r_min[d] = r_min ? r_min[d] : 0.0;
+  if (new_grid) {
+    for (int l = c->highest; l >= fft_lvl + 1; l--) restrict_lvl(c, 2, l);   // :113-115
+    free_new_grid(c, S, fft_lvl, nx, h);
+    // interp_bc's plane geometry (:128-139): tangential dims of each face
+    const int tdim[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+    for (int d = 0; d < 3; d++)
+      for (int q = 0; q < 2; q++) {
+        S->P.inv_dr[d][q] = 1.0 / h[tdim[d][q]];
+        S->P.r_min[d][q] = S->r_min[tdim[d][q]] - 0.5 * h[tdim[d][q]];
+      }
+  }
+  if (new_rhs) {
+    const FreeGrid& G = S->G;
+    const double rhs_fac = -1.0 / (4.0 * std::acos(-1.0));   // :67
+    Level* L = level_ptr(c, fft_lvl);
+    const size_t nr = (size_t)G.N[0] * G.N[1] * G.N[2], nz = (size_t)(G.N[0] / 2 + 1) * G.N[1] * G.N[2];
+    {
+      Prof p(c, "free_fft_solve", (double)nr, fft_lvl);
+      HIPCHK(hipMemsetAsync(S->d_R, 0, sizeof(double) * nr, c->stream));
+      if (L) launch_free_gather(L->view(), S->d_my, S->d_my_ix, S->n_my, G, rhs_fac, S->d_R, c->stream);
+      Transfer& T = S->gather;
+      if (T.n_send || T.n_recv) {
+        if (L) launch_free_pack(L->view(), S->d_my, S->n_my, S->d_send, c->stream);
+        exchange(c, T, S->d_send, S->d_recv);
+        launch_free_scatter(S->d_recv, S->d_recv_ix, T.n_recv, nc_f, G, rhs_fac, S->d_R, c->stream);
+      }
+      FFTCHK(hipfftExecD2Z(S->fwd, S->d_R, (hipfftDoubleComplex*)S->d_Z));
+      launch_free_mul(S->d_Z, S->d_karray, (long long)nz, c->stream);
+      FFTCHK(hipfftExecZ2D(S->inv, (hipfftDoubleComplex*)S->d_Z, S->d_R));
+      launch_free_planes(S->d_R, G, S->d_planes, c->stream);
+    }
+    free_store_bc(c, S, box_r_min);
+    // the solution as the initial guess on the FFT level, incl. ghosts (:176-183)
+    if (L) launch_free_guess(L->view(), S->d_my, S->d_my_ix, S->n_my, G, S->d_R, c->stream);
+    phi_dirty(c, fft_lvl);
+    for (int l = fft_lvl; l >= c->lowest + 1; l--) restrict_lvl(c, 1, l);   // :186-188
+    for (int l = fft_lvl; l <= c->highest - 1; l++) {                        // :191-195
+      prolong(c, l, 1, 1, 0);
+      fill_gc_lvl(c, l + 1, 1);
+    }
+    S->initialized = true;
+  }
+  if (fft_lvl < c->highest)   // :201-208
+    return fmgcycle ? fas_fmg(c, true, want_max_res) : fas_vcycle(c, c->lowest - 1, want_max_res, true);
+  return 0.0;
+}
+
+// ---------------------------------------------------------------------------
 // Plan builder (device side of mg_allocate_storage, m_allocate_storage.f90:51-99,
 // and of the three buffer dry runs m_ghost_cells.f90:17-62, m_restrict.f90:
 // 16-69, m_prolong.f90:16-48).
 void free_levels(omg_ctx* c) {
+  free_state_destroy(c);   // the FFT level belongs to the old tree
   for (auto& kv : c->levels) {
     Level& L = kv.second;
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
@@ -2008,22 +2371,31 @@ int omg_subtract_mean(omg_ctx* c, int iv, int include_ghostcells) {
 int omg_phi_bc_store(omg_ctx* c) {
   return guarded([&] {
     enter(c);
-    phi_dirty_all(c);
-    for (auto& kv : c->levels) {
-      Level& L = kv.second;
-      if (!L.n) continue;
-      GcBC g = bc_for(c, kv.first, 1);
-      g.phi_stored = 0;
-      launch_phi_bc_store(L.view(), g, L.d_nba, c->stream);
-      HIPCHK(hipMemcpyAsync(L.h_nba.data(), L.d_nba, sizeof(int) * L.h_nba.size(), hipMemcpyDeviceToHost,
-                            c->stream));
+    phi_bc_store(c);
+  });
+}
+
+int omg_poisson_free_3d(omg_ctx* c, int new_rhs, double max_fft_frac, int fmgcycle, int want_max_res,
+                        double* max_res, const double* r_min, const double* box_r_min) {
+  return guarded([&] {
+    enter(c);
+    const double r = poisson_free_3d(c, new_rhs != 0, max_fft_frac, fmgcycle != 0, want_max_res != 0, r_min,
+                                     box_r_min);
+    if (max_res && want_max_res) *max_res = r;
+  });
+}
+
+int omg_free_planes(omg_ctx* c, int* fft_lvl, int* nx, double* planes) {
+  return guarded([&] {
+    omg_free_state* S = c->free_state;
+    if (!S || !S->initialized) throw OmgError("omg_free_planes: no free-space solve yet");
+    *fft_lvl = S->fft_lvl;
+    for (int d = 0; d < 3; d++) nx[d] = S->G.nx[d];
+    if (planes) {
+      const size_t n = 2 * ((size_t)nx[1] * nx[2] + (size_t)nx[0] * nx[2] + (size_t)nx[0] * nx[1]);
+      HIPCHK(hipMemcpyAsync(planes, S->d_planes, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
-      for (int b = 0; b < L.n; b++)
-        for (int nb = 1; nb <= 6; nb++)
-          if (L.h_nbk[(size_t)b * 6 + nb - 1] == NB_PHYS)
-            c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = L.h_nba[(size_t)b * 6 + nb - 1];
     }
-    c->phi_bc_data_stored = 1;
   });
 }
 

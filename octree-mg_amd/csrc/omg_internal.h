@@ -1,9 +1,9 @@
 // omg_internal.h — device data model of the MI355X octree-mg V-cycle.
 //
 // Every octree level that this rank owns boxes on is one contiguous HBM arena
-//     data[var][box][stride]        stride = pad64((nc+2)^3) doubles
-// with boxes in the reference's my_ids order and each box stored exactly like
-// the reference's cc(0:nc+1,0:nc+1,0:nc+1) (i fastest).  Per-level topology
+//     data[var][box][stride]        stride = stored_cells(nc) padded to 64 doubles
+// with boxes in the reference's my_ids order; inside a box, the interior split
+// by red-black colour and the six ghost faces (omg_device.h).  Per-level topology
 // tables let one kernel launch cover a whole level: for every (box, face) a
 // kind + argument (local neighbour index / physical bc code / refinement-
 // boundary record / halo receive slot), parent and child offsets for the grid
@@ -181,7 +181,8 @@ struct KStat {
 
 }  // namespace omg
 
-struct omg_loop;   // in-process loopback transport (omg_api.cpp)
+struct omg_loop;          // in-process loopback transport (omg_api.cpp)
+struct omg_free_state;    // free-space boundary conditions (omg_api.cpp, omg_free.hip)
 
 namespace omg {
 struct TailArgs;   // omg_kernels.h
@@ -241,6 +242,7 @@ struct omg_ctx {
   double* h_scalar = nullptr;          // pinned host scratch
   double* d_stage = nullptr;           // upload/download staging (reference layout)
   size_t stage_n = 0;
+  omg_free_state* free_state = nullptr;   // m_free_space's free_bc (created on first use)
   // profiling
   bool profiling = false;
   std::map<std::string, omg::KStat> stats;
