@@ -182,13 +182,14 @@ int omg_diffusion_solve(omg_ctx *ctx, int op, double dt, double diffusion_coeff,
  * required"), as is a first call without new_rhs.  The transforms run on the
  * device (hipFFT); results agree with the reference at round-off.
  * omg_free_planes: the FFT level, nx (3 ints: the FFT level's domain + 2) and,
- * if planes is not NULL, the six boundary planes bc_x0, bc_x1 (nx2*nx3 each),
+ * if planes holds cap >= 2*(nx2*nx3 + nx1*nx3 + nx1*nx2) doubles (else
+ * nothing is copied), the six boundary planes bc_x0, bc_x1 (nx2*nx3 each),
  * bc_y0, bc_y1 (nx1*nx3), bc_z0, bc_z1 (nx1*nx2), first index fastest
  * (m_free_space.f90:163-171), for host copies of the boundary callback. */
 int omg_poisson_free_3d(omg_ctx *ctx, int new_rhs, double max_fft_frac, int fmgcycle,
                         int want_max_res, double *max_res, const double *r_min,
                         const double *box_r_min);
-int omg_free_planes(omg_ctx *ctx, int *fft_lvl, int *nx, double *planes);
+int omg_free_planes(omg_ctx *ctx, int *fft_lvl, int *nx, double *planes, long long cap);
 
 /* The communication plan of level lvl as built by omg_tree_setup: transfer
  * `which` (0 ghost faces, 1 restriction to lvl-1, 2 prolongation from lvl-1,

@@ -2385,14 +2385,14 @@ int omg_poisson_free_3d(omg_ctx* c, int new_rhs, double max_fft_frac, int fmgcyc
   });
 }
 
-int omg_free_planes(omg_ctx* c, int* fft_lvl, int* nx, double* planes) {
+int omg_free_planes(omg_ctx* c, int* fft_lvl, int* nx, double* planes, long long cap) {
   return guarded([&] {
     omg_free_state* S = c->free_state;
     if (!S || !S->initialized) throw OmgError("omg_free_planes: no free-space solve yet");
     *fft_lvl = S->fft_lvl;
     for (int d = 0; d < 3; d++) nx[d] = S->G.nx[d];
-    if (planes) {
-      const size_t n = 2 * ((size_t)nx[1] * nx[2] + (size_t)nx[0] * nx[2] + (size_t)nx[0] * nx[1]);
+    const size_t n = 2 * ((size_t)nx[1] * nx[2] + (size_t)nx[0] * nx[2] + (size_t)nx[0] * nx[1]);
+    if (planes && cap >= (long long)n) {
       HIPCHK(hipMemcpyAsync(planes, S->d_planes, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
     }

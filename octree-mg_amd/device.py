@@ -58,7 +58,7 @@ SIGNATURES = {
     "omg_set_rhs": (_I, [_P, _D, _D]),
     "omg_diffusion_solve": (_I, [_P, _I, _D, _D, _I, _D, C.POINTER(_I), C.POINTER(_D)]),
     "omg_poisson_free_3d": (_I, [_P, _I, _D, _I, _I, C.POINTER(_D), _DP, C.c_void_p]),
-    "omg_free_planes": (_I, [_P, C.POINTER(_I), _IP, C.c_void_p]),
+    "omg_free_planes": (_I, [_P, C.POINTER(_I), _IP, C.c_void_p, _LL]),
     "omg_synchronize": (_I, [_P]),
     "omg_stream": (_P, [_P]),
     "omg_set_profiling": (_I, [_P, _I]),

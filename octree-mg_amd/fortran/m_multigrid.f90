@@ -57,6 +57,7 @@ module m_multigrid
   public :: mg_gpu_to_host
   public :: mg_gpu_to_device
   public :: mg_gpu_diffusion_solve
+  public :: mg_gpu_poisson_free_3d
 
 contains
 
@@ -216,6 +217,49 @@ contains
     call mg_timer_end(mg%timers(timer_device_fmg))
     call sync_out(mg)
   end subroutine mg_gpu_diffusion_solve
+
+  !> mg_poisson_free_3d's work on the GPU for the drop-in m_free_space
+  !> (omg_poisson_free_3d: FFT level, Green's function, hipFFT solve,
+  !> boundary table, guess, FMG or V-cycle; m_free_space.f90:36-214).  The
+  !> six boundary planes come back in planes (allocated here; bc_x0, bc_x1,
+  !> bc_y0, bc_y1, bc_z0, bc_z1, first index fastest) with the FFT level and
+  !> its nx, for the host copy of the boundary callback.
+  subroutine mg_gpu_poisson_free_3d(mg, new_rhs, max_fft_frac, fmgcycle, want, res, &
+       fft_lvl, nx, planes)
+    type(mg_t), intent(inout)            :: mg
+    logical, intent(in)                  :: new_rhs, fmgcycle, want
+    real(dp), intent(in)                 :: max_fft_frac
+    real(dp), intent(out)                :: res
+    integer, intent(out)                 :: fft_lvl, nx(3)
+    real(dp), allocatable, intent(inout) :: planes(:)
+    real(c_double), allocatable          :: rmin(:, :)
+    real(c_double)                       :: r, dummy(1)
+    integer(c_int)                       :: lvl_c, nx_c(3)
+    integer                              :: id
+
+    call check_methods(mg)
+    if (timer_device_vcycle == -1) call add_timers(mg)
+    call sync_in(mg)
+    allocate(rmin(NDIM, mg%n_boxes))
+    do id = 1, mg%n_boxes
+       rmin(:, id) = mg%boxes(id)%r_min
+    end do
+    call mg_timer_start(mg%timers(timer_device_fmg))
+    call omg_ok(omg_poisson_free_3d(ctx, merge(1_c_int, 0_c_int, new_rhs), &
+         real(max_fft_frac, c_double), merge(1_c_int, 0_c_int, fmgcycle), &
+         merge(1_c_int, 0_c_int, want), r, mg%r_min, rmin), "mg_poisson_free_3d")
+    call omg_ok(omg_synchronize(ctx), "synchronize")
+    call mg_timer_end(mg%timers(timer_device_fmg))
+    call omg_ok(omg_free_planes(ctx, lvl_c, nx_c, dummy, 0_c_long_long), "free_planes")
+    fft_lvl = lvl_c
+    nx = nx_c
+    if (allocated(planes)) deallocate(planes)
+    allocate(planes(2 * (nx(2)*nx(3) + nx(1)*nx(3) + nx(1)*nx(2))))
+    call omg_ok(omg_free_planes(ctx, lvl_c, nx_c, planes, int(size(planes), c_long_long)), &
+         "free_planes")
+    call sync_out(mg)
+    res = r
+  end subroutine mg_gpu_poisson_free_3d
 
   !> Resident mode on/off.  When on, mg_fas_vcycle / mg_fas_fmg / mg_apply_op
   !> neither upload mg%boxes(:)%cc before nor download it after: the GPU copy

@@ -1,8 +1,7 @@
 !> Umbrella module with the name the reference's programs `use`
 !> (reference: src/m_octree_mg.f90:2-19), re-exporting the kept host modules
-!> of the reference and the GPU-backed m_multigrid of this directory.
-!> m_free_space is left out: it needs the third-party BigDFT FFT package
-!> (SURVEY.md §2, out of scope).
+!> of the reference and the GPU-backed m_multigrid and m_free_space of this
+!> directory.
 module m_octree_mg
   use m_data_structures
   use m_build_tree
@@ -16,6 +15,7 @@ module m_octree_mg
   use m_helmholtz
   use m_vhelmholtz
   use m_ahelmholtz
+  use m_free_space
   implicit none
   public
 end module m_octree_mg

@@ -18,6 +18,7 @@ module m_omg_capi
   public :: omg_level_size, omg_upload_level, omg_download_level
   public :: omg_fas_vcycle, omg_fas_fmg, omg_apply_op, omg_phi_bc_store
   public :: omg_synchronize, omg_diffusion_solve
+  public :: omg_poisson_free_3d, omg_free_planes
 
   interface
      function omg_last_error() bind(C, name="omg_last_error") result(p)
@@ -171,6 +172,27 @@ module m_omg_capi
        real(c_double), intent(out) :: res
        integer(c_int) :: ierr
      end function omg_diffusion_solve
+
+     function omg_poisson_free_3d(ctx, new_rhs, max_fft_frac, fmgcycle, want_max_res, &
+          max_res, r_min, box_r_min) bind(C, name="omg_poisson_free_3d") result(ierr)
+       import :: c_ptr, c_int, c_double
+       type(c_ptr), value          :: ctx
+       integer(c_int), value       :: new_rhs, fmgcycle, want_max_res
+       real(c_double), value       :: max_fft_frac
+       real(c_double), intent(out) :: max_res
+       real(c_double), intent(in)  :: r_min(*), box_r_min(*)
+       integer(c_int) :: ierr
+     end function omg_poisson_free_3d
+
+     function omg_free_planes(ctx, fft_lvl, nx, planes, cap) bind(C, name="omg_free_planes") &
+          result(ierr)
+       import :: c_ptr, c_int, c_double, c_long_long
+       type(c_ptr), value          :: ctx
+       integer(c_int), intent(out) :: fft_lvl, nx(3)
+       real(c_double), intent(out) :: planes(*)
+       integer(c_long_long), value :: cap
+       integer(c_int) :: ierr
+     end function omg_free_planes
 
      function omg_synchronize(ctx) bind(C, name="omg_synchronize") result(ierr)
        import :: c_ptr, c_int

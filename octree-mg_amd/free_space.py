@@ -86,10 +86,10 @@ def mg_poisson_free_3d(mg: MG, new_rhs: bool, max_fft_frac: float, fmgcycle: boo
     # the reference's side effects on mg: phi's boundary callback (:102-104)
     # and the stored boundary data (:174)
     lvl, nx = C.c_int(0), np.zeros(3, np.int32)
-    mg.ctx.call("free_planes", C.byref(lvl), nx, None)
+    mg.ctx.call("free_planes", C.byref(lvl), nx, None, 0)
     n1, n2, n3 = (int(v) for v in nx)
     planes = np.empty(2 * (n2 * n3 + n1 * n3 + n1 * n2))
-    mg.ctx.call("free_planes", C.byref(lvl), nx, planes.ctypes.data_as(C.c_void_p))
+    mg.ctx.call("free_planes", C.byref(lvl), nx, planes.ctypes.data_as(C.c_void_p), planes.size)
     cb = FreeBoundary(mg, lvl.value, nx, planes)
     for nb in range(1, 7):
         mg.bc[nb][MG_IPHI] = BC(MG_BC_DIRICHLET, 0.0, boundary_cond=cb)

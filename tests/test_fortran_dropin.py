@@ -112,3 +112,56 @@ def test_dropin_resident_mode(name):
     p = subprocess.run([RESIDENT] + cfg["args"].split() + ["x"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     assert parse(p.stdout) == cfg["runs"]["1"]["history"]
+
+
+# -- m_free_space ------------------------------------------------------------
+FREE_DRIVER = os.path.join(BUILD, "omg_free_golden_gpu")
+FREE_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "free_golden.json")))["configs"]
+
+
+def _free_history(its):
+    import struct
+    f = lambda h: struct.unpack(">d", bytes.fromhex(h))[0]
+    return [{"it": h["it"], "err": f(h["err"]), "err2": f(h["err2"]), "max_res": f(h["max_res"])} for h in its]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(FREE_GOLDEN))
+def test_dropin_free_space_golden(name):
+    """oracle/omg_free_golden.f90 (the reference's test_free_space set-up)
+    against the drop-in m_free_space: the reference's histories within the
+    round-off tolerance of the Green's-function solve (tests/freedriver.py)."""
+    from tests import freedriver as FD
+    if not os.path.exists(FREE_DRIVER):
+        pytest.skip("Fortran drop-in drivers not built")
+    cfg = FREE_GOLDEN[name]
+    p = subprocess.run([FREE_DRIVER] + cfg["args"].split() + ["x"], capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    its = []
+    for line in p.stdout.splitlines():
+        f = line.split()
+        if f and f[0] == "IT":
+            its.append({"it": int(f[1]), "err": f[2], "err2": f[3], "max_res": f[4]})
+    FD.compare_history(_free_history(its), FD.golden_history(cfg), FD.parse(cfg["args"]), name)
+
+
+@pytest.mark.gpu
+def test_reference_free_space_program():
+    """The reference's tests/test_free_space.f90, unmodified, linked against
+    the drop-in (8 64 64 64, its default fft_frac 0.15, 5 FMG iterations):
+    the printed max err / err2 / residual match the reference's run of the
+    same program (free64_box8_f) within the stated tolerance."""
+    from tests import freedriver as FD
+    exe = os.path.join(BUILD, "test_free_space_3d")
+    if not os.path.exists(exe):
+        pytest.skip("Fortran drop-in not built")
+    p = subprocess.run([exe, "8", "64", "64", "64"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    toks = p.stdout.replace("\n", " ").split("max err/err2/res")[1:]
+    got = []
+    for n, t in enumerate(toks, 1):
+        v = [float(x) for x in t.split()[:3]]
+        got.append({"it": n, "err": v[0], "err2": v[1], "max_res": v[2]})
+    cfg = FREE_GOLDEN["free64_box8_f"]
+    FD.compare_history(got, FD.golden_history(cfg), FD.parse(cfg["args"]), "test_free_space")
