@@ -1268,7 +1268,7 @@ void phi_bc_store(omg_ctx* c) {
   } while (0)
 
 // smallest even n >= m whose prime factors are 2, 3, 5, 7 (the transform
-// length of one padded axis; any n >= 2*nx gives the same linear convolution)
+// length of one padded axis)
 int fft_length(int m) {
   for (int n = std::max(m, 2);; n++) {
     if (n & 1) continue;
@@ -1381,10 +1381,13 @@ void free_create_kernel(omg_ctx* c, omg_free_state* S, const double h[3]) {
 // the FFT grid, its plans and the gather plan of the FFT level
 void free_new_grid(omg_ctx* c, omg_free_state* S, int fft_lvl, const int nx[3], const double h[3]) {
   FreeGrid& G = S->G;
+  // the density is zero on the ghost layer, so the offsets the solution
+  // needs are |d| <= nx-2 and N >= 2*(nx-2) gives the linear convolution
+  // (a power of two for power-of-two domains; the k_free_dft note)
   for (int d = 0; d < 3; d++) {
     G.nx[d] = nx[d];
     G.n0[d] = nx[d];
-    G.N[d] = fft_length(2 * nx[d]);
+    G.N[d] = fft_length(std::max(2 * (nx[d] - 2), nx[d]));   // and the nx points fit
   }
   free_create_kernel(c, S, h);
   const size_t nr = (size_t)G.N[0] * G.N[1] * G.N[2], nz = (size_t)(G.N[0] / 2 + 1) * G.N[1] * G.N[2];

@@ -21,9 +21,10 @@
 //   psolver_main.f90:91-556, psolver_base.f90:1720-2153): the zero-padded
 //   density goes through a D2Z transform (rocFFT via hipFFT, on the context
 //   stream), is multiplied by the real kernel spectrum (scaled by
-//   hx*hy*hz/(N1*N2*N3), PSolver's scal) and comes back with Z2D.  The padded
-//   sizes only need N >= 2*nx (the result is the linear convolution either
-//   way), so they are chosen as 2^a 3^b 5^c 7^d.
+//   hx*hy*hz/(N1*N2*N3), PSolver's scal) and comes back with Z2D.  The density
+//   is zero on the ghost layer, so the padded sizes only need N >= 2*(nx-2)
+//   (the result is the linear convolution either way); they are chosen as
+//   2^a 3^b 5^c 7^d, powers of two for power-of-two domains.
 //
 //   Use of the solution: the six boundary planes (m_free_space.f90:163-171),
 //   the interpolated Dirichlet values of every physical face of every level
@@ -167,8 +168,10 @@ __global__ void __launch_bounds__(256) k_free_tables(FreeTabArgs A) {
   }
 }
 
-// F[d][g][k] = K(0) + 2 sum_{n=1}^{n0-1} K(n) cos(2 pi k n / N), k = 0..N/2:
-// the transform of the even extension of one 1D table (it is real).
+// F[d][g][k], k = 0..N/2: the transform of the even extension of one 1D
+// table on N points (it is real),
+//   K(0) + 2 sum_{0 < n < N/2} K(n) cos(2 pi k n / N) + K(N/2) (-1)^k,
+// with K(n) = 0 beyond the table; the solution only needs offsets |n| <= N/2.
 __global__ void __launch_bounds__(256) k_free_dft(const double* tab, int n0max, FreeGrid G, double* F, int fmax) {
   const long long total = 3LL * kFreeNGauss * fmax;
   FREE_STRIDE(t, total) {
@@ -176,33 +179,41 @@ __global__ void __launch_bounds__(256) k_free_dft(const double* tab, int n0max, 
     const int N = G.N[d];
     if (k > N / 2) continue;
     const double* K = tab + ((long long)g * 3 + d) * n0max;
+    const int n_end = min(G.n0[d], N / 2);   // n < n_end: the doubled terms
     double s = 0.0;
-    for (int n = 1; n < G.n0[d]; n++) {
+    for (int n = 1; n < n_end; n++) {
       const long long kn = ((long long)k * n) % N;
       s = s + K[n] * cospi(2.0 * (double)kn / (double)N);
     }
-    F[((long long)d * kFreeNGauss + g) * fmax + k] = K[0] + 2.0 * s;
+    double f = K[0] + 2.0 * s;
+    if (N / 2 < G.n0[d]) f = f + ((k & 1) ? -K[N / 2] : K[N / 2]);
+    F[((long long)d * kFreeNGauss + g) * fmax + k] = f;
   }
 }
 
 // The kernel spectrum on the D2Z half grid [z][y][x <= N1/2], times scal:
-// sum over the Gaussians (reference order) of w_g Fx Fy Fz.
+// sum over the Gaussians (reference order) of w_g Fx Fy Fz.  F is even in
+// k, so one thread per (kx, ky <= N2/2, kz <= N3/2) writes up to four mirror
+// images in y and z.
 __global__ void __launch_bounds__(256) k_free_karray(const double* F, int fmax, const double* w, FreeGrid G,
                                                      double scal, double* karray) {
-  const int h1 = G.N[0] / 2 + 1;
-  const long long total = (long long)h1 * G.N[1] * G.N[2];
+  const int h1 = G.N[0] / 2 + 1, h2 = G.N[1] / 2 + 1, h3 = G.N[2] / 2 + 1;
+  const long long total = (long long)h1 * h2 * h3;
   FREE_STRIDE(t, total) {
     const int kx = (int)(t % h1);
-    const int ky0 = (int)((t / h1) % G.N[1]), kz0 = (int)(t / ((long long)h1 * G.N[1]));
-    const int ky = ky0 <= G.N[1] / 2 ? ky0 : G.N[1] - ky0;
-    const int kz = kz0 <= G.N[2] / 2 ? kz0 : G.N[2] - kz0;
+    const int ky = (int)((t / h1) % h2), kz = (int)(t / ((long long)h1 * h2));
     const double* Fx = F;
     const double* Fy = F + (long long)kFreeNGauss * fmax;
     const double* Fz = F + 2LL * kFreeNGauss * fmax;
     double s = 0.0;
     for (int g = 0; g < kFreeNGauss; g++)
       s = s + w[g] * Fx[(long long)g * fmax + kx] * Fy[(long long)g * fmax + ky] * Fz[(long long)g * fmax + kz];
-    karray[t] = s * scal;
+    s = s * scal;
+    const int ys[2] = {ky, ky == 0 || 2 * ky == G.N[1] ? -1 : G.N[1] - ky};
+    const int zs[2] = {kz, kz == 0 || 2 * kz == G.N[2] ? -1 : G.N[2] - kz};
+    for (int a = 0; a < 2; a++)
+      for (int b = 0; b < 2; b++)
+        if (ys[a] >= 0 && zs[b] >= 0) karray[((long long)zs[b] * G.N[1] + ys[a]) * h1 + kx] = s;
   }
 }
 
@@ -352,7 +363,7 @@ void launch_free_dft(const double* tab, int n0max, const FreeGrid& G, double* F,
 
 void launch_free_karray(const double* F, int fmax, const double* w, const FreeGrid& G, double scal,
                         double* karray, hipStream_t st) {
-  const long long n = (long long)(G.N[0] / 2 + 1) * G.N[1] * G.N[2];
+  const long long n = (long long)(G.N[0] / 2 + 1) * (G.N[1] / 2 + 1) * (G.N[2] / 2 + 1);
   k_free_karray<<<blocks_for(n), 256, 0, st>>>(F, fmax, w, G, scal, karray);
 }
 
