@@ -1034,6 +1034,24 @@ void run_tail(omg_ctx* c, int top) {
   A.maxbits = (unsigned long long*)c->d_scalar;
   A.coarse_its = (int*)(c->d_scalar + 1);
   A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
+  // the LDS-resident part of the tail (omg_tiles.hip): one box per level whose
+  // faces are physical or the box itself, the lowest levels up to 8^3 cells
+  // (at most three: 2^3, 4^3, 8^3, 5,120 doubles for their four variables),
+  // and a 16^3 top level right above them
+  auto lds_box_ok = [&](int l, int max_nc) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->n != 1 || L->nc > max_nc) return false;
+    for (int nb = 0; nb < 6; nb++) {
+      const int k = L->h_nbk[nb];
+      if (!(k == NB_PHYS || (k == NB_LOCAL && L->h_nba[nb] == 0))) return false;
+    }
+    return true;
+  };
+  A.lds_levels = 0;
+  while (A.lds_levels < std::min(A.n_lvls, kTailLdsMaxLevels) && lds_box_ok(c->lowest + A.lds_levels, 8))
+    A.lds_levels++;
+  A.lds_top = A.lds_levels > 0 && A.lds_levels == A.n_lvls - 1 && level_ptr(c, top)->nc == 16 &&
+              lds_box_ok(top, 16);
   const bool tail_timing = c->tail_timing;
   if (tail_timing) {
     if (!c->d_tail_stamps) HIPCHK(hipMalloc(&c->d_tail_stamps, 8 * 64));
@@ -1155,7 +1173,12 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
   double max_res = 0.0;
   for (int l = c->lowest; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
-    if (L && L->n) launch_copy_var(L->view(), 1, 3, c->stream);
+    // old = phi (:127-129).  Below the highest level, where every box is a
+    // parent, update_coarse's parent loop above left old equal to phi, ghost
+    // faces included, and nothing has written that level since (unless the
+    // cycles below subtract phi's mean, which covers every level)
+    const bool old_is_phi = l < c->highest && L && L->all_parents && !c->subtract_mean;
+    if (L && L->n && !old_is_phi) launch_copy_var(L->view(), 1, 3, c->stream);
     if (l > c->lowest) correct_and_fill(c, l - 1);
     if (l == c->highest)
       max_res = fas_vcycle(c, l, want_max_res, false);

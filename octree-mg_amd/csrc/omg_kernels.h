@@ -101,7 +101,13 @@ struct TailArgs {
   int* coarse_its;               // device: sweeps the coarse solve took
   int gs_lex;                    // smoother: lexicographic GS (else red-black)
   long long* stamps;             // OMG_TAIL_TIMING: wall clock per phase (thread 0), or null
+  // levels 0..lds_levels-1 run with their box resident in LDS (at most 8^3
+  // cells, a single box whose local faces are itself), and lds_top: the 16^3
+  // top level above them too (tail_lds_plan in omg_api.cpp)
+  int lds_levels, lds_top;
 };
+// how many of the tail's lowest levels qualify for the LDS-resident program
+constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 
 // LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16

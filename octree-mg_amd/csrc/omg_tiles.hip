@@ -14,6 +14,12 @@
 #include "omg_gsrb.h"
 #include "omg_kernels.h"
 
+// the coarse tail's levels resident in LDS: 1 = those of at most 8^3 cells,
+// 2 = and a 16^3 top level (0: the global-memory box programs for every
+// level; A/B builds only)
+#ifndef OMG_TAIL_LDS
+#define OMG_TAIL_LDS 2
+#endif
 // k_prolong_smooth tuning: waves per SIMD it is compiled for; PRE issues the
 // substep's rhs loads before the correction phases (A/B builds only)
 #ifndef OMG_PS_WAVES
@@ -1194,43 +1200,465 @@ __device__ void tail_correct(const TailArgs& A, int li, double* lds) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The levels of the tail with boxes of at most 8^3 cells run with their boxes
+// resident in LDS: all four variables of each such level (one box each) in a
+// plain (nc+2)^3 layout, i fastest (edges and corners unused), loaded once
+// and written back once.  Every step keeps the arithmetic of the global-memory
+// box programs above (gs_value / op_value on the same operands, the same
+// sequential restriction sum, the same prolongation order, the same ghost
+// formulas), so the results are bit-identical; only the L2 round trips and
+// the per-step LDS staging go away.  The one-box levels of the tail are
+// single boxes whose local neighbours are the box itself (periodic faces);
+// run_tail (omg_api.cpp) checks that when it sets lds_levels / lds_top.
+constexpr int kTailLdsLevels = kTailLdsMaxLevels;
+constexpr int kTailLdsDoubles = 4 * (10 * 10 * 10 + 6 * 6 * 6 + 4 * 4 * 4);
+// the physical bc values of each face cell of each level, resolved once
+// (stored in rhs ghosts / tabulated / constant)
+constexpr int kTailLdsBcDoubles = 6 * (8 * 8 + 4 * 4 + 2 * 2);
+// OMG_TAIL_LDS >= 2: a 16^3 top level as well, phi and rhs only (its old is
+// not used inside the tail, its res goes straight to HBM)
+constexpr int kTailBigS = 18, kTailBigS3 = kTailBigS * kTailBigS * kTailBigS;
+constexpr int kTailBigDoubles = 2 * kTailBigS3 + 6 * 16 * 16;
+
+struct TailBox {
+  double *P, *F, *O, *R;   // phi, rhs, old, res
+  double* B;               // bc value per face cell (6 nc^2)
+  int nc, S;
+  __device__ __forceinline__ int at(int i, int j, int k) const { return i + S * (j + S * k); }
+};
+
+// per LDS level, kept in LDS so the per-cell work never reads the tail's
+// argument block in HBM with lane-dependent indices
+__device__ __forceinline__ Nbr7 tail_nbr(const TailBox& X, const double* U, int c) {
+  Nbr7 s;
+  s.c = U[c];
+  s.xm = U[c - 1];
+  s.xp = U[c + 1];
+  s.ym = U[c - X.S];
+  s.yp = U[c + X.S];
+  s.zm = U[c - X.S * X.S];
+  s.zp = U[c + X.S * X.S];
+  return s;
+}
+
+struct TailLdsLevel {
+  int local[6];                // periodic face: the box itself on the other side
+  double c0[6], c1[6], c2[6];  // bc_to_gc coefficients of each physical face
+};
+
+__device__ __forceinline__ TailBox tail_box(const TailArgs& A, int li, double* tl) {
+  TailBox X;
+  int base = 0, bbase = kTailLdsDoubles;
+  for (int l = 0; l < li; l++) {
+    const int s = A.lv[l].L.nc + 2;
+    base += 4 * s * s * s;
+    bbase += 6 * A.lv[l].L.nc * A.lv[l].L.nc;
+  }
+  X.nc = A.lv[li].L.nc;
+  X.S = X.nc + 2;
+  const int s3 = X.S * X.S * X.S;
+  X.P = tl + base;
+  X.F = X.P + s3;
+  X.O = X.F + s3;
+  X.R = X.O + s3;
+  X.B = tl + bbase;
+  return X;
+}
+
+__device__ __forceinline__ TailBox tail_big_box(double* tl) {
+  TailBox X;
+  X.nc = 16;
+  X.S = kTailBigS;
+  X.P = tl + kTailLdsDoubles + kTailLdsBcDoubles;
+  X.F = X.P + kTailBigS3;
+  X.O = X.R = nullptr;
+  X.B = X.F + kTailBigS3;
+  return X;
+}
+
+// One box variable set of the LDS-resident tail, HBM <-> LDS: nvar
+// variables (1 = phi, 2 = rhs, ...) of the single box of level L, interior
+// and face ghosts, to / from the plain (nc+2)^3 arrays at dst (consecutive
+// per variable; edges and corners are zero in LDS and never written back).
+// Loads go in rounds of 8 per thread, all 8 issued before their LDS stores,
+// so each round costs one memory latency.
+template <bool LOAD>
+__device__ void tail_io_box(const LevelView& L, int nvar, double* dst) {
+  const int S = L.nc + 2, S3 = S * S * S, n = nvar * S3;
+  constexpr int R = 8;
+  for (int t0 = 0; t0 < n; t0 += R * kTailBS) {
+    int go[R], tt[R];
+    double v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int t = t0 + threadIdx.x + kTailBS * r;
+      go[r] = -1;
+      tt[r] = t < n ? t : -1;
+      if (t >= n) continue;
+      const int var = t / S3, q = t % S3;
+      const int i = q % S, j = (q / S) % S, k = q / (S * S);
+      const int nbnd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
+      if (nbnd >= 2) continue;
+      go[r] = (int)(boxp(L, var + 1, 0) - L.data) + off_cell(L, i, j, k);
+    }
+    if (LOAD) {
+#pragma unroll
+      for (int r = 0; r < R; r++) v[r] = go[r] >= 0 ? L.data[go[r]] : 0.0;
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (tt[r] >= 0) dst[tt[r]] = v[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (go[r] >= 0) L.data[go[r]] = dst[tt[r]];
+    }
+  }
+}
+
+// all four variables of the boxes of levels 0..ls (contiguous in LDS)
+template <bool LOAD>
+__device__ void tail_boxes_io(const TailArgs& A, int ls, double* tl) {
+  int base = 0;
+  for (int l = 0; l <= ls; l++) {
+    const LevelView& L = A.lv[l].L;
+    tail_io_box<LOAD>(L, 4, tl + base);
+    const int S = L.nc + 2;
+    base += 4 * S * S * S;
+  }
+  __syncthreads();
+}
+
+// the fill's per-level data (TailLdsLevel) and the bc value of every
+// physical face cell (bc_to_gc's argument: the stored value in the rhs ghost
+// when mg_phi_bc_store ran, else the tabulated or constant one); after the
+// rhs ghosts are in LDS
+__device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailLdsLevel& D) {
+  const TailLevel& T = A.lv[l];
+  const LevelView& L = T.L;
+  const GcBC& bc = T.bc;
+  const int nc = X.nc, nc2 = nc * nc;
+  if (threadIdx.x < 6) {
+    const int nb = threadIdx.x + 1;
+    const bool low = nb & 1;
+    int type;
+    if (bc.phi_stored) type = L.nba[nb - 1];
+    else if (bc.face_off && bc.face_off[nb - 1] >= 0) type = bc.face_type[nb - 1];
+    else type = bc.type[nb - 1];
+    double c0, c1, c2;
+    if (type == -10) {
+      c0 = 2; c1 = -1; c2 = 0;
+    } else if (type == -11) {
+      c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
+    } else {
+      c0 = 0; c1 = 2; c2 = -1;
+    }
+    D.local[nb - 1] = L.nbk[nb - 1] == NB_LOCAL;
+    D.c0[nb - 1] = c0;
+    D.c1[nb - 1] = c1;
+    D.c2[nb - 1] = c2;
+  }
+  for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
+    const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
+    if (L.nbk[nb - 1] != NB_PHYS) continue;
+    const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
+    double bv;
+    if (bc.phi_stored)
+      bv = X.F[d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g)];
+    else if (bc.face_off && bc.face_off[nb - 1] >= 0)
+      bv = bc.face_data[bc.face_off[nb - 1] + (a - 1) + (long long)nc * (c - 1)];
+    else
+      bv = bc.value[nb - 1];
+    X.B[p] = bv;
+  }
+}
+
+// phi and rhs of the 16^3 top level (interior and face ghosts) HBM <-> LDS;
+// only phi goes back
+template <bool LOAD>
+__device__ void tail_big_io(const LevelView& L, const TailBox& X) {
+  tail_io_box<LOAD>(L, LOAD ? 2 : 1, X.P);
+  __syncthreads();
+}
+
+// update_coarse's fine part for the 16^3 top level in LDS: one parent cell
+// per thread, its eight children's residuals (res = rhs - L phi, written to
+// HBM as residual_box leaves them) summed as restrict_onto sums them, next to
+// the sum of their phi
+template <int OP>
+__device__ void tail_big_resid_restrict(const TailArgs& A, int li, const TailBox& X, const TailBox& Xc) {
+  const LevelView& L = A.lv[li].L;
+  const OpCoef<OP> K(L, A.lambda);
+  const int dp = A.lv[li].dixp[0];
+  const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
+  double* res = boxp(L, 4, 0);
+  for (int q = threadIdx.x; q < 8 * 8 * 8; q += blockDim.x) {
+    const int i = q % 8 + 1, j = (q / 8) % 8 + 1, k = q / 64 + 1;
+    double ap = 0.0, ar = 0.0;
+    for (int kk = 0; kk < 2; kk++)
+      for (int jj = 0; jj < 2; jj++)
+        for (int ii = 0; ii < 2; ii++) {
+          const int fi = 2 * i - 1 + ii, fj = 2 * j - 1 + jj, fk = 2 * k - 1 + kk, c = X.at(fi, fj, fk);
+          const double r = X.F[c] - op_value<OP>(K, tail_nbr(X, X.P, c));
+          res[off_int(L, fi, fj, fk)] = r;
+          ap += X.P[c];
+          ar += r;
+        }
+    Xc.P[Xc.at(dx + i, dy + j, dz + k)] = 0.125 * ap;
+    Xc.R[Xc.at(dx + i, dy + j, dz + k)] = 0.125 * ar;
+  }
+  __syncthreads();
+}
+
+// mg_fill_ghost_cells_lvl of phi for the box in LDS: a periodic face copies
+// the opposite boundary layer (what the owner pushes), a physical face is
+// bc_to_gc's c0*bc + c1*x1 + c2*x2
+__device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
+  const int nc = X.nc, nc2 = nc * nc;
+  for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
+    const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1, g = low ? 0 : nc + 1, x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
+    auto cell_at = [&](int layer) {
+      return d == 1 ? X.at(layer, a, c) : d == 2 ? X.at(a, layer, c) : X.at(a, c, layer);
+    };
+    if (D.local[nb - 1]) {
+      X.P[cell_at(g)] = X.P[cell_at(low ? nc : 1)];
+      continue;
+    }
+    X.P[cell_at(g)] = D.c0[nb - 1] * X.B[p] + D.c1[nb - 1] * X.P[cell_at(x1)] + D.c2[nb - 1] * X.P[cell_at(x2)];
+  }
+  __syncthreads();
+}
+
+
+// smooth_boxes: red-black substeps (colour e = n & 1 for n = 1 .. 2 n_cycle)
+// or lexicographic sweeps (hyperplanes i+j+k = d, as gs_lex_box), each
+// followed by the ghost fill
+template <int OP, bool LEX>
+__device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X, int n_cycle) {
+  const OpCoef<OP> K(A.lv[li].L, A.lambda);
+  const int nc = X.nc, n3 = nc * nc * nc;
+  if constexpr (LEX) {
+    for (int n = 1; n <= n_cycle; n++) {
+      for (int d = 3; d <= 3 * nc; d++) {
+        for (int p = threadIdx.x; p < nc * nc; p += blockDim.x) {
+          const int j = p % nc + 1, k = p / nc + 1, i = d - j - k;
+          if (i < 1 || i > nc) continue;
+          const int c = X.at(i, j, k);
+          X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
+        }
+        __syncthreads();
+      }
+      tail_lds_fill(D, X);
+    }
+    return;
+  }
+  for (int n = 1; n <= 2 * n_cycle; n++) {
+    const int e = n & 1;
+    for (int q = threadIdx.x; q < n3; q += blockDim.x) {
+      const int i = q % nc + 1, j = (q / nc) % nc + 1, k = q / (nc * nc) + 1;
+      if (((i + j + k) & 1) != e) continue;
+      const int c = X.at(i, j, k);
+      X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
+    }
+    __syncthreads();
+    tail_lds_fill(D, X);
+  }
+}
+
+// residual_box (res = rhs - L phi) over the box, max |res| when asked, then
+// restrict_onto of phi and res into the parent box Xc (sequential 8-cell sum
+// from +0.0, i fastest, times 0.125)
+template <int OP>
+__device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X, const TailBox* Xc,
+                                    double* red) {
+  const OpCoef<OP> K(A.lv[li].L, A.lambda);
+  const int nc = X.nc, n3 = nc * nc * nc;
+  double mx = 0.0;
+  for (int q = threadIdx.x; q < n3; q += blockDim.x) {
+    const int c = X.at(q % nc + 1, (q / nc) % nc + 1, q / (nc * nc) + 1);
+    const double r = X.F[c] - op_value<OP>(K, tail_nbr(X, X.P, c));
+    X.R[c] = r;
+    mx = fmax(mx, fabs(r));
+  }
+  if (red) {
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+    __syncthreads();   // every thread has read the previous maximum
+    if (threadIdx.x == 0) *red = 0.0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned long long*>(red),
+                                           (unsigned long long)__double_as_longlong(mx));
+  }
+  __syncthreads();
+  if (Xc) {
+    const int dp = A.lv[li].dixp[0];
+    const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, hn = nc / 2;
+    for (int t = threadIdx.x; t < 2 * hn * hn * hn; t += blockDim.x) {
+      const int pass = t / (hn * hn * hn), q = t % (hn * hn * hn);
+      const int i = q % hn + 1, j = (q / hn) % hn + 1, k = q / (hn * hn) + 1;
+      const double* src = pass ? X.R : X.P;
+      double acc = 0.0;
+      for (int kk = 0; kk < 2; kk++)
+        for (int jj = 0; jj < 2; jj++)
+          for (int ii = 0; ii < 2; ii++) acc += src[X.at(2 * i - 1 + ii, 2 * j - 1 + jj, 2 * k - 1 + kk)];
+      (pass ? Xc->R : Xc->P)[Xc->at(dx + i, dy + j, dz + k)] = 0.125 * acc;
+    }
+    __syncthreads();
+  }
+  return red ? *red : 0.0;
+}
+
+// update_coarse's parent part: rhs = L(phi) + res on the interior, old = phi
+// on the whole stored box
+template <int OP>
+__device__ void tail_lds_coarse_rhs(const TailArgs& A, int li, const TailBox& X) {
+  const OpCoef<OP> K(A.lv[li].L, A.lambda);
+  const int nc = X.nc, s3 = X.S * X.S * X.S;
+  for (int q = threadIdx.x; q < s3; q += blockDim.x) {
+    const int i = q % X.S, j = (q / X.S) % X.S, k = q / (X.S * X.S);
+    X.O[q] = X.P[q];
+    if (i < 1 || i > nc || j < 1 || j > nc || k < 1 || k > nc) continue;
+    X.F[q] = op_value<OP>(K, tail_nbr(X, X.P, q)) + X.R[q];
+  }
+  __syncthreads();
+}
+
+// correct_children of the parent Xc (res = phi - old over its stored cells)
+// + mg_prolong_sparse onto the box + the ghost fill
+__device__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
+                                 const TailBox& Xc) {
+  const int sc3 = Xc.S * Xc.S * Xc.S;
+  for (int q = threadIdx.x; q < sc3; q += blockDim.x) Xc.R[q] = Xc.P[q] - Xc.O[q];
+  __syncthreads();
+  const int dp = A.lv[li].dixp[0];
+  const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, nc = X.nc, n3 = nc * nc * nc;
+  for (int q = threadIdx.x; q < n3; q += blockDim.x) {
+    const int i = q % nc + 1, j = (q / nc) % nc + 1, k = q / (nc * nc) + 1;
+    const int c0 = Xc.at(((i + 1) >> 1) + dx, ((j + 1) >> 1) + dy, ((k + 1) >> 1) + dz);
+    const double f0 = 0.25 * Xc.R[c0];
+    const double fx = 0.25 * Xc.R[(i & 1) ? c0 - 1 : c0 + 1];
+    const double fy = 0.25 * Xc.R[(j & 1) ? c0 - Xc.S : c0 + Xc.S];
+    const double fz = 0.25 * Xc.R[(k & 1) ? c0 - Xc.S * Xc.S : c0 + Xc.S * Xc.S];
+    const int c = X.at(i, j, k);
+    X.P[c] = X.P[c] + (f0 + fx + fy + fz);
+  }
+  __syncthreads();
+  tail_lds_fill(D, X);
+}
+
 template <int OP, bool LEX>
 __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restrict__ dA) {
-  __shared__ double lds[tail_lds<LEX>()];
+  // the global-memory box programs' LDS, which also holds the LDS-resident
+  // levels while they are in use (the two never overlap in time)
+  constexpr int kSmall = kTailLdsDoubles + kTailLdsBcDoubles + (OMG_TAIL_LDS >= 2 ? kTailBigDoubles : 0);
+  __shared__ double lds[tail_lds<LEX>() > kSmall ? tail_lds<LEX>() : kSmall];
+  __shared__ double red;
+  __shared__ TailLdsLevel tll[kTailLdsLevels + 1];
   const TailArgs& A = *dA;
   const int top = A.n_lvls - 1;
+  // levels 0..ls live in LDS, and with big the 16^3 top level above them
+  // (phi, rhs); the host decided which (run_tail)
+  const int ls = OMG_TAIL_LDS ? A.lds_levels - 1 : -1;
+  const bool big = OMG_TAIL_LDS >= 2 && A.lds_top;
+  const TailBox XB = tail_big_box(lds);
   int ns = 0;
   auto stamp = [&]() {
     if (A.stamps && threadIdx.x == 0) A.stamps[ns] = (long long)wall_clock64();
     ns++;
   };
+  auto enter_lds = [&]() {
+    tail_boxes_io<true>(A, ls, lds);
+    for (int l = 0; l <= ls; l++) tail_lds_setup(A, l, tail_box(A, l, lds), tll[l]);
+    __syncthreads();
+  };
   stamp();
-  for (int li = top; li >= 1; li--) {
+  if (ls == top) enter_lds();
+  if (big) {
+    tail_big_io<true>(A.lv[top].L, XB);
+    tail_boxes_io<true>(A, ls, lds);
+    for (int l = 0; l <= ls; l++) tail_lds_setup(A, l, tail_box(A, l, lds), tll[l]);
+    tail_lds_setup(A, top, XB, tll[top]);
+    __syncthreads();
+    const TailBox Xc = tail_box(A, ls, lds);
+    tail_lds_smooth<OP, LEX>(A, top, tll[top], XB, A.n_down);
+    stamp();
+    tail_big_resid_restrict<OP>(A, top, XB, Xc);
+    stamp();
+    tail_lds_fill(tll[ls], Xc);
+    stamp();
+    tail_lds_coarse_rhs<OP>(A, ls, Xc);
+    stamp();
+  }
+  for (int li = big ? top - 1 : top; li >= 1; li--) {
+    if (li <= ls) {
+      const TailBox X = tail_box(A, li, lds), Xc = tail_box(A, li - 1, lds);
+      tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_down);
+      stamp();
+      tail_lds_residual<OP>(A, li, X, &Xc, nullptr);
+      stamp();
+      tail_lds_fill(tll[li - 1], Xc);
+      stamp();
+      tail_lds_coarse_rhs<OP>(A, li - 1, Xc);
+      stamp();
+      continue;
+    }
     tail_smooth<OP, LEX>(A, li, A.n_down, lds);
     stamp();
     tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
     stamp();
+    if (li - 1 == ls) {   // the level below goes to LDS now
+      enter_lds();
+      const TailBox Xc = tail_box(A, ls, lds);
+      tail_lds_fill(tll[ls], Xc);
+      stamp();
+      tail_lds_coarse_rhs<OP>(A, ls, Xc);
+      stamp();
+      continue;
+    }
     tail_fill(A, li - 1);
     stamp();
     tail_coarse_rhs<OP>(A, li - 1, lds);
     stamp();
   }
   // coarse solve (m_multigrid.f90:197-208)
-  const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
   int its = 0;
-  for (int i = 1; i <= A.max_coarse; i++) {
-    tail_smooth<OP, LEX>(A, 0, A.n_up + A.n_down, lds);
-    its = i;
-    const double res = tail_residual<OP>(A, 0, 0, true, lds);
-    if (res < A.res_rel * init_res || res < A.res_abs) break;
+  if (ls >= 0) {
+    const TailBox X = tail_box(A, 0, lds);
+    const double init_res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
+    for (int i = 1; i <= A.max_coarse; i++) {
+      tail_lds_smooth<OP, LEX>(A, 0, tll[0], X, A.n_up + A.n_down);
+      its = i;
+      const double res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
+      if (res < A.res_rel * init_res || res < A.res_abs) break;
+    }
+  } else {
+    const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
+    for (int i = 1; i <= A.max_coarse; i++) {
+      tail_smooth<OP, LEX>(A, 0, A.n_up + A.n_down, lds);
+      its = i;
+      const double res = tail_residual<OP>(A, 0, 0, true, lds);
+      if (res < A.res_rel * init_res || res < A.res_abs) break;
+    }
   }
   stamp();
   for (int li = 1; li <= top; li++) {
+    if (li <= ls || big) {
+      const TailBox X = li <= ls ? tail_box(A, li, lds) : XB, Xc = tail_box(A, li - 1, lds);
+      tail_lds_correct(A, li, tll[li], X, Xc);
+      stamp();
+      tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_up);
+      stamp();
+      continue;
+    }
+    if (li == ls + 1 && ls >= 0) tail_boxes_io<false>(A, ls, lds);   // the LDS levels back to HBM first
     tail_correct(A, li, lds);
     stamp();
     tail_smooth<OP, LEX>(A, li, A.n_up, lds);
     stamp();
   }
+  if (ls == top || big) tail_boxes_io<false>(A, ls, lds);
+  if (big) tail_big_io<false>(A.lv[top].L, XB);
   if (threadIdx.x == 0) *A.coarse_its = its;
 }
 

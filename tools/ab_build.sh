@@ -10,14 +10,14 @@ rm -f ../_variants/libomg_*.so
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   d=/tmp/omg_var_$name; mkdir -p $d
-  for f in omg_kernels omg_sweep omg_tiles; do
+  for f in omg_kernels omg_sweep omg_tiles omg_free; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I/opt/rocm/include \
       $flags -c -o $d/$f.o $f.hip &
   done
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I/opt/rocm/include \
     $flags -x hip -c -o $d/omg_api.o omg_api.cpp &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o ../_variants/libomg_$name.so $d/*.o -shared -L/opt/rocm/lib -lrccl \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o ../_variants/libomg_$name.so $d/*.o -shared -L/opt/rocm/lib -lrccl -lhipfft \
     -Wl,-rpath,/opt/rocm/lib
 done
 ls -la ../_variants
