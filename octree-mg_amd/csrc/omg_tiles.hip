@@ -1454,12 +1454,13 @@ __device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D
     }
     return;
   }
+  const int h = nc / 2;
   for (int n = 1; n <= 2 * n_cycle; n++) {
     const int e = n & 1;
-    for (int q = threadIdx.x; q < n3; q += blockDim.x) {
-      const int i = q % nc + 1, j = (q / nc) % nc + 1, k = q / (nc * nc) + 1;
-      if (((i + j + k) & 1) != e) continue;
-      const int c = X.at(i, j, k);
+    // the cells of colour e only: i = 2*ih + 1 + p with (i+j+k) & 1 == e
+    for (int q = threadIdx.x; q < n3 / 2; q += blockDim.x) {
+      const int ih = q % h, row = q / h, j = row % nc + 1, k = row / nc + 1;
+      const int c = X.at(2 * ih + 1 + ((1 + j + k + e) & 1), j, k);
       X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
     }
     __syncthreads();
