@@ -539,15 +539,21 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
-// max_residual_lvl (m_multigrid.f90:296-311), this rank only
-double max_residual_lvl(omg_ctx* c, int lvl) {
+// max over levels lo..hi of max_residual_lvl (m_multigrid.f90:296-311), this
+// rank only: the levels' maxima fold into one word on the device, read back
+// with one synchronisation
+double max_residual_levels(omg_ctx* c, int lo, int hi) {
   unsigned long long* d = (unsigned long long*)c->d_scalar;
-  HIPCHK(hipMemsetAsync(d, 0, 8, c->stream));
-  residual_lvl(c, lvl, d);
+  for (int l = lo; l <= hi; l++) {
+    residual_lvl(c, l, c->d_maxslots);
+    launch_max_fold(c->d_maxslots, d, l > lo, c->stream);
+  }
   HIPCHK(hipMemcpyAsync(c->h_scalar, d, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return c->h_scalar[0];
 }
+
+double max_residual_lvl(omg_ctx* c, int lvl) { return max_residual_levels(c, lvl, lvl); }
 
 // the remote part of mg_restrict_lvl: children whose parent lives on another
 // rank are restricted into a buffer, exchanged and unpacked (m_restrict.f90:
@@ -1145,7 +1151,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   double max_res = 0.0;
   if (want_max_res) {
     double m = 0.0;
-    for (int l = min_lvl; l <= max_lvl; l++) m = std::max(max_residual_lvl(c, l), m);
+    if (min_lvl <= max_lvl) m = max_residual_levels(c, min_lvl, max_lvl);
     max_res = allreduce(c, m, true);
   }
   materialize_phi(c);   // nothing left pending after a cycle (defensive: all consumed)
@@ -1978,6 +1984,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
+    HIPCHK(hipMalloc(&c->d_maxslots, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
+    HIPCHK(hipMemset(c->d_maxslots, 0, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->stream_comm, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
@@ -2033,6 +2041,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     if (c->d_tail_stamps) (void)hipFree(c->d_tail_stamps);
     delete c->h_tail;
     dfree(c->d_red);
+    dfree(c->d_maxslots);
     dfree(c->d_stage);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);

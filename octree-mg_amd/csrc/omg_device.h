@@ -113,6 +113,28 @@ __device__ __forceinline__ void atomic_max_nonneg(unsigned long long* p, double 
   atomicMax(p, (unsigned long long)__double_as_longlong(v));
 }
 
+// Max |res| over a launch (max_residual_lvl, exact in any order). A
+// multi-workgroup launch issues one device-scope atomic per workgroup, spread
+// over kMaxSlots slots kMaxSlotStride words apart: the 32K workgroups of a
+// 512^3 level queueing on one address cost 2.4 ms per pass. launch_max_fold
+// folds the slots into one word and zeroes them again. A one-workgroup launch
+// (the coarse tail) keeps one atomic per wave on maxbits[0].
+template <int BS>
+__device__ __forceinline__ void launch_max(unsigned long long* maxbits, double mx) {
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+  if (gridDim.x == 1) {
+    if ((threadIdx.x & 63) == 0) atomic_max_nonneg(maxbits, mx);
+    return;
+  }
+  __shared__ double wmax[BS / 64];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < BS / 64; w++) mx = fmax(mx, wmax[w]);
+    atomic_max_nonneg(maxbits + (blockIdx.x % kMaxSlots) * kMaxSlotStride, mx);
+  }
+}
+
 template <int OP>
 struct OpCoef {
   double ix, iy, iz, fac, lambda;

@@ -186,6 +186,8 @@ struct omg_free_state;    // free-space boundary conditions (omg_api.cpp, omg_fr
 
 namespace omg {
 struct TailArgs;   // omg_kernels.h
+// slots of a multi-workgroup max-residual launch (launch_max, omg_device.h)
+constexpr int kMaxSlots = 256, kMaxSlotStride = 16;
 }
 
 struct omg_ctx {
@@ -232,6 +234,7 @@ struct omg_ctx {
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch
+  unsigned long long* d_maxslots = nullptr;   // launch_max slots (kept zeroed)
   // arguments of the coarse-tail kernel in device memory (a by-value kernel
   // argument indexed by level is copied to scratch per lane); uploaded when
   // they change

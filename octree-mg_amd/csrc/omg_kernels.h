@@ -46,6 +46,7 @@ void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st);
 void launch_box_op(const LevelView& L, int op, double lambda, int i_out, hipStream_t st);
 void launch_residual(const LevelView& L, int op, double lambda, unsigned long long* maxbits,
                      hipStream_t st);
+void launch_max_fold(unsigned long long* slots, unsigned long long* out, bool accumulate, hipStream_t st);
 void launch_fill_gc(const LevelView& L, int iv, int colours, const LevelView& C, const RBRec* rb,
                     const GcBC& bc, double* sendbuf, hipStream_t st);
 void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, const double* recv,

@@ -377,10 +377,29 @@ __global__ void __launch_bounds__(256) k_residual(LevelView L, double lambda, un
     boxp(L, 4, b)[o] = res;
     mx = fmax(mx, fabs(res));
   }
-  if (maxbits) {
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
-    if ((threadIdx.x & 63) == 0) atomic_max_nonneg(maxbits, mx);
+  if (maxbits) launch_max<256>(maxbits, mx);
+}
+
+// Folds the kMaxSlots slots of launch_max into *out (into max(*out, .) when
+// accumulating over levels) and zeroes them.
+__global__ void __launch_bounds__(kMaxSlots) k_max_fold(unsigned long long* slots, unsigned long long* out,
+                                                        int accumulate) {
+  unsigned long long* s = slots + threadIdx.x * kMaxSlotStride;
+  double mx = __longlong_as_double((long long)*s);
+  *s = 0ull;
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+  __shared__ double wmax[kMaxSlots / 64];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kMaxSlots / 64; w++) mx = fmax(mx, wmax[w]);
+    if (accumulate) mx = fmax(mx, __longlong_as_double((long long)*out));
+    *out = (unsigned long long)__double_as_longlong(mx);
   }
+}
+
+void launch_max_fold(unsigned long long* slots, unsigned long long* out, bool accumulate, hipStream_t st) {
+  k_max_fold<<<1, kMaxSlots, 0, st>>>(slots, out, accumulate ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------

@@ -131,10 +131,7 @@ __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const Le
     rv[r] = make_double2(r0, r1);
     st_nt(res + 2 * q2, r0, r1);
   }
-  if (maxbits) {
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
-    if ((tid & 63) == 0) atomic_max_nonneg(maxbits, mx);
-  }
+  if (maxbits) launch_max<BS>(maxbits, mx);
   if (!restrict_on || parent_local[b] < 0) return;
 
   // restrict_onto (m_restrict.f90:165-214): phi, then res, onto the parent's
