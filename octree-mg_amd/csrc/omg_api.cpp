@@ -549,6 +549,11 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     launch_max_fold(c->d_maxslots, d, l > lo, c->stream);
   }
   HIPCHK(hipMemcpyAsync(c->h_scalar, d, 8, hipMemcpyDeviceToHost, c->stream));
+  if (c->capturing) {   // run_cycle reads it once the graph has run
+    if (c->max_deferred) throw OmgError("internal: two max-residual readbacks in one captured cycle");
+    c->max_deferred = true;
+    return 0.0;
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
   return c->h_scalar[0];
 }
@@ -1060,18 +1065,12 @@ void run_tail(omg_ctx* c, int top) {
               lds_box_ok(top, 16);
   const bool tail_timing = c->tail_timing;
   if (tail_timing) {
-    if (!c->d_tail_stamps) HIPCHK(hipMalloc(&c->d_tail_stamps, 8 * 64));
+    if (!c->d_tail_stamps) HIPCHK(hipMalloc(&c->d_tail_stamps, 8 * 64));   // (never captured: graph_ok)
     A.stamps = c->d_tail_stamps;
   }
-  if (!c->d_tail) {
-    HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
-    c->h_tail = new TailArgs;
-    std::memset(c->h_tail, 0xff, sizeof(TailArgs));
-  }
   if (std::memcmp(&A, c->h_tail, sizeof(TailArgs)) != 0) {
-    *c->h_tail = A;
-    // pageable source: the copy is staged before the call returns
-    HIPCHK(hipMemcpyAsync(c->d_tail, c->h_tail, sizeof(TailArgs), hipMemcpyHostToDevice, c->stream));
+    *c->h_tail = A;   // what d_tail holds once the stream gets here
+    launch_store_tail(A, c->d_tail, c->stream);
   }
   {
     Prof p(c, "coarse_tail", 0.0, top);
@@ -1194,6 +1193,65 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
   return max_res;
 }
 
+// A whole cycle (V-cycle or FMG) as one HIP graph: the host logic runs as
+// usual while the stream is captured, so every kernel argument and every
+// host-side state change is exactly that of the direct launches; the graph of
+// the previous call with the same key is updated in place (same topology) or
+// re-instantiated, then launched.  A graph issues a dependent kernel in ~1.8
+// us of host time against ~3.2 us direct (tools/graph_probe.hip), but the
+// cycles measured no faster (C1 0.252 -> 0.260 ms, C4 0.553 -> 0.568, 512^3
+// FMG 11.65 -> 11.49): their small-level kernels are bound by their own
+// 3-5 us on the GPU, not by the host, and capturing costs what it saves.
+// Opt-in (OMG_GRAPH=1).  Only where the cycle never waits for the host:
+// one GPU, no subtract_mean (its side-stream chain spans calls), every
+// V-cycle ends in the coarse tail (the level-by-level coarse solve reads its
+// residual back per sweep), no profiling.
+bool graph_ok(omg_ctx* c) {
+  return !c->no_graph && !c->capturing && c->n_ranks == 1 && !c->subtract_mean && !c->profiling &&
+         !c->tail_timing && !c->no_tail && c->n_boxes > 0 && tail_top(c, c->highest) >= c->lowest;
+}
+
+template <typename F>
+double run_cycle(omg_ctx* c, int key, F&& body) {
+  if (!graph_ok(c)) return body();
+  c->capturing = true;
+  c->max_deferred = false;
+  HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  hipGraph_t g = nullptr;
+  try {
+    body();
+  } catch (...) {
+    c->capturing = false;
+    (void)hipStreamEndCapture(c->stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    throw;
+  }
+  c->capturing = false;
+  HIPCHK(hipStreamEndCapture(c->stream, &g));
+  size_t n_nodes = 0;
+  HIPCHK(hipGraphGetNodes(g, nullptr, &n_nodes));
+  if (n_nodes) {
+    hipGraphExec_t& ex = c->graphs[key];
+    if (ex) {
+      hipGraphNode_t err_node = nullptr;
+      hipGraphExecUpdateResult res;
+      if (hipGraphExecUpdate(ex, g, &err_node, &res) != hipSuccess || res != hipGraphExecUpdateSuccess) {
+        (void)hipGetLastError();
+        HIPCHK(hipGraphExecDestroy(ex));
+        ex = nullptr;
+      }
+    }
+    if (!ex) HIPCHK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphLaunch(ex, c->stream));
+  }
+  HIPCHK(hipGraphDestroy(g));
+  if (!c->max_deferred) return 0.0;
+  c->max_deferred = false;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return c->h_scalar[0];
+}
+
 // mg_set_methods' operator part + *_set_lambda (m_multigrid.f90:27-60,
 // m_helmholtz.f90:39-46, m_vhelmholtz.f90:51-58, m_ahelmholtz.f90:59-66)
 void set_operator(omg_ctx* c, int op, double lambda) {
@@ -1253,11 +1311,12 @@ void diffusion_solve(omg_ctx* c, int op, double dt, double coeff, int order, dou
     set_operator(c, op, 2 / dtc);
     set_rhs(c, -2 / dtc, -1.0);
   }
-  double res = fas_fmg(c, true, true);
+  double res = run_cycle(c, 2 + 2 + 4, [&] { return fas_fmg(c, true, true); });
   int n = 1;
   for (; n <= kDiffusionMaxIts; n++) {
     if (res <= max_res) break;
-    res = fas_vcycle(c, c->lowest - 1, true, true);
+    res = run_cycle(c, 1 + 2 + 4 + 8 * (c->lowest - 1 + 64),
+                    [&] { return fas_vcycle(c, c->lowest - 1, true, true); });
   }
   if (n_vcycles) *n_vcycles = n - 1;
   if (res_out) *res_out = res;
@@ -1596,7 +1655,9 @@ double poisson_free_3d(omg_ctx* c, bool new_rhs, double max_fft_frac, bool fmgcy
     S->initialized = true;
   }
   if (fft_lvl < c->highest)   // :201-208
-    return fmgcycle ? fas_fmg(c, true, want_max_res) : fas_vcycle(c, c->lowest - 1, want_max_res, true);
+    return run_cycle(c, 16 + (want_max_res ? 2 : 0) + (fmgcycle ? 1 : 0), [&] {
+      return fmgcycle ? fas_fmg(c, true, want_max_res) : fas_vcycle(c, c->lowest - 1, want_max_res, true);
+    });
   return 0.0;
 }
 
@@ -1978,6 +2039,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
     c->tail_timing = getenv("OMG_TAIL_TIMING") != nullptr;
     c->no_fill_tile = getenv("OMG_NO_FILL_TILE") != nullptr;
+    c->no_graph = getenv("OMG_GRAPH") == nullptr;
     c->no_fuse_down = getenv("OMG_NO_FUSE_DOWN") != nullptr;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1985,6 +2047,10 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMalloc(&c->d_maxslots, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
+    // (allocated here: no allocation may happen while a cycle is captured)
+    HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
+    c->h_tail = new TailArgs;
+    std::memset(c->h_tail, 0xff, sizeof(TailArgs));
     HIPCHK(hipMemset(c->d_maxslots, 0, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->stream_comm, hipStreamNonBlocking));
@@ -2042,6 +2108,9 @@ int omg_ctx_destroy(omg_ctx* c) {
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_maxslots);
+    for (auto& kv : c->graphs)
+      if (kv.second) (void)hipGraphExecDestroy(kv.second);
+    c->graphs.clear();
     dfree(c->d_stage);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);
@@ -2306,14 +2375,16 @@ int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
 
 int omg_fas_vcycle(omg_ctx* c, int highest_lvl, int want_max_res, double* max_res, int standalone) {
   return guarded([&] {
-    const double r = fas_vcycle(c, highest_lvl, want_max_res != 0, standalone != 0);
+    const double r = run_cycle(c, 1 + (want_max_res ? 2 : 0) + 4 * (standalone != 0) + 8 * (highest_lvl + 64),
+                               [&] { return fas_vcycle(c, highest_lvl, want_max_res != 0, standalone != 0); });
     if (want_max_res && max_res) *max_res = r;
   });
 }
 
 int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
   return guarded([&] {
-    const double r = fas_fmg(c, have_guess != 0, want_max_res != 0);
+    const double r = run_cycle(c, 2 + (want_max_res ? 2 : 0) + 4 * (have_guess != 0),
+                               [&] { return fas_fmg(c, have_guess != 0, want_max_res != 0); });
     if (want_max_res && max_res) *max_res = r;
   });
 }

@@ -246,6 +246,12 @@ struct omg_ctx {
   double* d_stage = nullptr;           // upload/download staging (reference layout)
   size_t stage_n = 0;
   omg_free_state* free_state = nullptr;   // m_free_space's free_bc (created on first use)
+  // cycles as HIP graphs (run_cycle): each call is captured, its executable
+  // graph updated in place and launched
+  bool no_graph = true;                // unless OMG_GRAPH is set: launch kernel by kernel
+  bool capturing = false;              // inside a capture: no host synchronisation
+  bool max_deferred = false;           // the max residual is read after the graph ran
+  std::map<int, hipGraphExec_t> graphs;   // by entry (run_cycle's key)
   // profiling
   bool profiling = false;
   std::map<std::string, omg::KStat> stats;

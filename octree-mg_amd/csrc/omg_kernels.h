@@ -110,6 +110,7 @@ struct TailArgs {
 // how many of the tail's lowest levels qualify for the LDS-resident program
 constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
+void launch_store_tail(const TailArgs& A, TailArgs* d, hipStream_t st);   // *d = A in stream order
 
 // LDS-tiled fused kernels (omg_tiles.hip), even box sizes 2..16
 bool tiled_nc(int nc);

@@ -1660,6 +1660,23 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
   if (threadIdx.x == 0) *A.coarse_its = its;
 }
 
+// The tail's arguments into device memory, carried as a kernel argument (a
+// captured graph keeps its own copy; a pageable memcpy node would read the host
+// buffer when the graph runs). The struct is the first kernel argument, at
+// offset 0 of the kernarg segment: read it from there as words, vector stores.
+__global__ void __launch_bounds__(256) k_store_tail(TailArgs A, TailArgs* d) {
+  (void)A;
+  static_assert(sizeof(TailArgs) % 4 == 0, "TailArgs is copied as 32-bit words");
+  typedef const __attribute__((address_space(4))) unsigned kword;
+  kword* s = (kword*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned* o = reinterpret_cast<unsigned*>(d);
+  for (int i = threadIdx.x; i < (int)(sizeof(TailArgs) / 4); i += blockDim.x) o[i] = s[i];
+}
+
+void launch_store_tail(const TailArgs& A, TailArgs* d, hipStream_t st) {
+  k_store_tail<<<1, 256, 0, st>>>(A, d);
+}
+
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st) {
   if (op == OP_HELM) {
     if (gs_lex)

@@ -190,3 +190,20 @@ def test_fused_down_substep_other_cycle_counts(down, up):
     for _ in range(3):
         assert dev.vcycle(True) == orc.vcycle(True)
         _assert_same(dev, orc, ivs=(1, 2, 3, 4))
+
+
+# the cycles captured as HIP graphs (OMG_GRAPH=1, read at context creation):
+# the same bits as the direct launches, on non-periodic one-GPU goldens (the
+# cases the graph path takes) with V-cycles, FMG and max-residual readbacks
+GRAPH_CASES = [n for n in ONE_RANK if " per " not in GOLDEN[n]["args"]][:6]
+
+
+@pytest.mark.parametrize("name", GRAPH_CASES)
+def test_graph_cycles_match_golden(name, monkeypatch):
+    monkeypatch.setenv("OMG_GRAPH", "1")
+    e = GOLDEN[name]
+    run = e["runs"]["1"]
+    out = run_problem(e["args"], backend="device")
+    assert out["history"] == run["history"]
+    if "phi_sha256" in run:
+        assert out["phi_sha256"] == run["phi_sha256"]
