@@ -751,11 +751,21 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
 // box of lvl+1 has its parent on this GPU and no refinement boundary.
 // then_gsrb: the caller smooths lvl+1 with red-black substeps right after
 // (colour 1 first), so colour 1's correction is dead where no face needs it.
-void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false) {
+// save_old (FMG, fused path only, see correct_fill_fused): old = phi of lvl+1
+// before the correction, the interior written by the fused kernel.
+bool correct_fill_fused(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
-  if (F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
-      !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv))) {
+  return F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
+         !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv));
+}
+
+void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false, bool save_old = false) {
+  Level* F = level_ptr(c, lvl + 1);
+  Level* C = level_ptr(c, lvl);
+  if (save_old && (then_gsrb || !correct_fill_fused(c, lvl)))
+    throw OmgError("internal: old = phi fused into an unfused correction");
+  if (correct_fill_fused(c, lvl)) {
     // every parent here has all its children on this GPU (no prolongation
     // traffic, every fine box has a local parent): the children form res
     const bool sub = (size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc;
@@ -766,7 +776,7 @@ void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false) {
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
-                          F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream);
+                          F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream, nullptr, 0, save_old);
     }
     finish_halo(c, F, 1);
     F->phi_gc_ok = true;
@@ -1182,9 +1192,16 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
     // parent, update_coarse's parent loop above left old equal to phi, ghost
     // faces included, and nothing has written that level since (unless the
     // cycles below subtract phi's mean, which covers every level)
+    // Elsewhere the copy's interior half rides on the fused correction, which
+    // loads the pre-correction interior anyway: only the ghost faces are copied
     const bool old_is_phi = l < c->highest && L && L->all_parents && !c->subtract_mean;
-    if (L && L->n && !old_is_phi) launch_copy_var(L->view(), 1, 3, c->stream);
-    if (l > c->lowest) correct_and_fill(c, l - 1);
+    const bool save_old = L && L->n && !old_is_phi && l > c->lowest && correct_fill_fused(c, l - 1);
+    if (save_old) {
+      launch_copy_ghosts(L->view(), c->stream);
+    } else if (L && L->n && !old_is_phi) {
+      launch_copy_var(L->view(), 1, 3, c->stream);
+    }
+    if (l > c->lowest) correct_and_fill(c, l - 1, false, save_old);
     if (l == c->highest)
       max_res = fas_vcycle(c, l, want_max_res, false);
     else

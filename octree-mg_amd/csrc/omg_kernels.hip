@@ -862,6 +862,21 @@ void launch_set_rhs(const LevelView& L, const int* leaves, int n_leaves, double 
   k_set_rhs<<<grid_for(work), 256, 0, st>>>(L, leaves, n_leaves, f1, f2);
 }
 
+__global__ void __launch_bounds__(256) k_copy_ghosts(LevelView L) {
+  const long long per = (L.stride - 2LL * L.hv) / 2;   // 16-B pairs per box
+  GRID_STRIDE(t, per * L.n) {
+    const int b = (int)(t / per);
+    const long long o = 2LL * L.hv + 2 * (t % per);
+    *reinterpret_cast<double2*>(boxp(L, 3, b) + o) = *reinterpret_cast<const double2*>(boxp(L, 1, b) + o);
+  }
+}
+
+void launch_copy_ghosts(const LevelView& L, hipStream_t st) {
+  const long long work = (L.stride - 2LL * L.hv) / 2 * L.n;
+  if (work <= 0) return;
+  k_copy_ghosts<<<grid_for(work), 256, 0, st>>>(L);
+}
+
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st) {
   const long long work = (long long)L.stride * L.n;
   if (work == 0) return;

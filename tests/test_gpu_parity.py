@@ -207,3 +207,21 @@ def test_graph_cycles_match_golden(name, monkeypatch):
     assert out["history"] == run["history"]
     if "phi_sha256" in run:
         assert out["phi_sha256"] == run["phi_sha256"]
+
+
+@pytest.mark.parametrize("args", ["8 32 32 32 1 f gsrb lpl 0 sol sol 1 lb 0",
+                                  "16 64 64 64 1 f gsrb lpl 0 sol sol 1 lb 0",
+                                  "8 32 32 32 1 f gs helm 3.5 n0 sol 1 lb 0",
+                                  "8 32 32 32 1 f gsrb lpl 0 per sol 1 lb 0"])
+@pytest.mark.parametrize("have_guess", [False, True])
+def test_fmg_full_state_matches_oracle(args, have_guess):
+    """Every stored cell of phi, rhs, old and res after FMG calls: FMG's
+    old = phi (m_multigrid.f90:127-129) is partly fused into the correction
+    kernel and partly skipped where update_coarse left old = phi already."""
+    cfg = parse(args)
+    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+    for be in (dev, orc):
+        setup_problem(be)
+    for _ in range(2):
+        assert dev.fmg(have_guess, True) == orc.fmg(have_guess, True)
+        _assert_same(dev, orc, ivs=(1, 2, 3, 4))
