@@ -444,7 +444,7 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (L->n) {
     Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc, lvl);
     if (iv != 1 || L->has_rb || c->no_fill_tile ||
-        !launch_fill_tile(L->view(), bc_for(c, lvl, iv), L->d_sendbuf, c->stream))
+        !launch_fill_tile(L->sweep_view(), bc_for(c, lvl, iv), L->d_sendbuf, c->stream))
       launch_fill_gc(L->view(), iv, 3, view_of(c, lvl - 1), L->d_rb, bc_for(c, lvl, iv), L->d_sendbuf,
                      c->stream);
   }
@@ -496,7 +496,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       // writes remote faces only)
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_bnd * L->nc * L->nc * L->nc, lvl);
-        launch_gs_substep(L->view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
+        launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
                           bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_bnd, L->n_bnd);
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
@@ -506,7 +506,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_int * L->nc * L->nc * L->nc, lvl);
-        launch_gs_substep(L->view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
+        launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
                           bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int);
       }
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
@@ -516,7 +516,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     }
     if (L->n) {
       Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc, lvl);
-      launch_gs_substep(L->view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
+      launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
                         L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream);
     }
     finish_halo(c, L, 1);
@@ -534,7 +534,7 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
   if (!L || L->n == 0) return;
   Prof p(c, "residual", (double)L->n * L->nc * L->nc * L->nc, lvl);
   if (tiled_level(c, L))
-    launch_resid_restrict(L->view(), empty_view(), c->op, c->lambda, maxbits, 0, nullptr, nullptr, c->stream);
+    launch_resid_restrict(L->sweep_view(), empty_view(), c->op, c->lambda, maxbits, 0, nullptr, nullptr, c->stream);
   else
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
@@ -656,24 +656,24 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       {
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
-        if (!launch_smooth_resid(F->view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
+        if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
                                  F->d_dix, c->stream, F->d_int, F->n_int))
           throw OmgError("smooth_resid: not available for this level");
       }
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
       {
         Prof p(c, "resid_restrict", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl);
-        launch_resid_restrict(F->view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+        launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
                               F->d_dix, c->stream, F->d_bnd, F->n_bnd);
       }
     } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
-      if (!launch_smooth_resid(F->view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
+      if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
                                F->d_dix, c->stream))
         throw OmgError("smooth_resid: not available for this level");
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
-      launch_resid_restrict(F->view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+      launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
                             F->d_dix, c->stream);
     }
     restrict_remote(c, 1, lvl);
@@ -687,7 +687,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
   Level* C = level_ptr(c, lvl - 1);
   if (C && !C->parents.empty()) {
     Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl - 1);
-    if (!launch_coarse_rhs_tile(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream))
+    if (!launch_coarse_rhs_tile(C->sweep_view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream))
       launch_coarse_rhs(C->view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream);
   }
 }
@@ -719,7 +719,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
   {
     const int n = split ? F->n_int : F->n;
     Prof p(c, "prolong_smooth", (double)n * F->nc * F->nc * F->nc, lvl + 1);
-    launch_prolong_smooth(C->view(), F->view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
+    launch_prolong_smooth(C->view(), F->sweep_view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
                           bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, split ? F->d_int : nullptr, n,
                           split ? F->d_push0 : nullptr, c->stream);
   }
@@ -729,7 +729,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
     // same-GPU neighbours above pushed them the corrected colour 0 (push0)
     {
       Prof p(c, "prolong_fill", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl + 1);
-      launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
+      launch_prolong_fill(C->view(), F->sweep_view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
                           F->d_sendbuf, true, !c->no_skip1, c->stream, F->d_bnd, F->n_bnd);
     }
     finish_halo(c, F, 1);
@@ -775,7 +775,7 @@ void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false, bool save_old
     }
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
-      launch_prolong_fill(C->view(), F->view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
+      launch_prolong_fill(C->view(), F->sweep_view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
                           F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream, nullptr, 0, save_old);
     }
     finish_halo(c, F, 1);
@@ -835,7 +835,7 @@ void leaf_box_sums(omg_ctx* c, int iv, int ch, hipStream_t st) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
     Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
-    launch_box_sums(L->view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
+    launch_box_sums(L->sweep_view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
   }
 }
 
@@ -957,7 +957,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       if (mode == kInCycle && L->all_parents) continue;
       Prof p(c, "subtract_rhs", (double)L->n * L->nc * L->nc * L->nc, l);
       if (l >= 1 && (int)L->leaves.size() == L->n && subtract_sums_nc(L->nc))
-        launch_subtract_sums(L->view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
+        launch_subtract_sums(L->sweep_view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
       else {
         launch_subtract(L->view(), 2, red_mean(c, kChRhs), 0, c->stream);
         if (l >= 1 && !L->leaves.empty()) all_fused = false;

@@ -54,10 +54,11 @@ __device__ __forceinline__ void pair_stencil(const double* so, const double* gb,
 
 // Bijective blockIdx -> box map giving each XCD one contiguous run of boxes
 // (workgroups are dealt round-robin over the 8 XCDs), so Morton-close
-// neighbour boxes share an L2.  Speed only, never correctness.
-__device__ __forceinline__ int xcd_box(int bid, int nb) {
+// neighbour boxes share an L2.  rev: each XCD walks its run backwards (the
+// level's passes alternate, LevelView::rev).  Speed only, never correctness.
+__device__ __forceinline__ int xcd_box(int bid, int nb, int rev = 0) {
   const int q = nb >> 3, r = nb & 7, x = bid & 7, pos = bid >> 3;
-  return x * q + min(x, r) + pos;
+  return x * q + min(x, r) + (rev ? q + (x < r) - 1 - pos : pos);
 }
 
 // physical ghost (set_ghost_cells + bc_to_gc, m_ghost_cells.f90:264-283, 682-766)

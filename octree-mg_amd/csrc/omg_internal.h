@@ -10,6 +10,7 @@
 // transfers, and the per-peer RCCL pack lists for multi-GPU halos.
 #pragma once
 
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -53,6 +54,7 @@ struct LevelView {
   const int8_t* nbk;     // [n*6]
   const int* nba;        // [n*6]
   const int* sendpos;    // [n*6] halo send slot of remote faces (or -1)
+  int rev;               // walk each XCD's run of boxes backwards (xcd_box)
 };
 
 // stored doubles per box and variable for box size nc (2 colours + 6 faces)
@@ -163,6 +165,20 @@ struct Level {
     v.nbk = d_nbk;
     v.nba = d_nba;
     v.sendpos = d_sendpos;
+    v.rev = 0;
+    return v;
+  }
+  // the view for a level-wide pass: successive passes walk the boxes in
+  // alternating directions, so each starts on the boxes the previous one
+  // touched last (still in the 256 MiB Infinity Cache) instead of the ones
+  // it touched first (evicted long ago)
+  // (OMG_NO_REV=1: always forwards, for A/B timing)
+  mutable int dir = 0;
+  LevelView sweep_view() const {
+    static const int on = getenv("OMG_NO_REV") ? 0 : 1;
+    LevelView v = view();
+    v.rev = dir & on;
+    dir ^= 1;
     return v;
   }
 };

@@ -30,7 +30,7 @@ __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, in
                                                   double* __restrict__ sendbuf, const double* __restrict__ shift,
                                                   const int* __restrict__ boxes, RbSide rbs) {
   __shared__ double lds[gsrb_lds<NC>()];
-  const int q = xcd_box(blockIdx.x, gridDim.x);
+  const int q = xcd_box(blockIdx.x, gridDim.x, L.rev);
   gsrb_box<NC, OP, BS, NT, false, RB>(L, lambda, e, colours, bc, sendbuf, shift, boxes ? boxes[q] : q, lds,
                                       nullptr, &rbs);
 }
@@ -53,22 +53,25 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   const dim3 g(boxes ? n_boxes : L.n);
   if (g.x == 0) return;
   const RbSide rbs{C, has_rb ? rb : nullptr};
+#ifndef OMG_GS_NT
+#define OMG_GS_NT 2
+#endif
 #define OMG_TILE_RB(NC, BS, RB)                                                                    \
   switch (op) {                                                                                      \
     case OP_HELM:                                                                                    \
-      k_gsrb_tile<NC, OP_HELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_HELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_VLPL:                                                                                    \
-      k_gsrb_tile<NC, OP_VLPL, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_VLPL, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_VHELM:                                                                                   \
-      k_gsrb_tile<NC, OP_VHELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_VHELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_AHELM:                                                                                   \
-      k_gsrb_tile<NC, OP_AHELM, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_AHELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     default:                                                                                         \
-      k_gsrb_tile<NC, OP_LPL, BS, 2, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_LPL, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
   }
 #define OMG_TILE(NC, BS)          \
   if (has_rb)                     \

@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(BS) k_resid_restrict(LevelView F, LevelView Cv
                                                        const int* parent_local, const int* dixp,
                                                        const int* list) {
   __shared__ double sb[Tl<NC>::NST];
-  const int q = xcd_box(blockIdx.x, gridDim.x);
+  const int q = xcd_box(blockIdx.x, gridDim.x, F.rev);
   resid_restrict_box<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp, list ? list[q] : q, sb);
 }
 
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   constexpr int H = NC / 2, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS;
   constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
   __shared__ double sb[TL::NST];
-  const int tid = threadIdx.x, bq = xcd_box(blockIdx.x, gridDim.x), b = list ? list[bq] : bq;
+  const int tid = threadIdx.x, bq = xcd_box(blockIdx.x, gridDim.x, F.rev), b = list ? list[bq] : bq;
   const long long boff = (long long)b * F.stride;
   double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, 
                                                      const int* parent_local, const int* dixp, GcBC bc,
                                                      double* sendbuf, int skip1, const int* list, int save_old) {
   __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
-  const int t = xcd_box(blockIdx.x, gridDim.x);
+  const int t = xcd_box(blockIdx.x, gridDim.x, F.rev);
   prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, list ? list[t] : t, lds, skip1 != 0,
                                 save_old != 0);
 }
@@ -682,7 +682,7 @@ __global__ void __launch_bounds__(BS, OMG_PS_WAVES) k_prolong_smooth(LevelView C
                                                        const int* parent_local, const int* dixp, GcBC bc,
                                                        int one_child, const int* list, const uint8_t* push0) {
   __shared__ double lds[prolong_smooth_lds<NC>()];
-  const int t = xcd_box(blockIdx.x, gridDim.x);
+  const int t = xcd_box(blockIdx.x, gridDim.x, F.rev);
   prolong_smooth_box<NC, OP, BS>(Cv, F, lambda, parent_local, dixp, bc, one_child, push0, list ? list[t] : t, lds);
 }
 
@@ -745,7 +745,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
   constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
   constexpr int NCH = NC * NC / R;
   __shared__ double lds[LPW * P];
-  const int lane = threadIdx.x, b0 = blockIdx.x * LPW;
+  const int lane = threadIdx.x, b0 = (L.rev ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * LPW;
   const long long hv = L.hv;
   double* src[PER];
   int dst[PER];
@@ -874,7 +874,7 @@ template <int NC, int BS>
 __global__ void __launch_bounds__(BS) k_fill_tile(LevelView L, GcBC bc, double* sendbuf) {
   constexpr int HV = Tl<NC>::HV;
   __shared__ double sb[2 * HV];
-  const int b = xcd_box(blockIdx.x, gridDim.x);
+  const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
   const double* u = L.phi + (long long)b * L.stride;
   for (int q = threadIdx.x; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
   __syncthreads();
@@ -1023,7 +1023,7 @@ __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambd
 template <int NC, int OP, int BS>
 __global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
   __shared__ double sb[Tl<NC>::NST];
-  coarse_rhs_box<NC, OP, BS, true>(Cv, lambda, parents[xcd_box(blockIdx.x, gridDim.x)], sb);
+  coarse_rhs_box<NC, OP, BS, true>(Cv, lambda, parents[xcd_box(blockIdx.x, gridDim.x, Cv.rev)], sb);
 }
 
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
