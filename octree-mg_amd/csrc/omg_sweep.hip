@@ -47,31 +47,39 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   GcBC b2 = bc;
   b2.phi_stored = bc.phi_stored;  // iv == 1 here
   // 16^3 boxes: 8 waves per box (4 boxes = 32 waves per CU, the LDS of 4
-  // boxes fits); streaming loads/stores are non-temporal: nothing a substep
-  // reads or writes is touched again before the next substep has swept the
-  // level, far beyond L2 / MALL at the sizes that matter.
+  // boxes fits); streaming loads/stores are non-temporal on large levels:
+  // nothing a substep reads or writes is touched again before the next
+  // substep has swept the level, far beyond L2 / MALL.  A level whose phi and
+  // rhs fit in about 1.5x the 256 MiB Infinity Cache streams with the default
+  // policy, so that the next pass (walking the other way) re-reads what this
+  // one touched last from the cache (OMG_GS_NT_BYTES: the bound, bytes).
+  // Measured -1 to -2 % per cycle at 256^3 (Laplacian, Helmholtz); the
+  // operators that also read eps lost 2-8 % and stay non-temporal.
+  static const long long nt_bytes = getenv("OMG_GS_NT_BYTES") ? atoll(getenv("OMG_GS_NT_BYTES")) : 400ll << 20;
+  const bool cached = (op == OP_LPL || op == OP_HELM) && 2ll * 8 * L.stride * L.n <= nt_bytes;
   const dim3 g(boxes ? n_boxes : L.n);
   if (g.x == 0) return;
   const RbSide rbs{C, has_rb ? rb : nullptr};
 #ifndef OMG_GS_NT
 #define OMG_GS_NT 2
 #endif
+#define OMG_GS_NT_NOW OMG_GS_NT
 #define OMG_TILE_RB(NC, BS, RB)                                                                    \
   switch (op) {                                                                                      \
     case OP_HELM:                                                                                    \
-      k_gsrb_tile<NC, OP_HELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_HELM, BS, OMG_GS_NT_NOW, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_VLPL:                                                                                    \
-      k_gsrb_tile<NC, OP_VLPL, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_VLPL, BS, OMG_GS_NT_NOW, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_VHELM:                                                                                   \
-      k_gsrb_tile<NC, OP_VHELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_VHELM, BS, OMG_GS_NT_NOW, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     case OP_AHELM:                                                                                   \
-      k_gsrb_tile<NC, OP_AHELM, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_AHELM, BS, OMG_GS_NT_NOW, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
       break;                                                                                         \
     default:                                                                                         \
-      k_gsrb_tile<NC, OP_LPL, BS, OMG_GS_NT, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
+      k_gsrb_tile<NC, OP_LPL, BS, OMG_GS_NT_NOW, RB><<<g, dim3(BS), 0, st>>>(L, lambda, e, colours, b2, sendbuf, shift, boxes, rbs); \
   }
 #define OMG_TILE(NC, BS)          \
   if (has_rb)                     \
@@ -79,7 +87,17 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   else                            \
     OMG_TILE_RB(NC, BS, false)
   switch (L.nc) {
-    case 16: OMG_TILE(16, 512) break;
+    case 16:
+      if (cached) {
+#undef OMG_GS_NT_NOW
+#define OMG_GS_NT_NOW 0
+        OMG_TILE(16, 512)
+      } else {
+#undef OMG_GS_NT_NOW
+#define OMG_GS_NT_NOW OMG_GS_NT
+        OMG_TILE(16, 512)
+      }
+      break;
     case 8: OMG_TILE(8, 256) break;
     case 4: OMG_TILE(4, 256) break;
     default: OMG_TILE(2, 256) break;
