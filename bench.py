@@ -1,21 +1,37 @@
 #!/usr/bin/env python3
-"""Benchmark: FAS V-cycles of the 3D Poisson problem, 512^3 per GPU.
+"""Benchmark: FAS V-cycles of the 3D Poisson problem.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N ... bench.py --gpus N ...     (one rank per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode weak|strong|weak256]
+    torchrun --nproc-per-node N ... bench.py --gpus N ...      (one rank per GPU)
+
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset) the script
+launches its N ranks itself: N child processes (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* set, one GPU each) started before this process touches
+the GPU; rank 0 prints the line.
 
 A "step" is one mg_fas_vcycle over the whole tree: box 16, fully periodic
-(so subtract_mean runs twice per cycle), red-black Gauss-Seidel, n_cycle_down =
-n_cycle_up = 2.  Weak scaling: every GPU owns a 512^3 octant (Morton chunks of
-mg_load_balance); the global domain is 512^3 x (1,1,1)/(2,1,1)/(2,2,1)/(2,2,2).
-Input is synthetic: u = prod(sin(2 pi 5 x)), rhs = L_h u on every level, phi0 = 0.
+(so subtract_mean runs twice per cycle), red-black Gauss-Seidel, n_cycle_down
+= n_cycle_up = 2.  Input is synthetic: u = prod(sin(2 pi 5 x)), rhs = L_h u on
+every level, phi0 = 0.  Partition: mg_load_balance's Morton chunks, one rank
+per GPU, halos over RCCL (ncclSend/ncclRecv).
+
+Modes (the domain for N ranks):
+  weak     (default) 512^3 per GPU: 512^3 x (1,1,1)/(2,1,1)/(2,2,1)/(2,2,2);
+           N = 1 is BASELINE's C3 workload on one GPU
+  strong   512^3 in total over the N GPUs (C3 exactly, "512^3, 8xMI355X")
+  weak256  SURVEY §8(d)'s weak curve: 256^3 per GPU, 512^3 at N = 8
+With N > 1 in weak mode the line also carries "c3_strong": the 512^3 problem
+split over the same N GPUs, timed the same way.  Every line carries
+"c4_refined": the one-level-refined octree of BASELINE's C4 (test_refinement,
+128^3 base, box 16, n_levels 2) split over the N ranks.
 
 value = finest-level cells x V-cycles / s over all ranks (the BASELINE metric).
-roofline: the red-black smoother kernel, algorithmic 12 B per level cell per
-substep (24 B per cell update), timed with HIP events on the
-library's stream in a separate pass, against 8 TB/s HBM3E.
+roofline: the red-black smoother kernel on the finest level, algorithmic 12 B
+per level cell per substep (24 B per cell update), timed with
+HIP events on the library's stream in a separate profiled cycle, against
+8 TB/s HBM3E; traffic from the committed rocprofv3 PMC summary.
 cpu_baseline: the reference itself (oracle/_ref, amdflang -O2 + MPICH) on the
-host cores, one V-cycle of the same 512^3 problem.
+host cores of this box at P = 1, 8 and the job's CPU share (rank 0, N = 1).
 """
 from __future__ import annotations
 
@@ -23,6 +39,7 @@ import argparse
 import json
 import os
 import re
+import socket
 import subprocess
 import sys
 import time
@@ -34,22 +51,20 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
-PER_GPU = 512
 BOX = 16
 REPLICATE_CELLS = int(os.environ.get("OMG_REPLICATE_CELLS", 64 * 16 ** 3))
-# V-cycles of the reference's CPU path in the cpu_baseline sample (~0.7-0.9 s
-# each at 512^3 on 8 host cores: ~10 s of CPU work)
-CPU_CYCLES = 12
-
+C4_ARGS = "16 128 128 128 10 v gsrb lpl 0 sol sol 2 lb 0"   # omg_golden / tests.mgdriver form
+METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512^3"
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
 # also reports what these do not account for
 KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
                    "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
+COMM_FAMILIES = ("comm", "comm_overlap")
 
 
-def pmc_traffic():
+def pmc_traffic(per_gpu_cells):
     """HBM bytes per launch of the finest-level smoother from the newest
     committed PMC summary (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2
     + WRITE_SIZE, the MI355X guide's gfx950 correction), or None."""
@@ -59,7 +74,7 @@ def pmc_traffic():
             d = json.load(open(f))
             for k, e in d["kernels"].items():
                 if re.match(r"void omg::k_gsrb_tile<16, 1[,>]", k) and "hbm_bytes_per_launch" in e:
-                    if e["workgroups"] == (PER_GPU // BOX) ** 3:
+                    if e["workgroups"] == per_gpu_cells // BOX ** 3:
                         return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
         except (OSError, ValueError, KeyError):
             continue
@@ -70,7 +85,50 @@ def rank_grid(n):
     return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}.get(n, (n, 1, 1))
 
 
-def setup_dist(n_gpus):
+def domain_for(mode, world):
+    if mode == "strong":
+        return np.array([512, 512, 512])
+    per = 256 if mode == "weak256" else 512
+    return np.array(rank_grid(world)) * per
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(n):
+    """N ranks of this script, one per GPU, started before any GPU call in
+    this process (nothing here initialises HIP); returns the worst exit code."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0:
+                    rc = rc or r
+                    for q in procs:   # one rank failed: the others would wait for it forever
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         import torch.distributed as dist
@@ -80,17 +138,17 @@ def setup_dist(n_gpus):
     return None, 0, 1, 0
 
 
-def build(omg, n_ranks, dev):
+def build(omg, domain, dev):
+    """C3's tree over `domain` on this rank's GPU, u / rhs = L_h u on every
+    level, phi = 0 (tests/test_uniform_grid.f90:137-170)."""
     T = omg.tree
     mg = omg.MG()
     mg.operator_type = T.MG_LAPLACIAN
     mg.smoother_type = T.MG_SMOOTHER_GSRB
     omg.mg_set_methods(mg)
     omg.mg_comm_init(mg)
-    domain = np.array(rank_grid(n_ranks)) * PER_GPU
     t0 = time.time()
-    omg.mg_build_rectangle(mg, domain, BOX, 1.0 / domain.astype(np.float64), [0.0] * 3,
-                           [True] * 3, 0)
+    omg.mg_build_rectangle(mg, domain, BOX, 1.0 / domain.astype(np.float64), [0.0] * 3, [True] * 3, 0)
     omg.mg_load_balance(mg)
     omg.mg_set_methods(mg)
     # coarse levels of at most 64 boxes of 16^3 live on every GPU: no
@@ -98,7 +156,6 @@ def build(omg, n_ranks, dev):
     mg.coarse_replication_cells = REPLICATE_CELLS
     t1 = time.time()
     omg.mg_allocate_storage(mg, device_index=dev)
-    # u on every level, rhs = L_h u, phi = 0 (tests/test_uniform_grid.f90:137-170);
     # every rank uploads every level (collective on replicated levels)
     for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
         ids = mg.lvls[lvl].my_ids
@@ -108,34 +165,242 @@ def build(omg, n_ranks, dev):
         n, nc = mg.ctx.level_size(lvl)
         mg.set_level(lvl, T.MG_IPHI, np.zeros((n, nc + 2, nc + 2, nc + 2)))
     mg.ctx.call("synchronize")
-    return mg, domain, t1 - t0, time.time() - t1
+    return mg, t1 - t0, time.time() - t1
+
+
+class Timer:
+    """Barrier + device synchronisation on both sides, max over ranks."""
+
+    def __init__(self, dist, ctx):
+        import torch
+        self.torch, self.dist, self.ctx = torch, dist, ctx
+
+    def barrier(self):
+        self.ctx.call("synchronize")
+        if self.torch.cuda.is_available():
+            self.torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+
+    def max_over_ranks(self, dt):
+        if not self.dist:
+            return dt
+        t = self.torch.tensor([dt], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def time(self, fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        self.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        self.barrier()
+        return self.max_over_ranks(time.perf_counter() - t0)
+
+
+def gather(dist, obj):
+    if not dist:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def profile_cycle(omg, mg, timer, cycle):
+    """One cycle with HIP events around every kernel family and comm round:
+    per-family totals (and on the finest level), the finest-level smoother's
+    launches, and this rank's exchange time."""
+    mg.ctx.call("reset_stats")
+    mg.ctx.call("set_profiling", 1)
+    timer.barrier()
+    tp = time.perf_counter()
+    cycle()
+    timer.barrier()
+    tp = time.perf_counter() - tp
+    mg.ctx.call("set_profiling", 0)
+    hi = mg.highest_lvl
+    total = 0.0
+    kern = {}
+    for name in KERNEL_FAMILIES:
+        n, ms, c = mg.ctx.kernel_stats(name)
+        if n:
+            total += ms
+            n1, ms1, _ = mg.ctx.kernel_stats(f"{name}@{hi}")
+            kern[name] = {"launches": n, "ms": round(ms, 4), f"launches_lvl{hi}": n1, f"ms_lvl{hi}": round(ms1, 4)}
+    comm = {}
+    for name in COMM_FAMILIES:
+        n, ms, doubles = mg.ctx.kernel_stats(name)
+        if n:
+            comm[name] = {"rounds": n, "ms": round(ms, 4), "MB_received": round(8e-6 * doubles, 3)}
+    # wall time of the profiled cycle (event pairs add a little) and what
+    # the families above do not account for (launch gaps, RCCL, host waits;
+    # side-stream work overlaps and can make it negative)
+    kern["profiled_cycle_ms"] = round(tp * 1e3, 4)
+    kern["unaccounted_ms"] = round(tp * 1e3 - total - comm.get("comm", {}).get("ms", 0.0), 4)
+    smoother = mg.ctx.kernel_stats(f"smoother_gsrb@{hi}")
+    return kern, comm, smoother
+
+
+def roofline(smoother, per_gpu_cells, boxes_hi, hi):
+    n, ms, upd = smoother
+    if not (n and ms > 0):
+        return None
+    alg_bytes = 24.0 * upd / n          # 24 B per cell update, per launch
+    dur = ms * 1e-3 / n
+    achieved = alg_bytes / dur / 1e9
+    traffic, tsrc = pmc_traffic(per_gpu_cells)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": f"k_gsrb_tile<16,OP_LPL> on level {hi} ({boxes_hi} boxes)",
+            "launches": n, "avg_launch_us": dur * 1e6,
+            "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_rule": "24 B per cell update x (level cells / 2) per substep",
+            "traffic_source": tsrc}
+
+
+def run_c3(omg, domain, dist, rank, world, dev, steps, warmup, profile=True):
+    mg, t_tree, t_alloc = build(omg, domain, dev)
+    timer = Timer(dist, mg.ctx)
+    dt = timer.time(lambda: omg.mg_fas_vcycle(mg), steps, warmup)
+    cells = float(np.prod(domain))
+    out = {"value": cells * steps / dt, "ms_per_step": dt * 1e3 / steps, "domain": [int(d) for d in domain],
+           "levels": [mg.lowest_lvl, mg.highest_lvl], "setup_s": {"tree": t_tree, "alloc_and_rhs": t_alloc},
+           "ref_unknowns_per_us": mg.n_boxes * BOX ** 3 * steps / dt * 1e-6}
+    n_comm, transport = mg.ctx.comm_info()
+    out["comm"] = {"transport": transport, "comm_ranks": n_comm}
+    if profile:
+        kern, comm, smoother = profile_cycle(omg, mg, timer, lambda: omg.mg_fas_vcycle(mg))
+        hi = mg.highest_lvl
+        out["kernels_one_cycle"] = kern
+        per_rank = gather(dist, {"rank": rank, "comm": comm, "boxes_lvl_hi": len(mg.lvls[hi].my_ids),
+                                 "profiled_cycle_ms": kern["profiled_cycle_ms"]})
+        out["comm"]["per_rank"] = per_rank
+        out["roofline"] = roofline(smoother, int(np.prod(domain)) // world, len(mg.lvls[hi].my_ids), hi)
+    omg.mg_deallocate_storage(mg)
+    return out
+
+
+def run_c4(omg, dist, world, steps=10, warmup=3):
+    """BASELINE's C4: the one-level-refined octree (test_refinement's tree,
+    128^3 base, box 16, n_levels 2), GSRB V-cycles, over the N ranks.
+    Cells = leaf cells of the tree (448 x 16^3 on level 1 + 512 x 16^3 on
+    level 2)."""
+    from tests import mgdriver as D   # problem set-up shared with the parity tests (device backend)
+    cfg = D.parse(C4_ARGS)
+    be = D.DeviceBackend(cfg)
+    D.setup_problem(be)
+    mg = be.mg
+    timer = Timer(dist, mg.ctx)
+    dt = timer.time(lambda: omg.mg_fas_vcycle(mg), steps, warmup)
+    cells = sum(len(mg.lvls[l].leaves) * mg.box_size_lvl[l] ** 3 for l in range(1, mg.highest_lvl + 1))
+    kern, comm, _ = profile_cycle(omg, mg, timer, lambda: omg.mg_fas_vcycle(mg))
+    hi = mg.highest_lvl
+    n, ms, upd = mg.ctx.kernel_stats(f"smoother_gsrb@{hi}")
+    fr = None
+    if world == 1 and n and ms > 0:
+        fr = {"avg_launch_us": ms * 1e3 / n, "achieved_GBs": 24.0 * upd / (ms * 1e-3) / 1e9,
+              "frac": 24.0 * upd / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    out = {"workload": "C4: test_refinement 2 16 128 128 128 (one refined level, box 16), GSRB, "
+                       "callback Dirichlet u",
+           "value": cells * steps / dt, "unit": "cell-updates/s (leaf cells)", "ms_per_step": dt * 1e3 / steps,
+           "leaf_cells": cells, "steps": steps, "warmup": warmup, "smoother_lvl2": fr,
+           "kernels_one_cycle": {k: v for k, v in kern.items() if k in ("profiled_cycle_ms", "smoother_gsrb")}}
+    omg.mg_deallocate_storage(mg)
+    return out
+
+
+def host_cores():
+    """Physical cores of the host (lscpu), and the CPUs this job may use."""
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")})
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    # the GPU box gives one GPU's job a share of 16 CPUs (OMP_NUM_THREADS)
+    share = min(share, int(os.environ.get("OMP_NUM_THREADS", share) or share))
+    return phys, os.cpu_count(), share
 
 
 def cpu_baseline(domain):
-    """The reference's own CPU path on this host, bounded to CPU_CYCLES V-cycles."""
+    """The reference's own CPU path (oracle/_ref/omg_golden, amdflang -O2 +
+    MPICH, mpiexec -n P, its mpi_wtime around the cycles) on this host:
+    P = 1 (one run of 1 V-cycle), P = 8 and P = the job's CPU share (min of 3
+    runs of 2 V-cycles each).  value = the 8-rank figure."""
     ref = os.path.join(ROOT, "oracle", "_ref", "omg_golden")
-    cores = min(8, os.cpu_count() or 1)
-    args = [str(BOX)] + [str(int(d)) for d in domain] + \
-        f"{CPU_CYCLES} v gsrb lpl 0 per sol 1 lb 0 x".split()
+    phys, logical, share = host_cores()
     if not os.path.exists(ref):
         return {"value": None, "unit": "cell-updates/s", "cores": 0, "kind": "reference",
                 "sample": "unavailable: oracle/_ref not built"}
     mpiexec = "/opt/conda/bin/mpiexec"
-    cmd = ([mpiexec, "-n", str(cores)] if cores > 1 and os.path.exists(mpiexec) else []) + [ref] + args
-    if not cmd[0].endswith("mpiexec"):
-        cores = 1
-    try:
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=240).stdout
-        t = float(re.search(r"TIME\s+(\S+)", out).group(1))
-    except Exception as e:  # noqa: BLE001
-        return {"value": None, "unit": "cell-updates/s", "cores": cores, "kind": "reference",
-                "sample": f"failed: {e}"}
     cells = float(np.prod(domain))
-    return {"value": cells / t, "unit": "cell-updates/s", "cores": cores, "kind": "reference",
-            "seconds_per_vcycle": t,
-            "sample": f"reference octree-mg (amdflang -O2, MPICH, {cores} ranks): {CPU_CYCLES} FAS V-cycles "
-                      f"({CPU_CYCLES * t:.1f} s), "
-                      f"{'x'.join(str(int(d)) for d in domain)} periodic GSRB box 16"}
+    runs = {}
+    plan = [(1, 1, 1), (8, 2, 3)] + ([(share, 2, 3)] if share not in (1, 8) else [])
+    for p, cycles, repeat in plan:
+        args = [str(BOX)] + [str(int(d)) for d in domain] + f"{cycles} v gsrb lpl 0 per sol 1 lb 0 x".split()
+        cmd = ([mpiexec, "-n", str(p)] if p > 1 else []) + [ref] + args
+        ts = []
+        for _ in range(repeat):
+            try:
+                out = subprocess.run(cmd, capture_output=True, text=True, timeout=180).stdout
+                ts.append(float(re.search(r"TIME\s+(\S+)", out).group(1)))
+            except Exception as e:  # noqa: BLE001
+                runs[str(p)] = {"error": f"{type(e).__name__}: {e}"[:200]}
+                break
+        if ts:
+            t = min(ts)
+            runs[str(p)] = {"seconds_per_vcycle": t, "value": cells / t, "runs": len(ts),
+                            "vcycles_per_run": cycles}
+    head = runs.get("8", {})
+    return {"value": head.get("value"), "unit": "cell-updates/s", "cores": 8, "kind": "reference",
+            "seconds_per_vcycle": head.get("seconds_per_vcycle"),
+            "host_physical_cores": phys, "host_logical_cpus": logical, "job_cpu_share": share,
+            "by_ranks": runs,
+            "sample": f"reference octree-mg (amdflang -O2, MPICH), mpiexec -n P, P in "
+                      f"{[p for p, _, _ in plan]}: {'x'.join(str(int(d)) for d in domain)} periodic GSRB "
+                      f"box 16, its own mpi_wtime per V-cycle; value = P = 8, min of 3 runs of 2 V-cycles"}
+
+
+def plan_check(omg, domain, dist, rank, world):
+    """--plan-only (CPU, no GPU): this rank's plan-only context
+    (OMG_DEVICE_NONE) of the bench's tree, and the check that every transfer
+    pairs up with its peer's, key for key in wire order (the contract
+    sort_and_transfer_buffers relies on, src/m_communication.f90:37-66)."""
+    T = omg.tree
+    tree = T.MGTree()
+    tree.n_cpu, tree.my_rank = world, rank
+    tree.build_rectangle(domain, BOX, 1.0 / domain.astype(np.float64), [0.0] * 3, [True] * 3, 0)
+    tree.load_balance()
+    ctx = omg.device.Context(-2, rank, world)
+    ctx.call("set_coarse_replication", REPLICATE_CELLS)
+    arrs = omg.mg._tree_arrays(tree)
+    ctx.call("tree_setup", tree.n_boxes, *arrs[:6], tree.lowest_lvl, tree.highest_lvl,
+             tree.first_normal_lvl, tree.box_size, arrs[6], arrs[7], arrs[8], arrs[9], 4)
+    mine = {(lvl, w, d): ctx.plan_transfer(lvl, w, d)
+            for lvl in range(tree.lowest_lvl, tree.highest_lvl + 1) for w in range(5) for d in (0, 1)}
+    ctx.close()
+    allp = gather(dist, mine)
+    problems = []
+    for (lvl, w, d), (items, _) in mine.items():
+        if d:
+            continue
+        for b in range(world):
+            sent = [k for p, k in items if p == b]
+            expected = [k for p, k in allp[b][(lvl, w, 1)][0] if p == rank]
+            if b == rank and sent:
+                problems.append(f"lvl {lvl} transfer {w}: sends to itself")
+            elif sent != expected:
+                problems.append(f"lvl {lvl} transfer {w}: {rank}->{b} sends {len(sent)}, {b} expects {len(expected)}")
+    hi = tree.highest_lvl
+    return {"rank": rank, "problems": problems, "boxes_lvl_hi": len(tree.lvls[hi].my_ids),
+            "halo_faces_recv_lvl_hi": len(mine[(hi, 0, 1)][0]),
+            "peers_lvl_hi": sorted({p for p, _ in mine[(hi, 0, 1)][0]})}
 
 
 def main():
@@ -143,109 +408,79 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--mode", choices=("weak", "strong", "weak256"), default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c3_strong / c4_refined sub-benchmarks")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="CPU only: launch the ranks, build each rank's communication plan, check they pair up")
     a = ap.parse_args()
 
-    dist, rank, world, local_rank = setup_dist(a.gpus)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(a.gpus))
+
+    dist, rank, world, local_rank = setup_dist()
     omg = __graft_entry__.load_package()
+    if a.plan_only:
+        per_rank = gather(dist, plan_check(omg, domain_for(a.mode, world), dist, rank, world))
+        if rank == 0:
+            print(json.dumps({"plan_only": True, "n_ranks": world, "mode": a.mode,
+                              "domain": [int(d) for d in domain_for(a.mode, world)],
+                              "ok": not any(r["problems"] for r in per_rank), "ranks": per_rank}), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     import torch
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
-    mg, domain, t_tree, t_alloc = build(omg, world, local_rank)
 
-    def barrier():
-        mg.ctx.call("synchronize")
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-
-    for _ in range(a.warmup):
-        omg.mg_fas_vcycle(mg)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        omg.mg_fas_vcycle(mg)
-    barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
-
-    cells = float(np.prod(domain))
-    value = cells * a.steps / dt
-
-    roof = None
-    kern = {}
-    if not a.no_profile_pass:
-        mg.ctx.call("reset_stats")
-        mg.ctx.call("set_profiling", 1)
-        barrier()
-        tp = time.perf_counter()
-        omg.mg_fas_vcycle(mg)
-        barrier()
-        tp = time.perf_counter() - tp
-        mg.ctx.call("set_profiling", 0)
-        hi = mg.highest_lvl
-        total = 0.0
-        for name in KERNEL_FAMILIES:
-            n, ms, c = mg.ctx.kernel_stats(name)
-            if n:
-                total += ms
-                n1, ms1, _ = mg.ctx.kernel_stats(f"{name}@{hi}")
-                kern[name] = {"launches": n, "ms": round(ms, 4), f"launches_lvl{hi}": n1,
-                              f"ms_lvl{hi}": round(ms1, 4)}
-        # wall time of the profiled cycle (event pairs add a little) and what
-        # the families above do not account for (launch gaps, RCCL, host
-        # waits; side-stream work overlaps and can make it negative)
-        kern["profiled_cycle_ms"] = round(tp * 1e3, 4)
-        kern["unaccounted_ms"] = round(tp * 1e3 - total, 4)
-        # dominant kernel: the red-black substep on the finest level
-        n, ms, upd = mg.ctx.kernel_stats(f"smoother_gsrb@{hi}")
-        if n and ms > 0:
-            alg_bytes = 24.0 * upd / n          # 24 B per cell update, per launch
-            dur = ms * 1e-3 / n
-            achieved = alg_bytes / dur / 1e9
-            traffic, tsrc = pmc_traffic()
-            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel": f"k_gsrb_tile<16,OP_LPL> on level {hi} ({len(mg.lvls[hi].my_ids)} boxes)",
-                    "launches": n, "avg_launch_us": dur * 1e6,
-                    "alg_bytes_per_launch": alg_bytes,
-                    "alg_bytes_rule": "24 B per cell update x (level cells / 2) per substep",
-                    "traffic_source": tsrc}
+    domain = domain_for(a.mode, world)
+    main_run = run_c3(omg, domain, dist, rank, world, local_rank, a.steps, a.warmup,
+                      profile=not a.no_profile_pass)
+    extra = {}
+    if not a.no_extra:
+        if world > 1 and a.mode != "strong":
+            s = run_c3(omg, domain_for("strong", world), dist, rank, world, local_rank, a.steps, a.warmup,
+                       profile=not a.no_profile_pass)
+            extra["c3_strong"] = {"workload": "C3: 512^3 in total over the N GPUs (strong scaling)",
+                                  "value": s["value"], "ms_per_step": s["ms_per_step"], "domain": s["domain"],
+                                  "steps": a.steps, "warmup": a.warmup, "roofline": s.get("roofline"),
+                                  "comm": s["comm"]}
+        extra["c4_refined"] = run_c4(omg, dist, world)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(domain)
 
     if rank == 0:
+        desc = {"weak": "512^3 per GPU", "strong": "512^3 over the N GPUs", "weak256": "256^3 per GPU"}[a.mode]
         line = {
-            "metric": "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512^3",
-            "value": value,
+            "metric": METRIC,
+            "value": main_run["value"],
             "unit": "cell-updates/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": dt * 1e3 / a.steps,
+            "ms_per_step": main_run["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.mode == "strong" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: u=prod(sin(10 pi x)), rhs=L_h u on every level, phi0=0",
-            "config": {"workload": "C3: 3D Poisson, 512^3 per GPU, box 16, periodic, GSRB "
+            "config": {"workload": f"C3: 3D Poisson, {desc}, box 16, periodic, GSRB "
                                    "FAS V-cycle (n_cycle_down=up=2)",
-                       "domain": [int(d) for d in domain], "box_size": BOX,
-                       "levels": [mg.lowest_lvl, mg.highest_lvl],
+                       "mode": a.mode, "domain": main_run["domain"], "box_size": BOX,
+                       "levels": main_run["levels"],
                        "parallelism": f"domain-decomposition x{world} (RCCL halos)"},
-            "roofline": roof,
+            "roofline": main_run.get("roofline"),
             "cpu_baseline": cpu,
-            "ref_unknowns_per_us": mg.n_boxes * BOX ** 3 * a.steps / dt * 1e-6,
-            "kernels_one_cycle": kern,
-            "setup_s": {"tree": t_tree, "alloc_and_rhs": t_alloc},
+            "comm": main_run["comm"],
+            "ref_unknowns_per_us": main_run["ref_unknowns_per_us"],
+            "kernels_one_cycle": main_run.get("kernels_one_cycle"),
+            "setup_s": main_run["setup_s"],
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -202,11 +202,31 @@ int omg_free_planes(omg_ctx *ctx, int *fft_lvl, int *nx, double *planes, long lo
 int omg_plan_transfer(omg_ctx *ctx, int lvl, int which, int dir, int cap, int *peers,
                       long long *keys, int *n_items, int *item_doubles);
 
+/* The context's communicator (no reference counterpart; mg%n_cpu of
+ * mg_comm_init, src/m_communication.f90:14-35, as the transport sees it):
+ * *n_ranks = the ranks it joins (ncclCommCount for RCCL), *transport = one of
+ * OMG_TRANSPORT_*. */
+enum { OMG_TRANSPORT_NONE = 0, OMG_TRANSPORT_RCCL = 1, OMG_TRANSPORT_LOOPBACK = 2 };
+int omg_comm_info(omg_ctx *ctx, int *n_ranks, int *transport);
+
 /* Stream / timing helpers for benchmarks. */
 int omg_synchronize(omg_ctx *ctx);
 void *omg_stream(omg_ctx *ctx);                 /* the hipStream_t all work runs on */
 /* Per-kernel HIP-event timing (off by default): when on, every launch of the
- * named kernel families is bracketed by events on the context stream. */
+ * named kernel families is bracketed by events on the stream it runs on, and
+ * kept per family and per family@level.  "comm" / "comm_overlap" are the
+ * RCCL (or loopback) rounds on the context stream / on the halo-overlap
+ * stream, with cells = doubles received.
+ * Environment switches read at omg_ctx_create ("0" = off):
+ *   OMG_ROCTX=1  roctx ranges per level step (rocprofv3 --marker-trace);
+ *   OMG_DEBUG=1  ghost faces start as signalling NaN and unstored edge /
+ *                corner cells download as signalling NaN (the reference's
+ *                DEBUG=1 -finit-real=snan, makerules.make:13-17);
+ *   OMG_GRAPH=1  capture each cycle as a HIP graph.
+ * Failure detection: a requested max residual (omg_fas_vcycle / omg_fas_fmg /
+ * omg_max_residual_lvl / omg_poisson_free_3d, and diffusion_solve's loop)
+ * that is NaN or Inf is an error, "non-finite residual", with max_res still
+ * written; the reference's max() drops NaN (m_multigrid.f90:226-234). */
 int omg_set_profiling(omg_ctx *ctx, int on);
 int omg_kernel_stats(omg_ctx *ctx, const char *name, long long *launches,
                      double *total_ms, double *cells);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <hipfft/hipfft.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -16,6 +17,7 @@
 #include <mutex>
 #include <tuple>
 #include <climits>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -92,6 +94,20 @@ void dfree(T*& p) {
 }
 
 const int kNeighbRev[6] = {2, 1, 4, 3, 6, 5};
+
+// an on/off switch from the environment: set and not "0" (or empty)
+bool env_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && *v && std::strcmp(v, "0") != 0;
+}
+
+// a signalling NaN (quiet bit clear): OMG_DEBUG's poison
+double snan_value() {
+  const unsigned long long bits = 0x7FF4000000000000ULL;
+  double d;
+  std::memcpy(&d, &bits, 8);
+  return d;
+}
 
 inline int pack_dix(const int d[3]) { return d[0] | (d[1] << 10) | (d[2] << 20); }
 
@@ -317,12 +333,70 @@ std::vector<double> loop_allgather(omg_ctx* c, double v) {
   return all;
 }
 
+// ---------------------------------------------------------------------------
+// profiling: HIP events around kernel families on the context stream
+constexpr int NO_LVL = INT_MIN;
+
+// (on `st`, the context stream by default; with OMG_ROCTX set, a roctx range
+// "name@lvl" around the host side of the step for rocprofv3 --marker-trace)
+struct Prof {
+  omg_ctx* c;
+  const char* name;
+  double cells;
+  int lvl;
+  hipStream_t st;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  bool range = false;
+  Prof(omg_ctx* c_, const char* n, double cl, int l = NO_LVL, hipStream_t s = nullptr)
+      : c(c_), name(n), cells(cl), lvl(l), st(s ? s : c_->stream) {
+    if (c->roctx) {
+      char buf[64];
+      if (lvl == NO_LVL) std::snprintf(buf, sizeof(buf), "%s", name);
+      else std::snprintf(buf, sizeof(buf), "%s@%d", name, lvl);
+      roctxRangePushA(buf);
+      range = true;
+    }
+    if (!c->profiling) return;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+  }
+  ~Prof() {
+    if (range) roctxRangePop();
+    if (!e0) return;
+    (void)hipEventRecord(e1, st);
+    c->pending.push_back({name, e0, e1, cells, lvl});
+  }
+};
+
+void resolve_stats(omg_ctx* c) {
+  if (c->pending.empty()) return;
+  for (auto& p : c->pending) {
+    float ms = 0;
+    HIPCHK(hipEventSynchronize(p.e1));
+    HIPCHK(hipEventElapsedTime(&ms, p.e0, p.e1));
+    for (int pass = 0; pass < (p.lvl == NO_LVL ? 1 : 2); pass++) {
+      auto& s = c->stats[pass ? std::string(p.name) + "@" + std::to_string(p.lvl) : std::string(p.name)];
+      s.launches++;
+      s.ms += ms;
+      s.cells += p.cells;
+    }
+    (void)hipEventDestroy(p.e0);
+    (void)hipEventDestroy(p.e1);
+  }
+  c->pending.clear();
+}
+
 // One grouped RCCL round: send segment i to peer i, receive likewise
 // (replaces sort_and_transfer_buffers, m_communication.f90:37-66).
-void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf, hipStream_t st = nullptr) {
+void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf, hipStream_t st = nullptr,
+              int lvl = NO_LVL) {
   if (c->n_ranks == 1) return;
   if (T.send.empty() && T.recv.empty()) return;
   if (!st) st = c->stream;
+  // "comm": one grouped round, timed on the stream it runs on; cells = the
+  // doubles this rank receives
+  Prof prof(c, st == c->stream ? "comm" : "comm_overlap", (double)T.n_recv * T.item_doubles, lvl, st);
   if (c->loop) {
     loop_exchange(c, T, sendbuf, recvbuf, st);
     return;
@@ -339,47 +413,6 @@ void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recv
     NCCLCHK(ncclRecv(recvbuf + (size_t)p.offset * per, n, ncclDouble, p.peer, comm, st));
   }
   NCCLCHK(ncclGroupEnd());
-}
-
-// ---------------------------------------------------------------------------
-// profiling: HIP events around kernel families on the context stream
-constexpr int NO_LVL = INT_MIN;
-
-struct Prof {
-  omg_ctx* c;
-  const char* name;
-  double cells;
-  int lvl;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  Prof(omg_ctx* c_, const char* n, double cl, int l = NO_LVL) : c(c_), name(n), cells(cl), lvl(l) {
-    if (!c->profiling) return;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, c->stream));
-  }
-  ~Prof() {
-    if (!e0) return;
-    (void)hipEventRecord(e1, c->stream);
-    c->pending.push_back({name, e0, e1, cells, lvl});
-  }
-};
-
-void resolve_stats(omg_ctx* c) {
-  if (c->pending.empty()) return;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (auto& p : c->pending) {
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, p.e0, p.e1));
-    for (int pass = 0; pass < (p.lvl == NO_LVL ? 1 : 2); pass++) {
-      auto& s = c->stats[pass ? std::string(p.name) + "@" + std::to_string(p.lvl) : std::string(p.name)];
-      s.launches++;
-      s.ms += ms;
-      s.cells += p.cells;
-    }
-    (void)hipEventDestroy(p.e0);
-    (void)hipEventDestroy(p.e1);
-  }
-  c->pending.clear();
 }
 
 // ---------------------------------------------------------------------------
@@ -413,7 +446,7 @@ void finish_rb(omg_ctx* c, Level* L, int iv);
 void finish_halo(omg_ctx* c, Level* L, int iv) {
   if (c->n_ranks == 1) return;
   if (L->halo.n_send || L->halo.n_recv) {
-    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf);
+    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
     launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
   }
   finish_rb(c, L, iv);
@@ -427,7 +460,7 @@ void finish_rb(omg_ctx* c, Level* L, int iv) {
   if (L->rbx.n_send || L->rbx.n_recv) {
     launch_rb_pack(view_of(c, L->lvl - 1), iv, L->rbx.d_send_items, L->rbx.n_send, L->nc, L->d_rbsend,
                    c->stream);
-    exchange(c, L->rbx, L->d_rbsend, L->d_rbrecv);
+    exchange(c, L->rbx, L->d_rbsend, L->d_rbrecv, nullptr, L->lvl);
     launch_rb_unpack(L->view(), iv, L->rbx.d_recv_items, L->rbx.n_recv, L->d_rbrecv, c->stream);
   }
 }
@@ -501,7 +534,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
-      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm);
+      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm, lvl);
       launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream_comm);
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       {
@@ -568,7 +601,7 @@ void restrict_remote(omg_ctx* c, int iv, int lvl) {
   Level* C = level_ptr(c, lvl - 1);
   if (c->n_ranks > 1 && F && C && (F->restr.n_send || F->restr.n_recv)) {
     launch_restrict_pack(F->view(), iv, F->restr.d_send_items, F->restr.n_send, F->d_sendbuf, c->stream);
-    exchange(c, F->restr, F->d_sendbuf, C->d_recvbuf);
+    exchange(c, F->restr, F->d_sendbuf, C->d_recvbuf, nullptr, lvl);
     launch_restrict_unpack(C->view(), iv, F->restr.d_recv_items, F->restr.n_recv, F->nc / 2, C->d_recvbuf,
                            c->stream);
   }
@@ -597,7 +630,7 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
   const LevelView FV = view_of(c, lvl + 1), CV = view_of(c, lvl);
   if (c->n_ranks > 1 && F && C && (F->prol.n_send || F->prol.n_recv)) {
     launch_prolong_pack(CV, FV, iv, F->prol.d_send_items, F->prol.n_send, C->d_sendbuf, c->stream);
-    exchange(c, F->prol, C->d_sendbuf, F->d_recvbuf);
+    exchange(c, F->prol, C->d_sendbuf, F->d_recvbuf, nullptr, lvl + 1);
     launch_prolong_unpack(FV, iv_to, add, F->prol.d_recv_items, F->prol.n_recv, F->d_recvbuf,
                           c->stream);
   }
@@ -651,7 +684,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
-      exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm);
+      exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm, lvl);
       launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm, 1);
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       {
@@ -1098,6 +1131,17 @@ void run_tail(omg_ctx* c, int top) {
   for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
 }
 
+// Failure detection: the device max residual is an exact max of
+// |res| over IEEE bits, so one NaN or Inf cell makes it non-finite.  The
+// reference's Fortran max() drops NaN operands (m_multigrid.f90:226-234,
+// 296-311) and reports a finite or zero residual for a diverged field; here
+// it is an error instead, the caller's output argument holding the bits.
+void check_finite_res(double r, const char* where) {
+  if (!std::isfinite(r))
+    throw OmgError(std::string(where) + ": non-finite residual (" + (std::isnan(r) ? "NaN" : "Inf") +
+                   "): phi or rhs holds NaN/Inf");
+}
+
 // mg_fas_vcycle (m_multigrid.f90:150-243)
 double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalone) {
   const bool has_highest = highest_lvl >= c->lowest;
@@ -1228,6 +1272,25 @@ bool graph_ok(omg_ctx* c) {
          !c->tail_timing && !c->no_tail && c->n_boxes > 0 && tail_top(c, c->highest) >= c->lowest;
 }
 
+// The host state the captured body changed assumes the graph ran.  When the
+// capture, instantiation or launch fails, that is rolled back to "unknown":
+// the tail arguments are re-uploaded by the next call (h_tail no longer
+// matches anything), the graph of this key is dropped, and every level's phi
+// ghost faces count as stale (the next cycle fills them).  (The graph path
+// runs without subtract_mean, so no mean / shift state is involved.)
+void graph_rollback(omg_ctx* c, int key) {
+  c->capturing = false;
+  c->max_deferred = false;
+  std::memset(c->h_tail, 0xff, sizeof(TailArgs));
+  auto it = c->graphs.find(key);
+  if (it != c->graphs.end()) {
+    if (it->second) (void)hipGraphExecDestroy(it->second);
+    c->graphs.erase(it);
+  }
+  phi_dirty_all(c);
+  (void)hipGetLastError();
+}
+
 template <typename F>
 double run_cycle(omg_ctx* c, int key, F&& body) {
   if (!graph_ok(c)) return body();
@@ -1236,31 +1299,44 @@ double run_cycle(omg_ctx* c, int key, F&& body) {
   HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   hipGraph_t g = nullptr;
   try {
+    if (c->graph_fail_at == 1) {   // one-shot test injection
+      c->graph_fail_at = 0;
+      throw OmgError("injected failure during capture (OMG_GRAPH_FAIL=1)");
+    }
     body();
   } catch (...) {
-    c->capturing = false;
     (void)hipStreamEndCapture(c->stream, &g);
     if (g) (void)hipGraphDestroy(g);
-    (void)hipGetLastError();
+    graph_rollback(c, key);
     throw;
   }
   c->capturing = false;
-  HIPCHK(hipStreamEndCapture(c->stream, &g));
-  size_t n_nodes = 0;
-  HIPCHK(hipGraphGetNodes(g, nullptr, &n_nodes));
-  if (n_nodes) {
-    hipGraphExec_t& ex = c->graphs[key];
-    if (ex) {
-      hipGraphNode_t err_node = nullptr;
-      hipGraphExecUpdateResult res;
-      if (hipGraphExecUpdate(ex, g, &err_node, &res) != hipSuccess || res != hipGraphExecUpdateSuccess) {
-        (void)hipGetLastError();
-        HIPCHK(hipGraphExecDestroy(ex));
-        ex = nullptr;
-      }
+  try {
+    HIPCHK(hipStreamEndCapture(c->stream, &g));
+    size_t n_nodes = 0;
+    HIPCHK(hipGraphGetNodes(g, nullptr, &n_nodes));
+    if (c->graph_fail_at == 2) {   // one-shot: the body ran (host state changed), the graph does not
+      c->graph_fail_at = 0;
+      throw OmgError("injected failure before the launch (OMG_GRAPH_FAIL=2)");
     }
-    if (!ex) HIPCHK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    HIPCHK(hipGraphLaunch(ex, c->stream));
+    if (n_nodes) {
+      hipGraphExec_t& ex = c->graphs[key];
+      if (ex) {
+        hipGraphNode_t err_node = nullptr;
+        hipGraphExecUpdateResult res;
+        if (hipGraphExecUpdate(ex, g, &err_node, &res) != hipSuccess || res != hipGraphExecUpdateSuccess) {
+          (void)hipGetLastError();
+          HIPCHK(hipGraphExecDestroy(ex));
+          ex = nullptr;
+        }
+      }
+      if (!ex) HIPCHK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      HIPCHK(hipGraphLaunch(ex, c->stream));
+    }
+  } catch (...) {
+    if (g) (void)hipGraphDestroy(g);
+    graph_rollback(c, key);
+    throw;
   }
   HIPCHK(hipGraphDestroy(g));
   if (!c->max_deferred) return 0.0;
@@ -1331,6 +1407,7 @@ void diffusion_solve(omg_ctx* c, int op, double dt, double coeff, int order, dou
   double res = run_cycle(c, 2 + 2 + 4, [&] { return fas_fmg(c, true, true); });
   int n = 1;
   for (; n <= kDiffusionMaxIts; n++) {
+    check_finite_res(res, "diffusion_solve");
     if (res <= max_res) break;
     res = run_cycle(c, 1 + 2 + 4 + 8 * (c->lowest - 1 + 64),
                     [&] { return fas_vcycle(c, c->lowest - 1, true, true); });
@@ -1626,6 +1703,13 @@ double poisson_free_3d(omg_ctx* c, bool new_rhs, double max_fft_frac, bool fmgcy
   for (int id : c->ids[fft_lvl])
     for (int d = 0; d < 3; d++) nx[d] = std::max(nx[d], c->ix[(size_t)(id - 1) * 3 + d] * nc_f);
   for (int d = 0; d < 3; d++) nx[d] += 2;
+  // the reference creates PSolver's kernel for (nx(1), nx(3), nx(3))
+  // (m_free_space.f90:118-120) and solves on (nx(1), nx(2), nx(3)): the two
+  // agree only when ny == nz, the only case it can solve (and that its
+  // fixtures cover); anything else is refused rather than guessed
+  if (nx[1] != nx[2])
+    throw OmgError("mg_poisson_free_3d: the FFT level needs ny == nz (the reference's kernel is built for "
+                   "(nx, nz, nz), m_free_space.f90:118-120)");
   const double h[3] = {c->drl[fft_lvl][0], c->drl[fft_lvl][1], c->drl[fft_lvl][2]};
   if (S->initialized && new_grid) free_grid_release(S);
   for (int d = 0; d < 3; d++) S->r_min[d] = r_min ? r_min[d] : 0.0;
@@ -1764,6 +1848,11 @@ void build_plan(omg_ctx* c) {
     if (L.n) {
       const size_t bytes = sizeof(double) * (size_t)c->n_vars * L.n * L.stride;
       dmalloc(&L.d_data, bytes, true);
+      L.d_phi = L.d_data;
+      if (c->debug && !g_host_only) {   // (L.view() needs only the arena fields here)
+        launch_poison_ghosts(L.view(), c->n_vars, snan_value(), nullptr);
+        HIPCHK(hipDeviceSynchronize());
+      }
     }
     // neighbour table + halo receive plan
     L.h_nbk.assign((size_t)L.n * 6, NB_LOCAL);
@@ -2051,13 +2140,16 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->device = device;
     c->rank = rank;
     c->n_ranks = n_ranks;
-    c->no_tail = getenv("OMG_NO_TAIL") != nullptr;
-    c->no_fuse_up = getenv("OMG_NO_FUSE_UP") != nullptr;
-    c->no_skip1 = getenv("OMG_NO_SKIP1") != nullptr;
-    c->tail_timing = getenv("OMG_TAIL_TIMING") != nullptr;
-    c->no_fill_tile = getenv("OMG_NO_FILL_TILE") != nullptr;
-    c->no_graph = getenv("OMG_GRAPH") == nullptr;
-    c->no_fuse_down = getenv("OMG_NO_FUSE_DOWN") != nullptr;
+    c->no_tail = env_flag("OMG_NO_TAIL");
+    c->no_fuse_up = env_flag("OMG_NO_FUSE_UP");
+    c->no_skip1 = env_flag("OMG_NO_SKIP1");
+    c->tail_timing = env_flag("OMG_TAIL_TIMING");
+    c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
+    c->no_graph = !env_flag("OMG_GRAPH");
+    c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
+    c->roctx = env_flag("OMG_ROCTX");
+    c->debug = env_flag("OMG_DEBUG");
+    if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
@@ -2355,7 +2447,7 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
       launch_from_ref(L->view(), iv, st, c->stream);
       if (L->repl.n_send || L->repl.n_recv) {
         launch_box_pack(L->view(), iv, L->repl.d_send_items, L->repl.n_send, L->d_sendbuf, c->stream);
-        exchange(c, L->repl, L->d_sendbuf, L->d_recvbuf);
+        exchange(c, L->repl, L->d_sendbuf, L->d_recvbuf, nullptr, lvl);
         launch_box_unpack(L->view(), iv, L->repl.d_recv_items, L->repl.n_recv, L->d_recvbuf, c->stream);
       }
       HIPCHK(hipStreamSynchronize(c->stream));
@@ -2376,7 +2468,7 @@ int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
     if (!L->n) return;
     const size_t s = L->nc + 2, box = s * s * s, n = box * L->n;
     double* st = stage(c, n);
-    launch_to_ref(L->view(), iv, st, c->stream);
+    launch_to_ref(L->view(), iv, st, c->debug ? snan_value() : 0.0, c->stream);
     if (L->replicated) {   // the host's boxes only
       std::vector<double> full(n);
       HIPCHK(hipMemcpyAsync(full.data(), st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
@@ -2395,6 +2487,7 @@ int omg_fas_vcycle(omg_ctx* c, int highest_lvl, int want_max_res, double* max_re
     const double r = run_cycle(c, 1 + (want_max_res ? 2 : 0) + 4 * (standalone != 0) + 8 * (highest_lvl + 64),
                                [&] { return fas_vcycle(c, highest_lvl, want_max_res != 0, standalone != 0); });
     if (want_max_res && max_res) *max_res = r;
+    if (want_max_res) check_finite_res(r, "mg_fas_vcycle");
   });
 }
 
@@ -2403,6 +2496,7 @@ int omg_fas_fmg(omg_ctx* c, int have_guess, int want_max_res, double* max_res) {
     const double r = run_cycle(c, 2 + (want_max_res ? 2 : 0) + 4 * (have_guess != 0),
                                [&] { return fas_fmg(c, have_guess != 0, want_max_res != 0); });
     if (want_max_res && max_res) *max_res = r;
+    if (want_max_res) check_finite_res(r, "mg_fas_fmg");
   });
 }
 
@@ -2477,6 +2571,7 @@ int omg_max_residual_lvl(omg_ctx* c, int lvl, double* out) {
   return guarded([&] {
     enter(c);
     *out = max_residual_lvl(c, lvl);
+    check_finite_res(*out, "max_residual_lvl");
   });
 }
 int omg_get_sum(omg_ctx* c, int iv, double* out) {
@@ -2505,6 +2600,7 @@ int omg_poisson_free_3d(omg_ctx* c, int new_rhs, double max_fft_frac, int fmgcyc
     const double r = poisson_free_3d(c, new_rhs != 0, max_fft_frac, fmgcycle != 0, want_max_res != 0, r_min,
                                      box_r_min);
     if (max_res && want_max_res) *max_res = r;
+    if (want_max_res) check_finite_res(r, "mg_poisson_free_3d");
   });
 }
 
@@ -2518,6 +2614,21 @@ int omg_free_planes(omg_ctx* c, int* fft_lvl, int* nx, double* planes, long long
     if (planes && cap >= (long long)n) {
       HIPCHK(hipMemcpyAsync(planes, S->d_planes, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
+    }
+  });
+}
+
+int omg_comm_info(omg_ctx* c, int* n_ranks, int* transport) {
+  return guarded([&] {
+    if (c->nccl) {
+      NCCLCHK(ncclCommCount((ncclComm_t)c->nccl, n_ranks));
+      *transport = OMG_TRANSPORT_RCCL;
+    } else if (c->loop) {
+      *n_ranks = c->loop->n_ranks;
+      *transport = OMG_TRANSPORT_LOOPBACK;
+    } else {
+      *n_ranks = c->n_ranks;
+      *transport = OMG_TRANSPORT_NONE;
     }
   });
 }

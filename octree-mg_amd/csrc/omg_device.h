@@ -108,6 +108,13 @@ struct Tl {
   }
 };
 
+// max of two |res| values (non-negative, or NaN) on their IEEE bit patterns:
+// the same result as fmax for numbers, but NaN and Inf propagate (fmax drops
+// a NaN operand), so a diverged field reaches the max residual
+__device__ __forceinline__ double amax(double a, double b) {
+  return (unsigned long long)__double_as_longlong(a) >= (unsigned long long)__double_as_longlong(b) ? a : b;
+}
+
 __device__ __forceinline__ void atomic_max_nonneg(unsigned long long* p, double v) {
   // |res| >= 0: IEEE bit patterns of non-negative doubles order like uint64
   atomicMax(p, (unsigned long long)__double_as_longlong(v));
@@ -121,7 +128,7 @@ __device__ __forceinline__ void atomic_max_nonneg(unsigned long long* p, double 
 // (the coarse tail) keeps one atomic per wave on maxbits[0].
 template <int BS>
 __device__ __forceinline__ void launch_max(unsigned long long* maxbits, double mx) {
-  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+  for (int off = 32; off > 0; off >>= 1) mx = amax(mx, __shfl_down(mx, off, 64));
   if (gridDim.x == 1) {
     if ((threadIdx.x & 63) == 0) atomic_max_nonneg(maxbits, mx);
     return;
@@ -130,7 +137,7 @@ __device__ __forceinline__ void launch_max(unsigned long long* maxbits, double m
   if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < BS / 64; w++) mx = fmax(mx, wmax[w]);
+    for (int w = 1; w < BS / 64; w++) mx = amax(mx, wmax[w]);
     atomic_max_nonneg(maxbits + (blockIdx.x % kMaxSlots) * kMaxSlotStride, mx);
   }
 }

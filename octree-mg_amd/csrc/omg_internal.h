@@ -268,8 +268,13 @@ struct omg_ctx {
   bool capturing = false;              // inside a capture: no host synchronisation
   bool max_deferred = false;           // the max residual is read after the graph ran
   std::map<int, hipGraphExec_t> graphs;   // by entry (run_cycle's key)
+  int graph_fail_at = 0;               // OMG_GRAPH_FAIL (tests): inject a failure in run_cycle
   // profiling
   bool profiling = false;
+  bool roctx = false;                  // OMG_ROCTX: roctx ranges per level step (rocprofv3 --marker-trace)
+  // OMG_DEBUG: ghost faces start as signalling NaN, unstored edge / corner
+  // cells download as signalling NaN (the reference's DEBUG=1 -finit-real=snan)
+  bool debug = false;
   std::map<std::string, omg::KStat> stats;
   std::vector<omg::PendingEv> pending;
 };

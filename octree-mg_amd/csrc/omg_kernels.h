@@ -74,7 +74,8 @@ void launch_subtract(const LevelView& L, int iv, const double* mean, int ghosts,
 void launch_set_rhs(const LevelView& L, const int* leaves, int n_leaves, double f1, double f2, hipStream_t st);
 void launch_copy_var(const LevelView& L, int src, int dst, hipStream_t st);
 void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t st);
-void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st);
+void launch_to_ref(const LevelView& L, int iv, double* ref, double unstored, hipStream_t st);
+void launch_poison_ghosts(const LevelView& L, int n_vars, double poison, hipStream_t st);
 void launch_phi_bc_store(const LevelView& L, const GcBC& bc, int* nba, hipStream_t st);
 
 // The coarse end of the V-cycle in ONE single-workgroup launch (omg_tiles.hip):

@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(256) k_residual(LevelView L, double lambda, un
     if (!cell_of(L, o, i, j, k)) continue;
     const double res = boxp(L, 2, b)[o] - apply_op<OP>(L, K, b, i, j, k);
     boxp(L, 4, b)[o] = res;
-    mx = fmax(mx, fabs(res));
+    mx = amax(mx, fabs(res));
   }
   if (maxbits) launch_max<256>(maxbits, mx);
 }
@@ -387,13 +387,13 @@ __global__ void __launch_bounds__(kMaxSlots) k_max_fold(unsigned long long* slot
   unsigned long long* s = slots + threadIdx.x * kMaxSlotStride;
   double mx = __longlong_as_double((long long)*s);
   *s = 0ull;
-  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+  for (int off = 32; off > 0; off >>= 1) mx = amax(mx, __shfl_down(mx, off, 64));
   __shared__ double wmax[kMaxSlots / 64];
   if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < kMaxSlots / 64; w++) mx = fmax(mx, wmax[w]);
-    if (accumulate) mx = fmax(mx, __longlong_as_double((long long)*out));
+    for (int w = 1; w < kMaxSlots / 64; w++) mx = amax(mx, wmax[w]);
+    if (accumulate) mx = amax(mx, __longlong_as_double((long long)*out));
     *out = (unsigned long long)__double_as_longlong(mx);
   }
 }
@@ -617,15 +617,37 @@ __global__ void __launch_bounds__(256) k_from_ref(LevelView L, int iv, const dou
   }
 }
 
-__global__ void __launch_bounds__(256) k_to_ref(LevelView L, int iv, double* ref) {
+// (unstored: what the edge and corner cells read back as, 0 or, in debug
+// mode, a signalling NaN)
+__global__ void __launch_bounds__(256) k_to_ref(LevelView L, int iv, double* ref, double unstored) {
   const int s = L.nc + 2;
   const long long per = (long long)s * s * s;
   GRID_STRIDE(t, per * L.n) {
     const int b = (int)(t / per);
     const int r = (int)(t % per), i = r % s, j = (r / s) % s, k = r / (s * s);
     const int nbnd = (i == 0 || i == s - 1) + (j == 0 || j == s - 1) + (k == 0 || k == s - 1);
-    ref[t] = nbnd >= 2 ? 0.0 : boxp(L, iv, b)[off_cell(L, i, j, k)];
+    ref[t] = nbnd >= 2 ? unstored : boxp(L, iv, b)[off_cell(L, i, j, k)];
   }
+}
+
+// Debug mode (OMG_DEBUG): every ghost face slot of every variable set to
+// `poison` (a signalling NaN), the reference's DEBUG=1 -finit-real=snan for
+// the cells that only a ghost fill, an upload or a store may define
+// (makerules.make:13-17); the interior keeps the reference's zeros
+// (m_allocate_storage.f90:75-76).
+__global__ void __launch_bounds__(256) k_poison_ghosts(LevelView L, int n_vars, double poison) {
+  const long long per = 6LL * L.fs;
+  GRID_STRIDE(t, per * L.n * n_vars) {
+    const long long q = t / per;
+    const int b = (int)(q % L.n), iv = (int)(q / L.n) + 1;
+    boxp(L, iv, b)[2LL * L.hv + t % per] = poison;
+  }
+}
+
+void launch_poison_ghosts(const LevelView& L, int n_vars, double poison, hipStream_t st) {
+  const long long work = 6LL * L.fs * L.n * n_vars;
+  if (work == 0) return;
+  k_poison_ghosts<<<grid_for(work), 256, 0, st>>>(L, n_vars, poison);
 }
 
 // mg_phi_bc_store_lvl (m_ghost_cells.f90:80-117): bc values -> rhs ghosts,
@@ -889,10 +911,10 @@ void launch_from_ref(const LevelView& L, int iv, const double* ref, hipStream_t 
   k_from_ref<<<grid_for(work), 256, 0, st>>>(L, iv, ref);
 }
 
-void launch_to_ref(const LevelView& L, int iv, double* ref, hipStream_t st) {
+void launch_to_ref(const LevelView& L, int iv, double* ref, double unstored, hipStream_t st) {
   const long long s = L.nc + 2, work = s * s * s * L.n;
   if (work == 0) return;
-  k_to_ref<<<grid_for(work), 256, 0, st>>>(L, iv, ref);
+  k_to_ref<<<grid_for(work), 256, 0, st>>>(L, iv, ref, unstored);
 }
 
 }  // namespace omg

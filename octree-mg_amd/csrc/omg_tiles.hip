@@ -127,7 +127,7 @@ __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const Le
     double l0, l1;
     op_pair<NC, OP>(K, F, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
     const double r0 = fr[r].x - l0, r1 = fr[r].y - l1;
-    mx = fmax(mx, fmax(fabs(r0), fabs(r1)));
+    mx = amax(mx, amax(fabs(r0), fabs(r1)));
     rv[r] = make_double2(r0, r1);
     st_nt(res + 2 * q2, r0, r1);
   }
@@ -1485,10 +1485,10 @@ __device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X,
     const int c = X.at(q % nc + 1, (q / nc) % nc + 1, q / (nc * nc) + 1);
     const double r = X.F[c] - op_value<OP>(K, tail_nbr(X, X.P, c));
     X.R[c] = r;
-    mx = fmax(mx, fabs(r));
+    mx = amax(mx, fabs(r));
   }
   if (red) {
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_down(mx, off, 64));
+    for (int off = 32; off > 0; off >>= 1) mx = amax(mx, __shfl_down(mx, off, 64));
     __syncthreads();   // every thread has read the previous maximum
     if (threadIdx.x == 0) *red = 0.0;
     __syncthreads();
@@ -1669,13 +1669,15 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
 
 // The tail's arguments into device memory, carried as a kernel argument (a
 // captured graph keeps its own copy; a pageable memcpy node would read the host
-// buffer when the graph runs). The struct is the first kernel argument, at
-// offset 0 of the kernarg segment: read it from there as words, vector stores.
+// buffer when the graph runs).  The parameter itself is copied, word by word
+// with vector stores (the compiler stages it wherever it likes: this one-block
+// kernel runs only when the arguments change), so no assumption on where the
+// by-value struct sits in the kernarg segment is made.
+static_assert(sizeof(TailArgs) % 4 == 0, "TailArgs is copied as 32-bit words");
+static_assert(sizeof(TailArgs) + sizeof(TailArgs*) <= 4096, "TailArgs must fit the 4 KiB kernel-argument limit");
+static_assert(alignof(TailArgs) <= 8, "TailArgs alignment");
 __global__ void __launch_bounds__(256) k_store_tail(TailArgs A, TailArgs* d) {
-  (void)A;
-  static_assert(sizeof(TailArgs) % 4 == 0, "TailArgs is copied as 32-bit words");
-  typedef const __attribute__((address_space(4))) unsigned kword;
-  kword* s = (kword*)__builtin_amdgcn_kernarg_segment_ptr();
+  const unsigned* s = reinterpret_cast<const unsigned*>(&A);
   unsigned* o = reinterpret_cast<unsigned*>(d);
   for (int i = threadIdx.x; i < (int)(sizeof(TailArgs) / 4); i += blockDim.x) o[i] = s[i];
 }

@@ -59,6 +59,7 @@ SIGNATURES = {
     "omg_diffusion_solve": (_I, [_P, _I, _D, _D, _I, _D, C.POINTER(_I), C.POINTER(_D)]),
     "omg_poisson_free_3d": (_I, [_P, _I, _D, _I, _I, C.POINTER(_D), _DP, C.c_void_p]),
     "omg_free_planes": (_I, [_P, C.POINTER(_I), _IP, C.c_void_p, _LL]),
+    "omg_comm_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I)]),
     "omg_synchronize": (_I, [_P]),
     "omg_stream": (_P, [_P]),
     "omg_set_profiling": (_I, [_P, _I]),
@@ -173,6 +174,13 @@ class Context:
         r = _D(0.0)
         self.call(name, *args, C.byref(r))
         return r.value
+
+    def comm_info(self):
+        """(ranks the communicator holds, transport): transport is "none",
+        "rccl" (ncclCommCount) or "loopback" (omg_comm_info)."""
+        n, t = _I(), _I()
+        self.call("comm_info", C.byref(n), C.byref(t))
+        return n.value, {0: "none", 1: "rccl", 2: "loopback"}[t.value]
 
     def kernel_stats(self, name):
         n, ms, cells = _LL(0), _D(0), _D(0)

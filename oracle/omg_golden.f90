@@ -31,7 +31,11 @@
 !     lb       lb (mg_load_balance) | lbp (+ mg_load_balance_parents)
 !     maxres   0 | 1  (request max_res from mg_fas_vcycle/mg_fas_fmg)
 !     dump     x, or a file: final phi interior of every box (ids order per
-!              level, lowest..highest, i fastest), raw float64, 1 rank only
+!              level, lowest..highest, i fastest), raw float64; with more
+!              than one rank every rank writes <file>.r<rank>: per box it
+!              owns, int32 lvl, int32 position in lvls(lvl)%ids, int32 nc,
+!              then the nc^3 doubles (tests/golden/make_golden.py reassembles
+!              the one-rank order)
 #include "cpp_macros.h"
 program omg_golden
   use mpi
@@ -188,7 +192,13 @@ program omg_golden
   t1 = mpi_wtime()
   if (mg%my_rank == 0) write(*, '(A,ES25.17,A,I0)') "TIME", (t1 - t0) / n_its, " NCPU ", mg%n_cpu
 
-  if (len_trim(a_dump) > 0 .and. mg%n_cpu == 1) call dump_phi(mg, trim(a_dump))
+  if (len_trim(a_dump) > 0) then
+     if (mg%n_cpu == 1) then
+        call dump_phi(mg, trim(a_dump))
+     else
+        call dump_phi_rank(mg, trim(a_dump))
+     end if
+  end if
 
   call mpi_barrier(mpi_comm_world, ierr)
   call mpi_finalize(ierr)
@@ -345,6 +355,30 @@ contains
     end do
     close(u)
   end subroutine dump_phi
+
+  ! multi-rank: this rank's boxes, each tagged with its place in the one-rank order
+  subroutine dump_phi_rank(mg, fname)
+    type(mg_t), intent(inout) :: mg
+    character(len=*), intent(in) :: fname
+    character(len=16) :: suffix
+    integer :: u, n, id, lvl, nc
+    write(suffix, '(A,I0)') ".r", mg%my_rank
+    open(newunit=u, file=fname // trim(suffix), access="stream", form="unformatted", status="replace")
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       nc = mg%box_size_lvl(lvl)
+       do n = 1, size(mg%lvls(lvl)%ids)
+          id = mg%lvls(lvl)%ids(n)
+          if (mg%boxes(id)%rank /= mg%my_rank) cycle
+          write(u) lvl, n, nc
+          if (mg%operator_type == mg_ahelmholtz) then
+             write(u) mg%boxes(id)%cc(1:nc, 1:nc, 1:nc, mg_irhs)
+          else
+             write(u) mg%boxes(id)%cc(1:nc, 1:nc, 1:nc, mg_iphi)
+          end if
+       end do
+    end do
+    close(u)
+  end subroutine dump_phi_rank
 
   subroutine sol_boundary_condition(box, nc, iv, nb, bc_type, bc)
     type(mg_box_t), intent(in) :: box

@@ -10,9 +10,11 @@ every box (ids order per level, lowest..highest, i fastest) where dumped.
 Only the numbers are committed (tests/golden/golden.json); the reference's
 sources and binaries never enter the repository.
 """
+import glob
 import hashlib
 import json
 import os
+import struct
 import subprocess
 import sys
 import tempfile
@@ -24,7 +26,7 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 # name: (box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres), dump?, ranks
 # BIG: too large for the CPU oracle in the quick CPU suite (the device is
 # compared with the reference's numbers directly; tests/test_gpu_parity.py)
-BIG = {"c3_per512_box16"}
+BIG = {"c3_per512_box16", "c2_256_box16_gsrb_d0", "c2_256_box16_gs_d0", "c5_helm256_box16_gsrb_d0"}
 CONFIGS = {
     # tests/test_uniform_grid 8 64 64 64 10 f, as shipped (GS)
     "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
@@ -54,7 +56,15 @@ CONFIGS = {
     "per128x64_box16_mixed": ("16 128 128 64 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 6]),
     # SURVEY §8(d) C3 at the bench's own size: 512^3 per GPU, box 16,
     # periodic, GSRB (the reference takes ~40 s on one core)
-    "c3_per512_box16": ("16 512 512 512 3 v gsrb lpl 0 per sol 1 lb 0", True, [1]),
+    # (2, 4 and 8 ranks: the BASELINE C3 configuration on 8 GPUs, and the
+    # MPICH allreduce order of get_sum at the bench's size)
+    "c3_per512_box16": ("16 512 512 512 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
+    # SURVEY §8(d) C2 at its own size: 256^3, box 16, Dirichlet 0, GSRB and
+    # the reference tests' lexicographic GS
+    "c2_256_box16_gsrb_d0": ("16 256 256 256 3 v gsrb lpl 0 d0 sol 1 lb 0", True, [1]),
+    "c2_256_box16_gs_d0": ("16 256 256 256 3 v gs lpl 0 d0 sol 1 lb 0", True, [1]),
+    # C5 at its own size: Helmholtz lambda = 10, 256^3, box 16
+    "c5_helm256_box16_gsrb_d0": ("16 256 256 256 3 v gsrb helm 10 d0 sol 1 lb 1", True, [1]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),
@@ -91,6 +101,25 @@ CONFIGS = {
     "diff_nonconv_helm_per_ref2": ("8 32 32 32 3 d2 gs helm 0.01 per phi 2 lb 0", False, [1], True),
     "diff_nonconv_vhelm_sol": ("8 32 32 32 3 d2 gs vhelm 0.001 sol phi 1 lb 0", False, [1], True),
 }
+
+
+def read_rank_dumps(fn):
+    """The multi-rank dump (omg_golden.f90 dump_phi_rank: <fn>.r<rank>, per
+    owned box int32 lvl, int32 position in lvls(lvl)%ids, int32 nc, nc^3
+    doubles) in the one-rank file's order: levels lowest first, ids order."""
+    boxes = []
+    for f in glob.glob(fn + ".r*"):
+        b = open(f, "rb").read()
+        o = 0
+        while o < len(b):
+            lvl, n, nc = struct.unpack_from("<3i", b, o)
+            o += 12
+            boxes.append(((lvl, n), b[o:o + 8 * nc ** 3]))
+            o += 8 * nc ** 3
+    boxes.sort(key=lambda x: x[0])
+    if len(set(k for k, _ in boxes)) != len(boxes):
+        raise RuntimeError("a box was dumped by two ranks")
+    return b"".join(v for _, v in boxes)
 
 
 def run(args, ranks, dump, expect_error=False):
@@ -135,7 +164,7 @@ def main():
             entry["big"] = True
         for r in ranks:
             with tempfile.TemporaryDirectory() as td:
-                fn = os.path.join(td, "phi.bin") if (dump and r == 1) else None
+                fn = os.path.join(td, "phi.bin") if dump else None
                 if expect_error:
                     its, t, err = run(args, r, fn, True)
                     entry["runs"][str(r)] = {"history": its, "error": err}
@@ -144,8 +173,11 @@ def main():
                 its, t = run(args, r, fn)
                 run_entry = {"history": its, "ref_seconds_per_cycle": t}
                 if fn:
-                    with open(fn, "rb") as f:
-                        b = f.read()
+                    if r == 1:
+                        with open(fn, "rb") as f:
+                            b = f.read()
+                    else:
+                        b = read_rank_dumps(fn)
                     key = "rhs_sha256" if " ahelm " in args else "phi_sha256"
                     run_entry[key] = hashlib.sha256(b).hexdigest()
                     run_entry["phi_bytes"] = len(b)

@@ -1,0 +1,41 @@
+"""bench.py's own multi-rank launcher on the CPU: `python bench.py --gpus N`
+without torchrun starts N ranks itself (one process each, gloo for the
+host-side collectives); with --plan-only every rank builds the bench tree's
+plan-only context (OMG_DEVICE_NONE) and the ranks check over gloo that every
+transfer pairs up with its peer's, key for key in wire order — the plans the
+RCCL halo exchange of the driver's multi-GPU run uses."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=600, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]   # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n,mode,domain", [(2, "weak", [1024, 512, 512]),
+                                           (4, "strong", [512, 512, 512]),
+                                           (8, "weak256", [512, 512, 512])])
+def test_launcher_spawns_ranks_whose_plans_pair_up(n, mode, domain):
+    out = _run("--gpus", str(n), "--mode", mode, "--plan-only")
+    assert out["n_ranks"] == n and out["domain"] == domain
+    assert [r["rank"] for r in out["ranks"]] == list(range(n))
+    assert out["ok"], [r["problems"] for r in out["ranks"]]
+    # Morton chunks: every rank owns an equal share of the finest level and
+    # exchanges faces with its octant neighbours only
+    boxes = {r["boxes_lvl_hi"] for r in out["ranks"]}
+    assert len(boxes) == 1
+    for r in out["ranks"]:
+        assert r["halo_faces_recv_lvl_hi"] > 0 and 1 <= len(r["peers_lvl_hi"]) <= min(3, n - 1)

@@ -12,16 +12,37 @@ import pytest
 from tests.mgdriver import run_problem, run_problem_loopback
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
-MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) for r in e["runs"] if int(r) > 1]
+MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if not e.get("big") for r in e["runs"] if int(r) > 1]
+# the BASELINE C3 configuration itself (512^3, box 16, periodic, GSRB) as the
+# reference ran it on 2, 4 and 8 MPI ranks
+BIG_MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if e.get("big") for r in e["runs"] if int(r) > 1]
 
 pytestmark = pytest.mark.gpu
+
+
+def _check(out, run):
+    """History bit for bit, and the final phi of every box (gathered from its
+    owner) against the reference's own per-rank dump where it made one."""
+    assert out["history"] == run["history"]
+    if "phi_sha256" in run:
+        assert out["phi_sha256"] == run["phi_sha256"]
 
 
 @pytest.mark.parametrize("name,ranks", MULTI)
 def test_multirank_matches_reference_golden(name, ranks):
     e = GOLDEN[name]
     out = run_problem_loopback(e["args"], ranks)
-    assert out["history"] == e["runs"][str(ranks)]["history"]
+    _check(out, e["runs"][str(ranks)])
+
+
+# bench.py's replication bound (64 boxes of 16^3) and none: the 8-GPU bench
+# configuration, every level's exchange through the same plans RCCL runs
+@pytest.mark.parametrize("rep", [0, 64 * 16 ** 3])
+@pytest.mark.parametrize("name,ranks", BIG_MULTI)
+def test_c3_512_multirank_matches_reference_golden(name, ranks, rep):
+    e = GOLDEN[name]
+    out = run_problem_loopback(e["args"], ranks, rep_cells=rep)
+    _check(out, e["runs"][str(ranks)])
 
 
 # Replicated coarse levels (omg_set_coarse_replication): every coarse level
@@ -33,7 +54,7 @@ def test_multirank_matches_reference_golden(name, ranks):
 def test_multirank_replicated_coarse_matches_golden(name, ranks, rep):
     e = GOLDEN[name]
     out = run_problem_loopback(e["args"], ranks, rep_cells=rep)
-    assert out["history"] == e["runs"][str(ranks)]["history"]
+    _check(out, e["runs"][str(ranks)])
 
 
 # Box-16 periodic levels where only the boxes without a face on another rank
@@ -50,7 +71,7 @@ FUSED = [("per128_box16_gsrb_v", 2), ("per128_box16_gsrb_v", 8), ("per128x64_box
 def test_multirank_fused_down_step_phi_matches_oracle(name, ranks):
     e = GOLDEN[name]
     out = run_problem_loopback(e["args"], ranks)
-    assert out["history"] == e["runs"][str(ranks)]["history"]
+    _check(out, e["runs"][str(ranks)])
     orc = run_problem(e["args"], backend="oracle", n_ranks=ranks)
     assert orc["history"] == out["history"]
     assert out["phi_sha256"] == orc["phi_sha256"]
