@@ -17,7 +17,7 @@ for spec in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I/opt/rocm/include \
     $flags -x hip -c -o $d/omg_api.o omg_api.cpp &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o ../_variants/libomg_$name.so $d/*.o -shared -L/opt/rocm/lib -lrccl -lhipfft \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o ../_variants/libomg_$name.so $d/*.o -shared -L/opt/rocm/lib -lrccl -lhipfft -lrocprofiler-sdk-roctx \
     -Wl,-rpath,/opt/rocm/lib
 done
 ls -la ../_variants
