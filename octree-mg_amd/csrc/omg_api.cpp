@@ -781,7 +781,8 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
 
 // correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
 // V-cycle and FMG run them (m_multigrid.f90:127-136, 216-219); fused when every
-// box of lvl+1 has its parent on this GPU and no refinement boundary.
+// box of lvl+1 has its parent on this GPU (refinement-boundary ghosts are
+// interpolated in the same kernel from lvl, which is final by then).
 // then_gsrb: the caller smooths lvl+1 with red-black substeps right after
 // (colour 1 first), so colour 1's correction is dead where no face needs it.
 // save_old (FMG, fused path only, see correct_fill_fused): old = phi of lvl+1
@@ -789,7 +790,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
 bool correct_fill_fused(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
-  return F && C && F->n && F->n_pairs == F->n && !F->has_rb && tiled_nc(F->nc) &&
+  return F && C && F->n && F->n_pairs == F->n && tiled_nc(F->nc) && !(F->has_rb && c->no_rb_fill_fuse) &&
          !(c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv));
 }
 
@@ -809,7 +810,8 @@ void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false, bool save_old
     {
       Prof p(c, "prolong_fill", (double)F->n * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->sweep_view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
-                          F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream, nullptr, 0, save_old);
+                          F->d_sendbuf, sub, then_gsrb && !c->no_skip1, c->stream, nullptr, 0, save_old,
+                          F->h_rb.empty() ? nullptr : F->d_rb);
     }
     finish_halo(c, F, 1);
     F->phi_gc_ok = true;
@@ -2147,6 +2149,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
+    c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only

@@ -1,6 +1,9 @@
 // omg_face.h — device helpers for the ghost-face work of the tiled kernels.
 #pragma once
 
+#include <cstddef>
+#include <type_traits>
+
 #include "omg_device.h"
 #include "omg_kernels.h"
 
@@ -128,11 +131,12 @@ __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int c
 
 // Ghost fill of phi for box b whose final interior is staged in LDS `sb`
 // (Tl<NC> layout): same-GPU faces pushed (colours mask), physical ghosts
-// recomputed, remote faces packed.  Refinement boundaries are not handled
-// here (levels that have them take the generic kernels).
-template <int NC>
+// recomputed, remote faces packed.  rb_ghost(arg, nb, a, c, x1, x2):
+// refinement-boundary faces (NB_RB) too, from the fine box's own boundary
+// cells and the coarse level (sides_rb); null: the level has none.
+template <int NC, class RbGhost = std::nullptr_t>
 __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const double* sb, int colours,
-                                               const GcBC& bc, double* sendbuf) {
+                                               const GcBC& bc, double* sendbuf, const RbGhost& rb_ghost = nullptr) {
   using TL = Tl<NC>;
   face_push_local<NC>(L, b, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
   double* u = L.phi + (long long)b * L.stride;
@@ -155,6 +159,11 @@ __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const 
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const int gi = TL::ogh(nb, a, c);
       u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, sb[TL::oint(i2, j2, k2)]);
+    } else if constexpr (!std::is_same<RbGhost, std::nullptr_t>::value) {
+      if (kind == NB_RB) {
+        const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
+        u[TL::ogh(nb, a, c)] = rb_ghost(arg, nb, a, c, v1, sb[TL::oint(i2, j2, k2)]);
+      }
     }
   }
 }

@@ -247,6 +247,7 @@ struct omg_ctx {
   bool no_skip1 = false;               // OMG_NO_SKIP1: correct colour 1 before the up-smoothing too
   bool no_fuse_down = false;           // OMG_NO_FUSE_DOWN: last down-substep and residual + restriction apart
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
+  bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

@@ -131,9 +131,12 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 // red-black substep follows, so all-local boxes correct and push colour 0 only
 // save_old (with !skip1): also old = phi on the interior, from the values
 // before the correction (FMG, launch_copy_ghosts for the ghost faces)
+// rb: the fine level's refinement-boundary records (its NB_RB ghosts are
+// interpolated from C, sides_rb), or null when it has none
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
-                         hipStream_t st, const int* list = nullptr, int n_list = 0, bool save_old = false);
+                         hipStream_t st, const int* list = nullptr, int n_list = 0, bool save_old = false,
+                         const RBRec* rb = nullptr);
 // old = phi on the ghost faces (and padding) of every box: [2*hv, stride)
 void launch_copy_ghosts(const LevelView& L, hipStream_t st);
 // correct_children + fill + the first up-smoothing substep (colour 1) in one

@@ -379,11 +379,11 @@ __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, 
 // save_old: FMG's `old = phi` of this level (m_multigrid.f90:127-129) for the
 // interior, from the pre-correction values loaded here anyway (the caller
 // copies the ghost faces before the launch; needs !skip1: every pair loaded).
-template <int NC, int BS, bool SUB>
+template <int NC, int BS, bool SUB, bool RB = false>
 __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
                                                  const int* parent_local, const int* dixp, const GcBC& bc,
                                                  double* sendbuf, int b, double* lds, bool skip1,
-                                                 bool save_old = false) {
+                                                 bool save_old = false, const RBRec* rb = nullptr) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
   double* cb = lds;                     // the parent's octant + one face layer around it
@@ -428,17 +428,29 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     if (save_old) st_nt(F.data + 2 * F.vstride + (long long)b * F.stride + 2 * q2, old[r].x, old[r].y);
   }
   __syncthreads();
-  tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf);
+  if constexpr (RB) {
+    // refinement boundaries: the coarse neighbour lives on Cv, the level the
+    // correction came from (fill_refinement_bnd + sides_rb, m_ghost_cells.f90:
+    // 287-328, 769-861), now final for this up-step
+    const RbSide rbs{Cv, rb};
+    tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf,
+                       [&](int arg, int nb, int a, int c, double v1, double v2) {
+                         return rb_ghost(F, rbs, arg, nb, a, c, v1, v2);
+                       });
+  } else {
+    tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf);
+  }
 }
 
-template <int NC, int BS, bool SUB>
+template <int NC, int BS, bool SUB, bool RB = false>
 __global__ void __launch_bounds__(BS) k_prolong_fill(LevelView Cv, LevelView F, int iv,
                                                      const int* parent_local, const int* dixp, GcBC bc,
-                                                     double* sendbuf, int skip1, const int* list, int save_old) {
+                                                     double* sendbuf, int skip1, const int* list, int save_old,
+                                                     const RBRec* rb) {
   __shared__ double lds[prolong_cb<NC>() + Tl<NC>::HV * 2];
   const int t = xcd_box(blockIdx.x, gridDim.x, F.rev);
-  prolong_fill_box<NC, BS, SUB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, list ? list[t] : t, lds, skip1 != 0,
-                                save_old != 0);
+  prolong_fill_box<NC, BS, SUB, RB>(Cv, F, iv, parent_local, dixp, bc, sendbuf, list ? list[t] : t, lds,
+                                    skip1 != 0, save_old != 0, rb);
 }
 
 // correct_children + fill + the first up-smoothing substep in one pass
@@ -935,16 +947,20 @@ void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, doubl
 
 void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const int* parent_local,
                          const int* dixp, const GcBC& bc, double* sendbuf, bool sub, bool skip1,
-                         hipStream_t st, const int* list, int n_list, bool save_old) {
+                         hipStream_t st, const int* list, int n_list, bool save_old, const RBRec* rb) {
   const int n = list ? n_list : F.n;
   if (n == 0) return;
   const dim3 g(n);
   const int so = save_old && !skip1;
-#define OMG_PF(NC, BS)                                                                                         \
-  if (sub)                                                                                                     \
-    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so);  \
-  else                                                                                                         \
-    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so);
+#define OMG_PF(NC, BS)                                                                                              \
+  if (rb && sub)                                                                                                    \
+    k_prolong_fill<NC, BS, true, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so, rb); \
+  else if (rb)                                                                                                      \
+    k_prolong_fill<NC, BS, false, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so, rb); \
+  else if (sub)                                                                                                     \
+    k_prolong_fill<NC, BS, true><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so, rb); \
+  else                                                                                                              \
+    k_prolong_fill<NC, BS, false><<<g, BS, 0, st>>>(C, F, iv, parent_local, dixp, bc, sendbuf, skip1, list, so, rb);
   switch (F.nc) {
     case 16: OMG_PF(16, 512) break;
     case 8: OMG_PF(8, 256) break;
