@@ -51,21 +51,32 @@ struct RbSide {
 // Refinement-boundary ghost (box_gc_for_fine_neighbor + sides_rb,
 // m_ghost_cells.f90:287-328, 500-577, 769-861) of face nb at (a, c) from the
 // two boundary cells v1 (layer x1) and v2 (layer x2) of the fine box.
-__device__ __forceinline__ double rb_ghost(const LevelView& L, const RbSide& R, int arg, int nb, int a, int c,
-                                           double v1, double v2) {
-  const RBRec rec = R.rb[arg];
+// The coarse operands: the coarse cell facing (a, c) and its four in-face
+// neighbours.  They stay fixed while the fine level is smoothed (nothing
+// writes the coarse level then), so the smoother loads them early.
+struct RbCoarse {
+  double tc, m1, p1, m2, p2;
+};
+__device__ __forceinline__ RbCoarse rb_coarse_load(const LevelView& L, const RbSide& R, const RBRec& rec, int nb,
+                                                   int a, int c) {
   const double* cu = R.C.phi + (long long)rec.coarse_idx * R.C.stride;
   const int d = (nb + 1) >> 1;
   const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;
   const int clayer = (nb & 1) ? L.nc : 1;
   const int i = (a + 1) >> 1, j = (c + 1) >> 1;
   auto T = [&](int p, int q) { return cu[off_face_cell(R.C, nb, clayer, rec.dix[t1] + p, rec.dix[t2] + q)]; };
-  const double tc = T(i, j);
-  const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
-  const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
-  double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
+  return RbCoarse{T(i, j), T(i - 1, j), T(i + 1, j), T(i, j - 1), T(i, j + 1)};
+}
+__device__ __forceinline__ double rb_ghost_from(const RbCoarse& t, int a, int c, double v1, double v2) {
+  const double g1 = 0.125 * (t.p1 - t.m1);
+  const double g2 = 0.125 * (t.p2 - t.m2);
+  double gv = ((a - 1) & 1) ? t.tc + g1 : t.tc - g1;
   gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
   return 0.5 * gv + 0.75 * v1 - 0.25 * v2;
+}
+__device__ __forceinline__ double rb_ghost(const LevelView& L, const RbSide& R, int arg, int nb, int a, int c,
+                                           double v1, double v2) {
+  return rb_ghost_from(rb_coarse_load(L, R, R.rb[arg], nb, a, c), a, c, v1, v2);
 }
 
 // Variable-coefficient operators read eps (var 5; vars 5..7 for the
@@ -142,6 +153,12 @@ __device__ __forceinline__ void op_pair(const OpCoef<OP>& K, const LevelView& L,
 #define OMG_T_YZ 0
 #endif
 
+// timing switch: 0 = refinement-boundary coarse operands loaded in the ghost
+// fill instead of prefetched
+#ifndef OMG_RB_PRE
+#define OMG_RB_PRE 1
+#endif
+
 // RB: the level has refinement-boundary faces (a separate instantiation keeps
 // their interpolation out of the plain kernels)
 template <int NC, int OP, int BS, int NT, bool PRE = false, bool RB = false>
@@ -158,6 +175,25 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   const long long boff = (long long)b * L.stride;
   double* __restrict__ u = L.phi + boff;
   const OpCoef<OP> K(L, lambda);
+
+  // Refinement-boundary faces: the face kinds and records are issued first,
+  // the coarse operands after the stream-in (below), so the ghost fill after
+  // the substep finds them in registers instead of running three dependent
+  // loads (kind -> record -> coarse cells) at the end.
+  constexpr bool RBP = RB && OMG_RB_PRE;
+  constexpr int NF = 6 * NC * NC, NPF = RBP ? (NF + BS - 1) / BS : 1;
+  int rkind[NPF], rarg[NPF];
+  RBRec rrec[NPF];
+  RbCoarse rt[NPF];
+  if constexpr (RBP) {
+#pragma unroll
+    for (int r = 0; r < NPF; r++) {
+      const int p = tid + BS * r;
+      const long long fidx = (long long)b * 6 + (p < NF ? p / (NC * NC) : 0);
+      rkind[r] = p < NF ? L.nbk[fidx] : NB_LOCAL;
+      rarg[r] = p < NF ? L.nba[fidx] : 0;
+    }
+  }
 
   // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
   if (!PRE) {
@@ -190,7 +226,20 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   else
     gsrb_load_rhs<NC, BS, NT>(L, e, b, frs);
   const double2* fr = frs.v;
+  if constexpr (RBP) {
+#pragma unroll
+    for (int r = 0; r < NPF; r++)
+      if (rkind[r] == NB_RB) rrec[r] = rbs->rb[rarg[r]];
+  }
   __syncthreads();
+  if constexpr (RBP) {
+#pragma unroll
+    for (int r = 0; r < NPF; r++) {
+      if (rkind[r] != NB_RB) continue;
+      const int p = tid + BS * r, cell = p % (NC * NC);
+      rt[r] = rb_coarse_load(L, *rbs, rrec[r], p / (NC * NC) + 1, cell % NC + 1, cell / NC + 1);
+    }
+  }
 
   // ---- colour e update ----------------------------------------------------
   // Each thread updates two neighbouring cells of one row (colour indices ih,
@@ -273,12 +322,11 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     return ((i + j + k) & 1) == e ? se[idx] : so[idx];
   };
   face_push_local<NC>(L, b, colours, cellv, (OMG_T_YZ & 1) ? 0x3u : 0x3fu);
-  for (int p = tid; p < 6 * NC * NC; p += BS) {
+  auto fill_cell = [&](int p, int kind, int arg, const RbCoarse* rc) {
+    if (kind == NB_LOCAL) return;
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
     const long long fidx = (long long)b * 6 + nb - 1;
-    const int kind = L.nbk[fidx];
-    if (kind == NB_LOCAL) continue;
-    const int a = cell % NC + 1, c = cell / NC + 1, arg = L.nba[fidx];
+    const int a = cell % NC + 1, c = cell / NC + 1;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1;
     // boundary cell x1 (and x2) of this face
@@ -296,8 +344,20 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, cellv(i2, j2, k2));
     } else if (RB && kind == NB_RB) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
-      u[off_gh(L, nb, a, c)] = rb_ghost(L, *rbs, arg, nb, a, c, v1, cellv(i2, j2, k2));
+      const double v2 = cellv(i2, j2, k2);
+      u[off_gh(L, nb, a, c)] = RBP ? rb_ghost_from(*rc, a, c, v1, v2) : rb_ghost(L, *rbs, arg, nb, a, c, v1, v2);
     }   // NB_RBREM: the caller's refinement-boundary exchange (finish_rb)
+  };
+  if constexpr (RBP) {
+#pragma unroll
+    for (int r = 0; r < NPF; r++)
+      if (tid + BS * r < NF) fill_cell(tid + BS * r, rkind[r], rarg[r], &rt[r]);
+  } else {
+    for (int p = tid; p < NF; p += BS) {
+      const long long fidx = (long long)b * 6 + p / (NC * NC);
+      const int kind = L.nbk[fidx];
+      if (kind != NB_LOCAL) fill_cell(p, kind, L.nba[fidx], nullptr);
+    }
   }
 }
 
