@@ -485,9 +485,27 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
 }
 
 void materialize_level(omg_ctx* c, Level* L);
+void drop_rhs_lex(omg_ctx* c);
 void phi_mean_ready(omg_ctx* c);
 double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
+
+// whether launch_gsrb_resident serves this level: one GPU's boxes only (no
+// face on another rank, no refinement boundary toward one), all resident at
+// once, box 16 or 8, Laplacian / Helmholtz; never inside a captured cycle, and
+// not under the loopback transport, whose ranks share one GPU and could each
+// hold part of the CUs their grid barriers wait for
+bool resident_level(omg_ctx* c, Level* L) {
+  if (c->no_resident || c->capturing || c->loop || !L->n || L->has_remote || (L->nc != 16 && L->nc != 8) ||
+      (c->op != OP_LPL && c->op != OP_HELM))
+    return false;
+  if (L->resident_ok < 0) {
+    bool ok = true;
+    for (int8_t k : L->h_nbk) ok = ok && k != NB_REMOTE && k != NB_RBREM;
+    L->resident_ok = ok && L->n <= gsrb_resident_capacity(L->nc, c->op, L->has_rb);
+  }
+  return L->resident_ok > 0;
+}
 
 // smooth_boxes (m_multigrid.f90:404-424)
 void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0) {
@@ -501,16 +519,33 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
                       !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
+    // the compacted-plane kernel reads rhs from its plane-order copy, rebuilt
+    // here when a write since the last build dropped it (update_coarse for
+    // the levels below the top, every entry point that may change rhs)
+    const bool plane = L->n && n_sub >= 1 && L->d_rhs_lex && gs_lex_plane_ok(L->nc, c->op);
+    if (plane && !L->rhs_lex_ok) {
+      Prof p(c, "rhs_lex", (double)L->n * L->nc * L->nc * L->nc, lvl);
+      launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream);
+      L->rhs_lex_ok = true;
+    }
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gs_lex(L->view(), c->op, c->lambda, c->stream);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr);
       }
       fill_gc_lvl(c, lvl, 1);
     }
     return;
   }
-  for (int n = first_substep; n <= n_sub; n++) {
+  // small levels: the substeps after the first in one launch (resident
+  // boxes, grid barrier between substeps); the first stays a plain substep
+  // when it absorbs a shift or the ghosts are not current (its fill follows)
+  int n_end = n_sub;
+  if (resident_level(c, L)) {
+    const int n_res = (absorb || !L->phi_gc_ok) ? first_substep + 1 : first_substep;
+    if (n_sub - n_res + 1 >= 2) n_end = n_res - 1;
+  }
+  for (int n = first_substep; n <= n_end; n++) {
     // substep n updates the cells with i+j+k+n even, i.e. colour e = n mod 2,
     // and ends with the ghost fill; same-GPU neighbours only need colour e
     // when their ghost faces were consistent before the substep.
@@ -555,6 +590,13 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     finish_halo(c, L, 1);
     if (odd || !L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
   }
+  if (n_end < n_sub) {
+    Prof p(c, "smoother_gsrb", 0.5 * (n_sub - n_end) * L->n * L->nc * L->nc * L->nc, lvl);
+    if (!launch_gsrb_resident(L->view(), c->op, c->lambda, n_end + 1, n_sub, view_of(c, lvl - 1), L->d_rb,
+                              L->has_rb, bc_for(c, lvl, 1), c->d_gbar, c->stream))
+      throw OmgError("smooth_boxes: resident smoother not available for this level");
+    c->gbar_used = true;
+  }
 }
 
 bool tiled_level(omg_ctx* c, const Level* L) {
@@ -572,6 +614,24 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
+// The resident smoother's grid barrier waits a bounded time: a timeout (a
+// grid that was not resident at once) leaves a flag, reported here as an
+// error at the next read-back instead of a hang.
+void grid_barrier_verdict(omg_ctx* c, unsigned flag) {
+  c->gbar_used = false;
+  if (!flag) return;
+  HIPCHK(hipMemsetAsync(c->d_gbar, 0, 4 * sizeof(unsigned), c->stream));
+  throw OmgError("resident smoother: grid barrier timed out (workgroups not co-resident); set OMG_NO_RESIDENT=1");
+}
+void check_grid_barrier(omg_ctx* c) {
+  if (!c->gbar_used || c->capturing) return;
+  unsigned f = 0;
+  HIPCHK(hipMemcpyAsync(c->h_scalar + 3, c->d_gbar + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  f = *reinterpret_cast<const unsigned*>(c->h_scalar + 3);
+  grid_barrier_verdict(c, f);
+}
+
 // max over levels lo..hi of max_residual_lvl (m_multigrid.f90:296-311), this
 // rank only: the levels' maxima fold into one word on the device, read back
 // with one synchronisation
@@ -587,7 +647,10 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     c->max_deferred = true;
     return 0.0;
   }
+  const bool gbar = c->gbar_used;
+  if (gbar) HIPCHK(hipMemcpyAsync(c->h_scalar + 3, c->d_gbar + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (gbar) grid_barrier_verdict(c, *reinterpret_cast<const unsigned*>(c->h_scalar + 3));
   return c->h_scalar[0];
 }
 
@@ -662,6 +725,7 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
 void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
   Level* F = level_ptr(c, lvl);
   if (Level* Cl = level_ptr(c, lvl - 1)) {
+    Cl->rhs_lex_ok = false;   // its rhs is rewritten below
     // restriction overwrites every box of an all-parents level (interior), and
     // the fill below every ghost face: a pending shift there is dead
     if (Cl->all_parents) Cl->shift_pending = false;
@@ -952,7 +1016,26 @@ void materialize_phi(omg_ctx* c) {
   for (auto& kv : c->levels) materialize_level(c, &kv.second);
   c->phi_shift_pending = false;
 }
-void drop_rhs_cache(omg_ctx* c) { c->rhs_cache_valid = false; }
+// the plane-order rhs copies: every write of a level's rhs drops its copy
+void drop_rhs_lex(omg_ctx* c) {
+  for (auto& kv : c->levels) kv.second.rhs_lex_ok = false;
+}
+// plane-order rhs buffers for the levels the compacted-plane lexicographic
+// kernel serves (allocated outside any graph capture: tree setup, smoother
+// choice)
+void ensure_rhs_lex(omg_ctx* c) {
+  if (c->host_only || c->smoother == OMG_SMOOTHER_GSRB || c->no_gs_plane) return;
+  for (auto& kv : c->levels) {
+    Level& L = kv.second;
+    if (L.d_rhs_lex || !L.n || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
+    dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
+    L.rhs_lex_ok = false;
+  }
+}
+void drop_rhs_cache(omg_ctx* c) {
+  c->rhs_cache_valid = false;
+  drop_rhs_lex(c);
+}
 // entry points other than the cycles: apply pending phi work first; `writes`
 // = the call may change rhs (the cached rhs sum is dropped)
 void enter(omg_ctx* c, bool writes = true) {
@@ -984,6 +1067,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       leaf_sum_device(c, 2, kChRhs);
     }
     c->rhs_cache_valid = false;
+    drop_rhs_lex(c);
     mean_device(c, kChRhs);
     bool all_fused = true;
     for (int l = c->lowest; l <= c->highest; l++) {
@@ -1073,6 +1157,7 @@ void run_tail(omg_ctx* c, int top) {
       if (L->all_parents && l < top) L->shift_pending = false;   // overwritten by the restriction
       else materialize_level(c, L);
     }
+    L->rhs_lex_ok = false;   // the tail writes the rhs of the levels below its top
     TailLevel& T = A.lv[l - c->lowest];
     T.L = L->view();
     T.bc = bc_for(c, l, 1);
@@ -1775,6 +1860,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
+    dfree(L.d_rhs_lex);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
@@ -2092,6 +2178,7 @@ void build_plan(omg_ctx* c) {
       dmalloc(&L.d_rbrecv, sizeof(double) * (size_t)L.rbx.n_recv * L.rbx.item_doubles);
     }
   }
+  ensure_rhs_lex(c);
 }
 
 }  // namespace
@@ -2150,6 +2237,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
+    c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
+    c->no_resident = env_flag("OMG_NO_RESIDENT");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only
@@ -2159,6 +2248,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMalloc(&c->d_maxslots, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
+    HIPCHK(hipMalloc(&c->d_gbar, 4 * sizeof(unsigned)));
+    HIPCHK(hipMemset(c->d_gbar, 0, 4 * sizeof(unsigned)));
     // (allocated here: no allocation may happen while a cycle is captured)
     HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
     c->h_tail = new TailArgs;
@@ -2220,6 +2311,7 @@ int omg_ctx_destroy(omg_ctx* c) {
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_maxslots);
+    dfree(c->d_gbar);
     for (auto& kv : c->graphs)
       if (kv.second) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -2329,6 +2421,7 @@ int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up,
       throw OmgError("unsupported smoother type");
     c->smoother = smoother;
     c->n_substeps = smoother == OMG_SMOOTHER_GSRB ? 2 : 1;
+    ensure_rhs_lex(c);
     c->n_cycle_down = n_cycle_down;
     c->n_cycle_up = n_cycle_up;
     c->max_coarse_cycles = max_coarse_cycles;
@@ -2640,6 +2733,7 @@ int omg_synchronize(omg_ctx* c) {
   return guarded([&] {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->stream2));
+    check_grid_barrier(c);
   });
 }
 

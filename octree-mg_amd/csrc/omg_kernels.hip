@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 namespace omg {
 
@@ -337,6 +338,205 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
     for (int s = 0; s < PF; s++)
 #pragma unroll
       for (int r = 0; r < NL; r++) ring[s][r] = ringn[s][r];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Lexicographic GS over compacted hyperplanes.  k_gs_lex_wave gives every
+// thread a fixed line (j, k) and walks all 46 planes, so 65 % of its slots
+// fall outside the box, and each lane reads the rhs of its own line: 64 cache
+// lines per wave-instruction.  Here the cells of plane d = i+j+k are numbered
+// (k, then j, ascending) and thread t takes the t-th: a 16^3 plane has at most
+// 192 cells, one per thread of a 192-thread workgroup.  rhs is read from a
+// copy in that plane order (k_rhs_lex, built once per cycle per level), so
+// each plane's rhs is one contiguous run.  Same cells per plane, same
+// operands and gs_value: bit-identical.
+template <int NC>
+struct LexPlanes {
+  static constexpr int NPL = 3 * NC - 2, N3 = NC * NC * NC;
+  unsigned short cell[N3];       // dense (NC+2)^3 index of the t-th cell in plane order
+  unsigned short off[NPL + 1];   // first cell of plane d - 3
+  int maxn;                      // the largest plane
+};
+template <int NC>
+constexpr LexPlanes<NC> make_lex_planes() {
+  LexPlanes<NC> P{};
+  constexpr int S = NC + 2;
+  int t = 0;
+  P.maxn = 0;
+  for (int d = 3; d <= 3 * NC; d++) {
+    P.off[d - 3] = (unsigned short)t;
+    for (int k = 1; k <= NC; k++)
+      for (int j = 1; j <= NC; j++) {
+        const int i = d - j - k;
+        if (i >= 1 && i <= NC) P.cell[t++] = (unsigned short)(i + S * (j + S * k));
+      }
+    if (t - P.off[d - 3] > P.maxn) P.maxn = t - P.off[d - 3];
+  }
+  P.off[LexPlanes<NC>::NPL] = (unsigned short)t;
+  return P;
+}
+constexpr LexPlanes<16> kLexPlanes16 = make_lex_planes<16>();
+constexpr LexPlanes<8> kLexPlanes8 = make_lex_planes<8>();
+static_assert(kLexPlanes16.off[LexPlanes<16>::NPL] == 4096 && kLexPlanes16.maxn == 192, "16^3 planes");
+static_assert(kLexPlanes8.off[LexPlanes<8>::NPL] == 512 && kLexPlanes8.maxn == 48, "8^3 planes");
+__constant__ LexPlanes<16> dLexPlanes16 = kLexPlanes16;
+__constant__ LexPlanes<8> dLexPlanes8 = kLexPlanes8;
+template <int NC>
+__device__ __forceinline__ const LexPlanes<NC>& lex_planes() {
+  if constexpr (NC == 16) return dLexPlanes16;
+  else return dLexPlanes8;
+}
+template <int NC>
+constexpr int lex_maxn() { return NC == 16 ? kLexPlanes16.maxn : kLexPlanes8.maxn; }
+
+// rhs of every box in plane order: rl[b * NC^3 + t] = rhs at the t-th cell
+template <int NC>
+__global__ void __launch_bounds__(256) k_rhs_lex(LevelView L, double* __restrict__ rl) {
+  using TL = Tl<NC>;
+  constexpr int N3 = NC * NC * NC, S = NC + 2;
+  __shared__ double F[N3];
+  const LexPlanes<NC>& X = lex_planes<NC>();
+  const int b = blockIdx.x;
+  const v2d* f = reinterpret_cast<const v2d*>(boxp(L, 2, b));
+  for (int q = threadIdx.x; q < N3 / 2; q += blockDim.x) reinterpret_cast<v2d*>(F)[q] = f[q];
+  __syncthreads();
+  double* o = rl + (long long)b * N3;
+  for (int t = threadIdx.x; t < N3; t += blockDim.x) {
+    const int c = X.cell[t], i = c % S, j = (c / S) % S, k = c / (S * S);
+    o[t] = F[TL::oint(i, j, k)];
+  }
+}
+
+template <int OP, int NC, int T, int WPS>
+__global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lambda,
+                                                         const double* __restrict__ rl) {
+  using TL = Tl<NC>;
+  constexpr int S = NC + 2, N3 = NC * NC * NC, H = TL::H, HV = TL::HV, FS = TL::FS;
+  constexpr int NPL = LexPlanes<NC>::NPL, PF = OMG_GS_PF, NQ = (TL::NST / 2 + T - 1) / T;
+  constexpr int NLP = (lex_maxn<NC>() + T - 1) / T;   // cells per thread per plane
+  constexpr int NPP = ((NPL + PF - 1) / PF) * PF;     // planes padded to whole groups of PF
+  __shared__ double P[gs_wave_lds<NC, T>()];
+  const LexPlanes<NC>& X = lex_planes<NC>();
+  const int tid = threadIdx.x, G = gridDim.x;
+  const OpCoef<OP> K(L, lambda);
+  auto dense = [&](int q) {
+    int i, j, k;
+    if (q < 2 * HV) {
+      TL::decode(q, i, j, k);
+    } else {
+      const int r0 = q - 2 * HV, nb = r0 / FS + 1, r1 = r0 % FS;
+      const int e = r1 >= H * NC, r = r1 - e * H * NC, ah = r % H, c = r / H + 1;
+      const int g = (nb & 1) ? 0 : NC + 1;
+      const int a = 2 * ah + 1 + ((1 + g + c + e) & 1);
+      const int d = (nb + 1) >> 1;
+      if (d == 1) { i = g; j = a; k = c; }
+      else if (d == 2) { i = a; j = g; k = c; }
+      else { i = a; j = c; k = g; }
+    }
+    return i + S * (j + S * k);
+  };
+  constexpr int NG2 = (HV + T - 1) / T;
+  unsigned scat[NQ], gath[NG2];
+#pragma unroll
+  for (int r = 0; r < NQ; r++) {
+    const int q2 = min(tid + T * r, TL::NST / 2 - 1);
+    scat[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
+  }
+#pragma unroll
+  for (int r = 0; r < NG2; r++) {
+    const int q2 = min(tid + T * r, HV - 1);
+    gath[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
+  }
+  // plane pl's rhs and LDS cell of this thread's slots (clamped: past-the-end
+  // slots and padding planes read a valid cell and update nothing)
+  auto plane_issue = [&](const double* rb, int pl, double* ov, int* oc) {
+    const int p = min(pl, NPL - 1), o = X.off[p], n = X.off[p + 1] - o;
+#pragma unroll
+    for (int r = 0; r < NLP; r++) {
+      const int idx = o + min(tid + T * r, n - 1);
+      oc[r] = X.cell[idx];
+      ov[r] = rb[idx];
+    }
+  };
+  double rv[PF][NLP], rvn[PF][NLP];
+  int rc[PF][NLP], rcn[PF][NLP];
+  v2d buf[NQ];
+  auto issue = [&](int q, double (*gv)[NLP], int (*gc)[NLP]) {
+    const int b = xcd_box(q, L.n);
+    const double* rb = rl + (long long)b * N3;
+#pragma unroll
+    for (int s = 0; s < PF; s++) plane_issue(rb, s, gv[s], gc[s]);
+    const double* u = boxp(L, 1, b);
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      const int q2 = tid + T * r;
+      if (q2 < TL::NST / 2) buf[r] = *reinterpret_cast<const v2d*>(u + 2 * q2);
+    }
+  };
+  int q = blockIdx.x;
+  if (q >= L.n) return;
+  issue(q, rv, rc);
+  for (; q < L.n; q += G) {
+    const int b = xcd_box(q, L.n);
+    double* __restrict__ u = boxp(L, 1, b);
+    const double* __restrict__ rb = rl + (long long)b * N3;
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      const int q2 = tid + T * r;
+      if (q2 < TL::NST / 2) {
+        P[scat[r] & 0xffff] = buf[r].x;
+        P[scat[r] >> 16] = buf[r].y;
+      }
+    }
+    if (q + G < L.n) issue(q + G, rvn, rcn);
+    __syncthreads();
+#pragma unroll 1
+    for (int p0 = 0; p0 < NPP; p0 += PF) {
+#pragma unroll
+      for (int s = 0; s < PF; s++) {
+        const int pl = p0 + s;
+        const int n = pl < NPL ? X.off[pl + 1] - X.off[pl] : 0;
+        Nbr7 st[NLP];
+        int w[NLP];
+#pragma unroll
+        for (int r = 0; r < NLP; r++) {
+          const int c = rc[s][r];
+          st[r].c = P[c];
+          st[r].xm = P[c - 1];
+          st[r].xp = P[c + 1];
+          st[r].ym = P[c - S];
+          st[r].yp = P[c + S];
+          st[r].zm = P[c - S * S];
+          st[r].zp = P[c + S * S];
+          w[r] = tid + T * r < n ? c : S * S * S + tid;
+        }
+        double nv[NLP];
+#pragma unroll
+        for (int r = 0; r < NLP; r++) nv[r] = gs_value<OP>(K, st[r], rv[s][r]);
+#pragma unroll
+        for (int r = 0; r < NLP; r++) P[w[r]] = nv[r];
+        plane_issue(rb, pl + PF, rv[s], rc[s]);
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NG2; r++) {
+      const int q2 = tid + T * r;
+      if (q2 >= HV) break;
+      v2d v;
+      v.x = P[gath[r] & 0xffff];
+      v.y = P[gath[r] >> 16];
+      *reinterpret_cast<v2d*>(u + 2 * q2) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PF; s++)
+#pragma unroll
+      for (int r = 0; r < NLP; r++) {
+        rv[s][r] = rvn[s][r];
+        rc[s][r] = rcn[s][r];
+      }
   }
 }
 
@@ -733,8 +933,39 @@ static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
   }
 }
 
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st) {
+#ifndef OMG_GS_TP16
+#define OMG_GS_TP16 256
+#endif
+bool gs_lex_plane_ok(int nc, int op) { return (nc == 16 || nc == 8) && (op == OP_LPL || op == OP_HELM); }
+
+void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st) {
   if (L.n == 0) return;
+  if (L.nc == 16)
+    k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
+  else
+    k_rhs_lex<8><<<L.n, 256, 0, st>>>(L, rl);
+}
+
+template <int OP>
+static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hipStream_t st) {
+  if (L.nc == 16) {
+    constexpr int T = OMG_GS_TP16;
+    k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
+  } else {
+    k_gs_lex_plane<OP, 8, 64, 4><<<gs_grid(L.n, 16), 64, 0, st>>>(L, lambda, rl);
+  }
+}
+
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl) {
+  if (L.n == 0) return;
+  if (rl) {
+    if (!gs_lex_plane_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no plane-order kernel for this level");
+    if (op == OP_HELM)
+      gs_lex_plane<OP_HELM>(L, lambda, rl, st);
+    else
+      gs_lex_plane<OP_LPL>(L, lambda, rl, st);
+    return;
+  }
   static const bool wg = getenv("OMG_GS_LEX_WG") != nullptr;
   if ((L.nc == 16 || L.nc == 8) && (op == OP_LPL || op == OP_HELM) && !wg) {
     // persistent, software-pipelined (k_gs_lex_wave); OMG_GS_LEX_WG: the
