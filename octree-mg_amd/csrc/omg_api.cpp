@@ -490,23 +490,6 @@ void phi_mean_ready(omg_ctx* c);
 double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
 
-// whether launch_gsrb_resident serves this level: one GPU's boxes only (no
-// face on another rank, no refinement boundary toward one), all resident at
-// once, box 16 or 8, Laplacian / Helmholtz; never inside a captured cycle, and
-// not under the loopback transport, whose ranks share one GPU and could each
-// hold part of the CUs their grid barriers wait for
-bool resident_level(omg_ctx* c, Level* L) {
-  if (c->no_resident || c->capturing || c->loop || !L->n || L->has_remote || (L->nc != 16 && L->nc != 8) ||
-      (c->op != OP_LPL && c->op != OP_HELM))
-    return false;
-  if (L->resident_ok < 0) {
-    bool ok = true;
-    for (int8_t k : L->h_nbk) ok = ok && k != NB_REMOTE && k != NB_RBREM;
-    L->resident_ok = ok && L->n <= gsrb_resident_capacity(L->nc, c->op, L->has_rb);
-  }
-  return L->resident_ok > 0;
-}
-
 // smooth_boxes (m_multigrid.f90:404-424)
 void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0) {
   Level* L = level_ptr(c, lvl);
@@ -522,7 +505,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // the compacted-plane kernel reads rhs from its plane-order copy, rebuilt
     // here when a write since the last build dropped it (update_coarse for
     // the levels below the top, every entry point that may change rhs)
-    const bool plane = L->n && n_sub >= 1 && L->d_rhs_lex && gs_lex_plane_ok(L->nc, c->op);
+    const bool plane = n_sub >= 1 && L->d_rhs_lex && gs_lex_plane_ok(L->nc, c->op);
     if (plane && !L->rhs_lex_ok) {
       Prof p(c, "rhs_lex", (double)L->n * L->nc * L->nc * L->nc, lvl);
       launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream);
@@ -537,15 +520,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     }
     return;
   }
-  // small levels: the substeps after the first in one launch (resident
-  // boxes, grid barrier between substeps); the first stays a plain substep
-  // when it absorbs a shift or the ghosts are not current (its fill follows)
-  int n_end = n_sub;
-  if (resident_level(c, L)) {
-    const int n_res = (absorb || !L->phi_gc_ok) ? first_substep + 1 : first_substep;
-    if (n_sub - n_res + 1 >= 2) n_end = n_res - 1;
-  }
-  for (int n = first_substep; n <= n_end; n++) {
+  for (int n = first_substep; n <= n_sub; n++) {
     // substep n updates the cells with i+j+k+n even, i.e. colour e = n mod 2,
     // and ends with the ghost fill; same-GPU neighbours only need colour e
     // when their ghost faces were consistent before the substep.
@@ -590,13 +565,6 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     finish_halo(c, L, 1);
     if (odd || !L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
   }
-  if (n_end < n_sub) {
-    Prof p(c, "smoother_gsrb", 0.5 * (n_sub - n_end) * L->n * L->nc * L->nc * L->nc, lvl);
-    if (!launch_gsrb_resident(L->view(), c->op, c->lambda, n_end + 1, n_sub, view_of(c, lvl - 1), L->d_rb,
-                              L->has_rb, bc_for(c, lvl, 1), c->d_gbar, c->stream))
-      throw OmgError("smooth_boxes: resident smoother not available for this level");
-    c->gbar_used = true;
-  }
 }
 
 bool tiled_level(omg_ctx* c, const Level* L) {
@@ -614,24 +582,6 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
-// The resident smoother's grid barrier waits a bounded time: a timeout (a
-// grid that was not resident at once) leaves a flag, reported here as an
-// error at the next read-back instead of a hang.
-void grid_barrier_verdict(omg_ctx* c, unsigned flag) {
-  c->gbar_used = false;
-  if (!flag) return;
-  HIPCHK(hipMemsetAsync(c->d_gbar, 0, 4 * sizeof(unsigned), c->stream));
-  throw OmgError("resident smoother: grid barrier timed out (workgroups not co-resident); set OMG_NO_RESIDENT=1");
-}
-void check_grid_barrier(omg_ctx* c) {
-  if (!c->gbar_used || c->capturing) return;
-  unsigned f = 0;
-  HIPCHK(hipMemcpyAsync(c->h_scalar + 3, c->d_gbar + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  f = *reinterpret_cast<const unsigned*>(c->h_scalar + 3);
-  grid_barrier_verdict(c, f);
-}
-
 // max over levels lo..hi of max_residual_lvl (m_multigrid.f90:296-311), this
 // rank only: the levels' maxima fold into one word on the device, read back
 // with one synchronisation
@@ -647,10 +597,7 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     c->max_deferred = true;
     return 0.0;
   }
-  const bool gbar = c->gbar_used;
-  if (gbar) HIPCHK(hipMemcpyAsync(c->h_scalar + 3, c->d_gbar + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (gbar) grid_barrier_verdict(c, *reinterpret_cast<const unsigned*>(c->h_scalar + 3));
   return c->h_scalar[0];
 }
 
@@ -1022,12 +969,15 @@ void drop_rhs_lex(omg_ctx* c) {
 }
 // plane-order rhs buffers for the levels the compacted-plane lexicographic
 // kernel serves (allocated outside any graph capture: tree setup, smoother
-// choice)
+// choice): 16^3 levels large enough that the sweep is bandwidth-bound; on
+// small levels the per-cycle copy costs more than it saves (C1: 0.255 ->
+// 0.293 ms with it on its 8^3 levels, profiles/r03/v7_README.txt)
+constexpr int kGsPlaneMinBoxes = 2048;
 void ensure_rhs_lex(omg_ctx* c) {
   if (c->host_only || c->smoother == OMG_SMOOTHER_GSRB || c->no_gs_plane) return;
   for (auto& kv : c->levels) {
     Level& L = kv.second;
-    if (L.d_rhs_lex || !L.n || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
+    if (L.d_rhs_lex || L.n < kGsPlaneMinBoxes || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
     L.rhs_lex_ok = false;
   }
@@ -2238,7 +2188,6 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
-    c->no_resident = env_flag("OMG_NO_RESIDENT");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only
@@ -2248,8 +2197,6 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMalloc(&c->d_maxslots, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
-    HIPCHK(hipMalloc(&c->d_gbar, 4 * sizeof(unsigned)));
-    HIPCHK(hipMemset(c->d_gbar, 0, 4 * sizeof(unsigned)));
     // (allocated here: no allocation may happen while a cycle is captured)
     HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
     c->h_tail = new TailArgs;
@@ -2311,7 +2258,6 @@ int omg_ctx_destroy(omg_ctx* c) {
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_maxslots);
-    dfree(c->d_gbar);
     for (auto& kv : c->graphs)
       if (kv.second) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -2733,7 +2679,6 @@ int omg_synchronize(omg_ctx* c) {
   return guarded([&] {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->stream2));
-    check_grid_barrier(c);
   });
 }
 

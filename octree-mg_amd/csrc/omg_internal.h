@@ -135,7 +135,6 @@ struct Level {
   double* d_scratch_rhs = nullptr;   // leaf sums of rhs for the next get_sum
   double* d_rhs_lex = nullptr;       // rhs in plane order for the lexicographic smoother (ensure_rhs_lex)
   bool rhs_lex_ok = false;           // d_rhs_lex equals rhs (dropped by every rhs writer)
-  int resident_ok = -1;              // resident_level(): -1 not yet decided
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
   int* d_int = nullptr;
   int n_bnd = 0, n_int = 0;
@@ -252,9 +251,6 @@ struct omg_ctx {
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
-  bool no_resident = false;            // OMG_NO_RESIDENT: small levels smoothed one launch per substep
-  unsigned* d_gbar = nullptr;          // grid barrier of the resident smoother: count, generation, timeout flag
-  bool gbar_used = false;
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

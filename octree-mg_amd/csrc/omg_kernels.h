@@ -44,12 +44,6 @@ void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs in plane order (launch_rhs_lex) for the compacted-plane kernel
 // (gs_lex_plane_ok levels); null: the line-per-thread kernels
-// all red-black substeps n_first..n_last of a small level in one launch (grid
-// barrier between substeps); false: not available for this level (size,
-// operator, occupancy), nothing launched
-bool launch_gsrb_resident(const LevelView& L, int op, double lambda, int n_first, int n_last, const LevelView& C,
-                          const RBRec* rb, bool has_rb, const GcBC& bc, unsigned* bar, hipStream_t st);
-int gsrb_resident_capacity(int nc, int op, bool has_rb);
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr);
 bool gs_lex_plane_ok(int nc, int op);
 void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st);

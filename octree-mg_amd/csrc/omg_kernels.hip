@@ -347,10 +347,12 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
 // fall outside the box, and each lane reads the rhs of its own line: 64 cache
 // lines per wave-instruction.  Here the cells of plane d = i+j+k are numbered
 // (k, then j, ascending) and thread t takes the t-th: a 16^3 plane has at most
-// 192 cells, one per thread of a 192-thread workgroup.  rhs is read from a
-// copy in that plane order (k_rhs_lex, built once per cycle per level), so
-// each plane's rhs is one contiguous run.  Same cells per plane, same
-// operands and gs_value: bit-identical.
+// 192 cells, so of a 256-thread workgroup (four waves; fewer threads spill the
+// next box's prefetch) only the waves that hold cells of the plane work on it.
+// rhs is read from a copy in that plane order (k_rhs_lex, rebuilt only after a
+// write of the level's rhs), so each plane's rhs is one contiguous run.  Same
+// cells per plane, same operands and gs_value: bit-identical.  Measured
+// 1190 -> 1100 us per 512^3 sweep (profiles/r03/v7_README.txt).
 template <int NC>
 struct LexPlanes {
   static constexpr int NPL = 3 * NC - 2, N3 = NC * NC * NC;
@@ -376,19 +378,39 @@ constexpr LexPlanes<NC> make_lex_planes() {
   P.off[LexPlanes<NC>::NPL] = (unsigned short)t;
   return P;
 }
+// 16^3 boxes only: the kernel pays off on large levels of 16^3 boxes
+// (gs_lex_plane_ok)
 constexpr LexPlanes<16> kLexPlanes16 = make_lex_planes<16>();
-constexpr LexPlanes<8> kLexPlanes8 = make_lex_planes<8>();
 static_assert(kLexPlanes16.off[LexPlanes<16>::NPL] == 4096 && kLexPlanes16.maxn == 192, "16^3 planes");
-static_assert(kLexPlanes8.off[LexPlanes<8>::NPL] == 512 && kLexPlanes8.maxn == 48, "8^3 planes");
 __constant__ LexPlanes<16> dLexPlanes16 = kLexPlanes16;
-__constant__ LexPlanes<8> dLexPlanes8 = kLexPlanes8;
 template <int NC>
 __device__ __forceinline__ const LexPlanes<NC>& lex_planes() {
-  if constexpr (NC == 16) return dLexPlanes16;
-  else return dLexPlanes8;
+  static_assert(NC == 16, "16^3 boxes");
+  return dLexPlanes16;
 }
 template <int NC>
-constexpr int lex_maxn() { return NC == 16 ? kLexPlanes16.maxn : kLexPlanes8.maxn; }
+constexpr int lex_maxn() { return kLexPlanes16.maxn; }
+// the size and the first cell of plane p = d - 3 in closed form (inclusion-
+// exclusion over the box's three extents), so the sweep computes them in
+// scalar registers instead of loading them: a load per plane would make every
+// plane wait for the whole prefetch queue (waits are in issue order)
+__host__ __device__ constexpr int lex_c2(int x) { return x >= 2 ? x * (x - 1) / 2 : 0; }
+__host__ __device__ constexpr int lex_c3(int x) { return x >= 3 ? x * (x - 1) * (x - 2) / 6 : 0; }
+template <int NC>
+__host__ __device__ constexpr int lex_plane_n(int p) {
+  return lex_c2(p + 2) - 3 * lex_c2(p - NC + 2) + 3 * lex_c2(p - 2 * NC + 2);
+}
+template <int NC>
+__host__ __device__ constexpr int lex_plane_off(int p) {
+  return lex_c3(p + 2) - 3 * lex_c3(p - NC + 2) + 3 * lex_c3(p - 2 * NC + 2);
+}
+template <int NC>
+constexpr bool lex_closed_form_ok(const LexPlanes<NC>& P) {
+  for (int p = 0; p < LexPlanes<NC>::NPL; p++)
+    if (lex_plane_off<NC>(p) != P.off[p] || lex_plane_n<NC>(p) != P.off[p + 1] - P.off[p]) return false;
+  return true;
+}
+static_assert(lex_closed_form_ok<16>(kLexPlanes16), "plane sizes");
 
 // rhs of every box in plane order: rl[b * NC^3 + t] = rhs at the t-th cell
 template <int NC>
@@ -419,7 +441,9 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lam
   __shared__ double P[gs_wave_lds<NC, T>()];
   const LexPlanes<NC>& X = lex_planes<NC>();
   const int tid = threadIdx.x, G = gridDim.x;
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);   // this wave's first thread
   const OpCoef<OP> K(L, lambda);
+  static_assert(NLP == 1 || T % 64 == 0, "wave-aligned slots");
   auto dense = [&](int q) {
     int i, j, k;
     if (q < 2 * HV) {
@@ -451,7 +475,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lam
   // plane pl's rhs and LDS cell of this thread's slots (clamped: past-the-end
   // slots and padding planes read a valid cell and update nothing)
   auto plane_issue = [&](const double* rb, int pl, double* ov, int* oc) {
-    const int p = min(pl, NPL - 1), o = X.off[p], n = X.off[p + 1] - o;
+    const int p = min(pl, NPL - 1), o = lex_plane_off<NC>(p), n = lex_plane_n<NC>(p);
 #pragma unroll
     for (int r = 0; r < NLP; r++) {
       const int idx = o + min(tid + T * r, n - 1);
@@ -496,26 +520,23 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lam
 #pragma unroll
       for (int s = 0; s < PF; s++) {
         const int pl = p0 + s;
-        const int n = pl < NPL ? X.off[pl + 1] - X.off[pl] : 0;
-        Nbr7 st[NLP];
-        int w[NLP];
+        const int n = pl < NPL ? lex_plane_n<NC>(pl) : 0;
 #pragma unroll
         for (int r = 0; r < NLP; r++) {
+          // waves past the plane's last cell skip it (a wave-uniform branch)
+          if (wbase + T * r >= n) continue;
           const int c = rc[s][r];
-          st[r].c = P[c];
-          st[r].xm = P[c - 1];
-          st[r].xp = P[c + 1];
-          st[r].ym = P[c - S];
-          st[r].yp = P[c + S];
-          st[r].zm = P[c - S * S];
-          st[r].zp = P[c + S * S];
-          w[r] = tid + T * r < n ? c : S * S * S + tid;
+          Nbr7 st;
+          st.c = P[c];
+          st.xm = P[c - 1];
+          st.xp = P[c + 1];
+          st.ym = P[c - S];
+          st.yp = P[c + S];
+          st.zm = P[c - S * S];
+          st.zp = P[c + S * S];
+          const double nv = gs_value<OP>(K, st, rv[s][r]);
+          P[tid + T * r < n ? c : S * S * S + tid] = nv;
         }
-        double nv[NLP];
-#pragma unroll
-        for (int r = 0; r < NLP; r++) nv[r] = gs_value<OP>(K, st[r], rv[s][r]);
-#pragma unroll
-        for (int r = 0; r < NLP; r++) P[w[r]] = nv[r];
         plane_issue(rb, pl + PF, rv[s], rc[s]);
         __syncthreads();
       }
@@ -936,24 +957,18 @@ static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
 #ifndef OMG_GS_TP16
 #define OMG_GS_TP16 256
 #endif
-bool gs_lex_plane_ok(int nc, int op) { return (nc == 16 || nc == 8) && (op == OP_LPL || op == OP_HELM); }
+bool gs_lex_plane_ok(int nc, int op) { return nc == 16 && (op == OP_LPL || op == OP_HELM); }
 
 void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st) {
   if (L.n == 0) return;
-  if (L.nc == 16)
-    k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
-  else
-    k_rhs_lex<8><<<L.n, 256, 0, st>>>(L, rl);
+  if (L.nc != 16) throw std::runtime_error("launch_rhs_lex: 16^3 boxes only");
+  k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
 }
 
 template <int OP>
 static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hipStream_t st) {
-  if (L.nc == 16) {
-    constexpr int T = OMG_GS_TP16;
-    k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
-  } else {
-    k_gs_lex_plane<OP, 8, 64, 4><<<gs_grid(L.n, 16), 64, 0, st>>>(L, lambda, rl);
-  }
+  constexpr int T = OMG_GS_TP16;
+  k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
 }
 
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl) {
