@@ -1303,10 +1303,13 @@ __device__ __forceinline__ TailBox tail_big_box(double* tl) {
 // per variable; edges and corners are zero in LDS and never written back).
 // Loads go in rounds of 8 per thread, all 8 issued before their LDS stores,
 // so each round costs one memory latency.
+#ifndef OMG_TAIL_IO_R
+#define OMG_TAIL_IO_R 8
+#endif
 template <bool LOAD>
 __device__ void tail_io_box(const LevelView& L, int nvar, double* dst) {
   const int S = L.nc + 2, S3 = S * S * S, n = nvar * S3;
-  constexpr int R = 8;
+  constexpr int R = OMG_TAIL_IO_R;
   for (int t0 = 0; t0 < n; t0 += R * kTailBS) {
     int go[R], tt[R];
     double v[R];
