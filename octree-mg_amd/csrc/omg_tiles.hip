@@ -1245,6 +1245,9 @@ struct TailBox {
   double *P, *F, *O, *R;   // phi, rhs, old, res
   double* B;               // bc value per face cell (6 nc^2)
   int nc, S;
+  int ln;                  // log2(nc): the per-cell index math uses shifts and masks
+                           // (nc is a power of two; division by a runtime value
+                           // costs tens of instructions per cell)
   __device__ __forceinline__ int at(int i, int j, int k) const { return i + S * (j + S * k); }
 };
 
@@ -1277,6 +1280,7 @@ __device__ __forceinline__ TailBox tail_box(const TailArgs& A, int li, double* t
   }
   X.nc = A.lv[li].L.nc;
   X.S = X.nc + 2;
+  X.ln = 31 - __clz(X.nc);
   const int s3 = X.S * X.S * X.S;
   X.P = tl + base;
   X.F = X.P + s3;
@@ -1290,6 +1294,7 @@ __device__ __forceinline__ TailBox tail_big_box(double* tl) {
   TailBox X;
   X.nc = 16;
   X.S = kTailBigS;
+  X.ln = 4;
   X.P = tl + kTailLdsDoubles + kTailLdsBcDoubles;
   X.F = X.P + kTailBigS3;
   X.O = X.R = nullptr;
@@ -1437,9 +1442,9 @@ __device__ void tail_big_resid_restrict(const TailArgs& A, int li, const TailBox
 // the opposite boundary layer (what the owner pushes), a physical face is
 // bc_to_gc's c0*bc + c1*x1 + c2*x2
 __device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
-  const int nc = X.nc, nc2 = nc * nc;
+  const int nc = X.nc, nc2 = nc * nc, ln = X.ln;
   for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
-    const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
+    const int nb = (p >> (2 * ln)) + 1, cell = p & (nc2 - 1), a = (cell & (nc - 1)) + 1, c = (cell >> ln) + 1;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, g = low ? 0 : nc + 1, x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
     auto cell_at = [&](int layer) {
@@ -1466,7 +1471,7 @@ __device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D
     for (int n = 1; n <= n_cycle; n++) {
       for (int d = 3; d <= 3 * nc; d++) {
         for (int p = threadIdx.x; p < nc * nc; p += blockDim.x) {
-          const int j = p % nc + 1, k = p / nc + 1, i = d - j - k;
+          const int j = (p & (nc - 1)) + 1, k = (p >> X.ln) + 1, i = d - j - k;
           if (i < 1 || i > nc) continue;
           const int c = X.at(i, j, k);
           X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
@@ -1482,7 +1487,7 @@ __device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D
     const int e = n & 1;
     // the cells of colour e only: i = 2*ih + 1 + p with (i+j+k) & 1 == e
     for (int q = threadIdx.x; q < n3 / 2; q += blockDim.x) {
-      const int ih = q % h, row = q / h, j = row % nc + 1, k = row / nc + 1;
+      const int ih = q & (h - 1), row = q >> (X.ln - 1), j = (row & (nc - 1)) + 1, k = (row >> X.ln) + 1;
       const int c = X.at(2 * ih + 1 + ((1 + j + k + e) & 1), j, k);
       X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
     }
@@ -1500,8 +1505,9 @@ __device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X,
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, n3 = nc * nc * nc;
   double mx = 0.0;
+  const int ln = X.ln;
   for (int q = threadIdx.x; q < n3; q += blockDim.x) {
-    const int c = X.at(q % nc + 1, (q / nc) % nc + 1, q / (nc * nc) + 1);
+    const int c = X.at((q & (nc - 1)) + 1, ((q >> ln) & (nc - 1)) + 1, (q >> (2 * ln)) + 1);
     const double r = X.F[c] - op_value<OP>(K, tail_nbr(X, X.P, c));
     X.R[c] = r;
     mx = amax(mx, fabs(r));
@@ -1518,9 +1524,10 @@ __device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X,
   if (Xc) {
     const int dp = A.lv[li].dixp[0];
     const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, hn = nc / 2;
+    const int lh = ln - 1;   // log2(hn)
     for (int t = threadIdx.x; t < 2 * hn * hn * hn; t += blockDim.x) {
-      const int pass = t / (hn * hn * hn), q = t % (hn * hn * hn);
-      const int i = q % hn + 1, j = (q / hn) % hn + 1, k = q / (hn * hn) + 1;
+      const int pass = t >> (3 * lh), q = t & (hn * hn * hn - 1);
+      const int i = (q & (hn - 1)) + 1, j = ((q >> lh) & (hn - 1)) + 1, k = (q >> (2 * lh)) + 1;
       const double* src = pass ? X.R : X.P;
       double acc = 0.0;
       for (int kk = 0; kk < 2; kk++)
@@ -1557,8 +1564,9 @@ __device__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& 
   __syncthreads();
   const int dp = A.lv[li].dixp[0];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, nc = X.nc, n3 = nc * nc * nc;
+  const int ln = X.ln;
   for (int q = threadIdx.x; q < n3; q += blockDim.x) {
-    const int i = q % nc + 1, j = (q / nc) % nc + 1, k = q / (nc * nc) + 1;
+    const int i = (q & (nc - 1)) + 1, j = ((q >> ln) & (nc - 1)) + 1, k = (q >> (2 * ln)) + 1;
     const int c0 = Xc.at(((i + 1) >> 1) + dx, ((j + 1) >> 1) + dy, ((k + 1) >> 1) + dz);
     const double f0 = 0.25 * Xc.R[c0];
     const double fx = 0.25 * Xc.R[(i & 1) ? c0 - 1 : c0 + 1];

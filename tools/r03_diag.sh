@@ -13,4 +13,4 @@ python3 $R/tools/trace_by_grid.py $f > $O/diag_trace_C4_by_grid.txt
 head -45 $O/diag_trace_C4_by_grid.txt
 cd $R
 bash tools/r03_tailtime.sh "C4 C3 C1" diag_tail || exit 1
-bash tools/r03_abn.sh "" "C4 C3 C1" diag_io24 OMG_LIB=octree-mg_amd/_variants/libomg_io24.so || exit 1
+bash tools/r03_abn.sh "c1_ or c4 or per or ref or u32 or helm32" "C4 C3 C1" diag_ab OMG_LIB=octree-mg_amd/_variants/libomg_io24.so OMG_LIB=octree-mg_amd/_variants/libomg_head.so || exit 1
