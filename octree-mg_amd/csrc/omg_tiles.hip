@@ -1302,45 +1302,91 @@ __device__ __forceinline__ TailBox tail_big_box(double* tl) {
   return X;
 }
 
-// One box variable set of the LDS-resident tail, HBM <-> LDS: nvar
-// variables (1 = phi, 2 = rhs, ...) of the single box of level L, interior
-// and face ghosts, to / from the plain (nc+2)^3 arrays at dst (consecutive
-// per variable; edges and corners are zero in LDS and never written back).
-// Loads go in rounds of 8 per thread, all 8 issued before their LDS stores,
-// so each round costs one memory latency.
-#ifndef OMG_TAIL_IO_R
-#define OMG_TAIL_IO_R 8
-#endif
-template <bool LOAD>
-__device__ void tail_io_box(const LevelView& L, int nvar, double* dst) {
-  const int S = L.nc + 2, S3 = S * S * S, n = nvar * S3;
-  constexpr int R = OMG_TAIL_IO_R;
-  for (int t0 = 0; t0 < n; t0 += R * kTailBS) {
-    int go[R], tt[R];
-    double v[R];
+// One box variable set of the LDS-resident tail, HBM <-> LDS: NV variables
+// (1 = phi, 2 = rhs, ...) of the single box of level L, interior and face
+// ghosts, to / from the plain (NC+2)^3 arrays at dst (consecutive per
+// variable).  The stored box is contiguous per variable (omg_device.h), so
+// each thread moves whole 16-B pairs: all loads of the box are issued at once
+// (one memory latency) and scattered to their plain positions in LDS; the
+// edges and corners, which the device does not store, are zeroed in LDS and
+// never written back.
+template <int NC>
+__device__ __forceinline__ int stored_dense(int q) {
+  using TL = Tl<NC>;
+  constexpr int S = NC + 2, H = TL::H, HV = TL::HV, FS = TL::FS;
+  int i, j, k;
+  if (q < 2 * HV) {
+    TL::decode(q, i, j, k);
+  } else {
+    const int r0 = q - 2 * HV, nb = r0 / FS + 1, r1 = r0 % FS;
+    const int e = r1 >= H * NC, r = r1 - e * H * NC, ah = r % H, c = r / H + 1;
+    const int g = (nb & 1) ? 0 : NC + 1;
+    const int a = 2 * ah + 1 + ((1 + g + c + e) & 1);
+    const int d = (nb + 1) >> 1;
+    if (d == 1) { i = g; j = a; k = c; }
+    else if (d == 2) { i = a; j = g; k = c; }
+    else { i = a; j = c; k = g; }
+  }
+  return i + S * (j + S * k);
+}
+
+template <int NC, int NV, bool LOAD>
+__device__ void tail_io_stored(const LevelView& L, double* dst) {
+  constexpr int S = NC + 2, S3 = S * S * S, NP = Tl<NC>::NST / 2, N = NV * NP;
+  constexpr int R = (N + kTailBS - 1) / kTailBS;
+  const int tid = threadIdx.x;
+  if (LOAD) {
+    // edges and corners: 12 edges of NC cells and 8 corners per variable
+    constexpr int NE = 12 * NC + 8;
+    for (int t = tid; t < NV * NE; t += kTailBS) {
+      const int var = t / NE, e = t % NE;
+      int x, y, z;
+      if (e < 12 * NC) {
+        const int ax = e / (4 * NC), w = e % (4 * NC), m = w / NC, a = w % NC + 1;
+        const int u = (m & 1) ? S - 1 : 0, v = (m & 2) ? S - 1 : 0;
+        if (ax == 0) { x = a; y = u; z = v; }
+        else if (ax == 1) { x = u; y = a; z = v; }
+        else { x = u; y = v; z = a; }
+      } else {
+        const int m = e - 12 * NC;
+        x = (m & 1) ? S - 1 : 0; y = (m & 2) ? S - 1 : 0; z = (m & 4) ? S - 1 : 0;
+      }
+      dst[var * S3 + x + S * (y + S * z)] = 0.0;
+    }
+    v2d v[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      const int t = t0 + threadIdx.x + kTailBS * r;
-      go[r] = -1;
-      tt[r] = t < n ? t : -1;
-      if (t >= n) continue;
-      const int var = t / S3, q = t % S3;
-      const int i = q % S, j = (q / S) % S, k = q / (S * S);
-      const int nbnd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
-      if (nbnd >= 2) continue;
-      go[r] = (int)(boxp(L, var + 1, 0) - L.data) + off_cell(L, i, j, k);
+      const int t = tid + kTailBS * r;
+      if (t < N) v[r] = reinterpret_cast<const v2d*>(boxp(L, t / NP + 1, 0))[t % NP];
     }
-    if (LOAD) {
 #pragma unroll
-      for (int r = 0; r < R; r++) v[r] = go[r] >= 0 ? L.data[go[r]] : 0.0;
-#pragma unroll
-      for (int r = 0; r < R; r++)
-        if (tt[r] >= 0) dst[tt[r]] = v[r];
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; r++)
-        if (go[r] >= 0) L.data[go[r]] = dst[tt[r]];
+    for (int r = 0; r < R; r++) {
+      const int t = tid + kTailBS * r;
+      if (t >= N) continue;
+      const int var = t / NP, p = t % NP;
+      dst[var * S3 + stored_dense<NC>(2 * p)] = v[r].x;
+      dst[var * S3 + stored_dense<NC>(2 * p + 1)] = v[r].y;
     }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int t = tid + kTailBS * r;
+      if (t >= N) continue;
+      const int var = t / NP, p = t % NP;
+      v2d x;
+      x.x = dst[var * S3 + stored_dense<NC>(2 * p)];
+      x.y = dst[var * S3 + stored_dense<NC>(2 * p + 1)];
+      reinterpret_cast<v2d*>(boxp(L, var + 1, 0))[p] = x;
+    }
+  }
+}
+
+template <bool LOAD>
+__device__ void tail_io_box(const LevelView& L, double* dst) {   // the LDS levels: all four variables
+  switch (L.nc) {
+    case 8: tail_io_stored<8, 4, LOAD>(L, dst); break;
+    case 4: tail_io_stored<4, 4, LOAD>(L, dst); break;
+    default: tail_io_stored<2, 4, LOAD>(L, dst); break;
   }
 }
 
@@ -1350,7 +1396,7 @@ __device__ void tail_boxes_io(const TailArgs& A, int ls, double* tl) {
   int base = 0;
   for (int l = 0; l <= ls; l++) {
     const LevelView& L = A.lv[l].L;
-    tail_io_box<LOAD>(L, 4, tl + base);
+    tail_io_box<LOAD>(L, tl + base);
     const int S = L.nc + 2;
     base += 4 * S * S * S;
   }
@@ -1405,7 +1451,10 @@ __device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailL
 // only phi goes back
 template <bool LOAD>
 __device__ void tail_big_io(const LevelView& L, const TailBox& X) {
-  tail_io_box<LOAD>(L, LOAD ? 2 : 1, X.P);
+  if (LOAD)
+    tail_io_stored<16, 2, true>(L, X.P);
+  else
+    tail_io_stored<16, 1, false>(L, X.P);
   __syncthreads();
 }
 
