@@ -1490,7 +1490,36 @@ __device__ void tail_big_resid_restrict(const TailArgs& A, int li, const TailBox
 // mg_fill_ghost_cells_lvl of phi for the box in LDS: a periodic face copies
 // the opposite boundary layer (what the owner pushes), a physical face is
 // bc_to_gc's c0*bc + c1*x1 + c2*x2
+template <int NC>
+__device__ __forceinline__ void tail_lds_fill_nc(const TailLdsLevel& D, const TailBox& X) {
+  constexpr int S = NC + 2, NF = 6 * NC * NC, R = (NF + kTailBS - 1) / kTailBS;
+  int gd[R];
+  double v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {   // every face cell's reads first, then the ghost writes
+    const int p = threadIdx.x + kTailBS * r;
+    if (p >= NF) continue;
+    const int nb = p / (NC * NC) + 1, cell = p % (NC * NC), a = cell % NC + 1, c = cell / NC + 1;
+    const bool low = nb & 1;
+    const int d = (nb + 1) >> 1, g = low ? 0 : NC + 1, x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
+    auto cell_at = [&](int layer) {
+      return d == 1 ? layer + S * (a + S * c) : d == 2 ? a + S * (layer + S * c) : a + S * (c + S * layer);
+    };
+    gd[r] = cell_at(g);
+    if (D.local[nb - 1])
+      v[r] = X.P[cell_at(low ? NC : 1)];
+    else
+      v[r] = D.c0[nb - 1] * X.B[p] + D.c1[nb - 1] * X.P[cell_at(x1)] + D.c2[nb - 1] * X.P[cell_at(x2)];
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (threadIdx.x + kTailBS * r < NF) X.P[gd[r]] = v[r];
+  __syncthreads();
+}
+
 __device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
+  // ghosts are written only from interior cells, so the reads may precede the writes
+  if (X.nc == 16) return tail_lds_fill_nc<16>(D, X);
   const int nc = X.nc, nc2 = nc * nc, ln = X.ln;
   for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
     const int nb = (p >> (2 * ln)) + 1, cell = p & (nc2 - 1), a = (cell & (nc - 1)) + 1, c = (cell >> ln) + 1;
@@ -1508,6 +1537,29 @@ __device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
   __syncthreads();
 }
 
+
+// one red-black substep (colour e) of an NC^3 box in LDS: the cells of colour
+// e only, i = 2*ih + 1 + p with (i+j+k) & 1 == e; colour e reads colour 1-e
+// only (gs_value has no centre term), so all reads may precede the updates
+template <int NC, int OP>
+__device__ __forceinline__ void tail_rb_substep(const OpCoef<OP>& K, const TailBox& X, int e) {
+  constexpr int S = NC + 2, H = NC / 2, NQ = NC * NC * NC / 2, R = (NQ + kTailBS - 1) / kTailBS;
+  int cc[R];
+  Nbr7 st[R];
+  double f[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int q = threadIdx.x + kTailBS * r;
+    if (q >= NQ) continue;
+    const int ih = q % H, row = q / H, j = row % NC + 1, k = row / NC + 1;
+    cc[r] = 2 * ih + 1 + ((1 + j + k + e) & 1) + S * (j + S * k);
+    st[r] = tail_nbr(X, X.P, cc[r]);
+    f[r] = X.F[cc[r]];
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (threadIdx.x + kTailBS * r < NQ) X.P[cc[r]] = gs_value<OP>(K, st[r], f[r]);
+}
 
 // smooth_boxes: red-black substeps (colour e = n & 1 for n = 1 .. 2 n_cycle)
 // or lexicographic sweeps (hyperplanes i+j+k = d, as gs_lex_box), each
@@ -1534,6 +1586,13 @@ __device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D
   const int h = nc / 2;
   for (int n = 1; n <= 2 * n_cycle; n++) {
     const int e = n & 1;
+    if (nc == 16) {   // the box size known at compile time: every read of a
+                      // thread's cells issued before its first update
+      tail_rb_substep<16, OP>(K, X, e);
+      __syncthreads();
+      tail_lds_fill(D, X);
+      continue;
+    }
     // the cells of colour e only: i = 2*ih + 1 + p with (i+j+k) & 1 == e
     for (int q = threadIdx.x; q < n3 / 2; q += blockDim.x) {
       const int ih = q & (h - 1), row = q >> (X.ln - 1), j = (row & (nc - 1)) + 1, k = (row >> X.ln) + 1;
@@ -1606,8 +1665,46 @@ __device__ void tail_lds_coarse_rhs(const TailArgs& A, int li, const TailBox& X)
 
 // correct_children of the parent Xc (res = phi - old over its stored cells)
 // + mg_prolong_sparse onto the box + the ghost fill
+template <int NC>
+__device__ __forceinline__ void tail_correct_nc(const TailArgs& A, int li, const TailBox& X, const TailBox& Xc) {
+  constexpr int S = NC + 2, SC = NC / 2 + 2, SC3 = SC * SC * SC, N3 = NC * NC * NC;
+  constexpr int R = (N3 + kTailBS - 1) / kTailBS, RC = (SC3 + kTailBS - 1) / kTailBS;
+#pragma unroll
+  for (int r = 0; r < RC; r++) {
+    const int q = threadIdx.x + kTailBS * r;
+    if (q < SC3) Xc.R[q] = Xc.P[q] - Xc.O[q];
+  }
+  __syncthreads();
+  const int dp = A.lv[li].dixp[0];
+  const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
+  int cc[R];
+  double nv[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int q = threadIdx.x + kTailBS * r;
+    if (q >= N3) continue;
+    const int i = q % NC + 1, j = (q / NC) % NC + 1, k = q / (NC * NC) + 1;
+    const int c0 = (((i + 1) >> 1) + dx) + SC * ((((j + 1) >> 1) + dy) + SC * (((k + 1) >> 1) + dz));
+    const double f0 = 0.25 * Xc.R[c0];
+    const double fx = 0.25 * Xc.R[(i & 1) ? c0 - 1 : c0 + 1];
+    const double fy = 0.25 * Xc.R[(j & 1) ? c0 - SC : c0 + SC];
+    const double fz = 0.25 * Xc.R[(k & 1) ? c0 - SC * SC : c0 + SC * SC];
+    cc[r] = i + S * (j + S * k);
+    nv[r] = X.P[cc[r]] + (f0 + fx + fy + fz);
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (threadIdx.x + kTailBS * r < N3) X.P[cc[r]] = nv[r];
+  __syncthreads();
+}
+
 __device__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
                                  const TailBox& Xc) {
+  if (X.nc == 16 && Xc.S == 10) {   // the 16^3 level, a one-box parent of half the size
+    tail_correct_nc<16>(A, li, X, Xc);
+    tail_lds_fill(D, X);
+    return;
+  }
   const int sc3 = Xc.S * Xc.S * Xc.S;
   for (int q = threadIdx.x; q < sc3; q += blockDim.x) Xc.R[q] = Xc.P[q] - Xc.O[q];
   __syncthreads();
