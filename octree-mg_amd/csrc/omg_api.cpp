@@ -508,13 +508,13 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     const bool plane = n_sub >= 1 && L->d_rhs_lex && gs_lex_plane_ok(L->nc, c->op);
     if (plane && !L->rhs_lex_ok) {
       Prof p(c, "rhs_lex", (double)L->n * L->nc * L->nc * L->nc, lvl);
-      launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream);
+      launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream, !c->gs_lex_plane);
       L->rhs_lex_ok = true;
     }
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr, !c->gs_lex_plane);
       }
       fill_gc_lvl(c, lvl, 1);
     }
@@ -2188,6 +2188,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
+    c->gs_lex_plane = env_flag("OMG_GS_LEX_PLANE");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only

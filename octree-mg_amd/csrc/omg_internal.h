@@ -251,6 +251,7 @@ struct omg_ctx {
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
+  bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

@@ -42,11 +42,14 @@ inline bool gs_tiled(int nc, int op, bool has_rb) {
 }
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
-// rl: rhs in plane order (launch_rhs_lex) for the compacted-plane kernel
-// (gs_lex_plane_ok levels); null: the line-per-thread kernels
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr);
+// rl: rhs copy (launch_rhs_lex) for the register-ring kernel (reg) or the
+// compacted-plane kernel, on gs_lex_plane_ok levels; null: the
+// line-per-thread kernels
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr,
+                   bool reg = true);
 bool gs_lex_plane_ok(int nc, int op);
-void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st);
+// the copy in ring order (reg) or in plane order
+void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg = true);
 void launch_box_op(const LevelView& L, int op, double lambda, int i_out, hipStream_t st);
 void launch_residual(const LevelView& L, int op, double lambda, unsigned long long* maxbits,
                      hipStream_t st);

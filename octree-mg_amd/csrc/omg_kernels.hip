@@ -561,6 +561,212 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lam
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lexicographic GS with the box in registers (round 3).  The plane kernels
+// above keep the box in LDS (46.6 KB: three boxes per CU) and pay a workgroup
+// barrier per hyperplane; their sweep is latency-bound at 36 % of HBM.
+//
+// Here one wave sweeps one 16^3 box.  Lane l owns the four x-lines
+// (j, k) = (l % 16 + 1, 4 (l / 16) + r + 1), r = 0..3, and keeps each line's
+// 18 cells (interior i = 1..16 and the two x ghosts) in a ring of registers:
+// cell i of line (j, k) in slot (i + j + k) mod 18.  Step t updates cell
+// i = t - j - k of every line, i.e. the hyperplane i + j + k = t.  In the
+// skewed ring every operand of step t sits in a slot that is the same for all
+// lanes and lines:
+//   xm, and the y-/z-lower neighbours' cell i: slot t - 1 (updated at t - 1),
+//   xp, and the y-/z-upper neighbours' cell i: slot t + 1 (not yet updated),
+// so the unrolled sweep indexes registers statically.  The y neighbours are
+// the lanes beside this one in its 16-lane row (DPP row shifts; the lanes at
+// the row ends keep the y ghost, read from LDS, as the shift's old value), the
+// z neighbours the lane's own next line or, across lane groups, the lane 16
+// away (ds_bpermute), with the z ghosts at the box faces.  No LDS traffic for
+// phi and no barrier per step: the box passes through LDS only to be rotated
+// into and out of the ring (18 KB per box, so 8 boxes share a CU).  rhs comes
+// from a copy in the ring's order (k_rhs_reg, rebuilt after rhs writes like
+// the plane-order copy): the step-t values of all 256 lines are one
+// contiguous 2 KB run, prefetched PF steps ahead.  Every cell is updated
+// after its lower neighbours and before its upper ones, with the same
+// operands and gs_value as the reference's i-fastest loop: bit-identical.
+constexpr int kLexRing = 18;                       // interior + 2 x ghosts per line
+constexpr int kLexGPad = 16;                       // slack around each y/z ghost face in LDS
+constexpr int kLexGFace = 256 + 2 * kLexGPad;
+
+// value of the lane one below / above in this lane's 16-lane row; the first /
+// last lane of the row keeps `old` (row_shr:1 / row_shl:1, bound_ctrl off)
+__device__ __forceinline__ double dpp_row_prev(double v, double old) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x111, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x111, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_row_next(double v, double old) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x101, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x101, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// rhs of every 16^3 box in ring order: rl[b*4096 + ((i+j+k) & 15)*256 + r*64 + l]
+// for cell (i, j, k) of lane l = (j-1) + 16*((k-1)/4), line r = (k-1) % 4;
+// a bijection (each line has one cell per value of (i+j+k) mod 16)
+__global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict__ rl) {
+  using TL = Tl<16>;
+  __shared__ double F[4096];
+  const int b = blockIdx.x;
+  const v2d* f = reinterpret_cast<const v2d*>(boxp(L, 2, b));
+  for (int q = threadIdx.x; q < 2048; q += blockDim.x) reinterpret_cast<v2d*>(F)[q] = f[q];
+  __syncthreads();
+  double* o = rl + (long long)b * 4096;
+  for (int d = threadIdx.x; d < 4096; d += blockDim.x) {
+    const int s = d >> 8, r = (d >> 6) & 3, l = d & 63;
+    const int j = (l & 15) + 1, k = 4 * (l >> 4) + r + 1, i = ((s - j - k - 1) & 15) + 1;
+    o[d] = F[TL::oint(i, j, k)];
+  }
+}
+
+#ifndef OMG_GS_REG_WPS
+#define OMG_GS_REG_WPS 2
+#endif
+template <int OP, int PF>
+__global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl) {
+  constexpr int NC = 16, H = 8, HV = 2048, FH = 128, FS = 256, R = kLexRing, T0 = 3, T1 = 3 * NC;
+  static_assert(R % PF == 0, "the rhs ring index must repeat with the register ring");
+  __shared__ double stage[R * 64];          // one line of every lane, slot-major
+  __shared__ double G[4 * kLexGFace];       // y/z ghost faces, plain [c][a] with slack
+  const int l = threadIdx.x, kq = l >> 4, j = (l & 15) + 1;
+  const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
+  double* __restrict__ u = boxp(L, 1, b);
+  const double* __restrict__ rb = rl + (long long)b * (NC * NC * NC);
+  const OpCoef<OP> K(L, lambda);
+
+  // y/z ghost faces (nb = 3..6: j = 0, j = 17, k = 0, k = 17; tangential
+  // (a, c) = (i, k) or (i, j)) into G[f][c-1][a-1]
+  {
+    const double* gf = u + 2 * HV + 2 * FS;
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+      const int q = l + 64 * n;                      // double pair of faces 3..6
+      const v2d x = ld_nt(gf + 2 * q);
+      const int f = q >> 7, r1 = (2 * q) & (FS - 1);
+      const int e = r1 >= FH, rr = r1 - e * FH, ah = rr % H, c = rr / H + 1;
+      const int g = (f & 1) ? NC + 1 : 0;            // f = nb - 3: even f is a low face
+      const int a = 2 * ah + 1 + ((1 + g + c + e) & 1);
+      double* gp = G + f * kLexGFace + kLexGPad + NC * (c - 1) + (a - 1);
+      gp[0] = x.x;
+      gp[2] = x.y;
+    }
+  }
+
+  // the ring: interior planes k = 4 kq' + r + 1 (both colours) and the x
+  // ghosts of line r go through `stage` in slot-major order
+  double ring[4][R];
+  const int jr = (l >> 2) + 1, ihr = 2 * (l & 3);    // row / first colour index of this lane's loads
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    v2d buf[8];
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+      const int k = 4 * (n >> 1) + r + 1, e = n & 1;
+      buf[n] = ld_nt(u + e * HV + FH * (k - 1) + 2 * l);
+    }
+    const int kr = 4 * kq + r + 1;
+    const double gx0 = u[2 * HV + ((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
+    const double gx1 = u[2 * HV + FS + ((NC + 1 + j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
+    __syncthreads();                                 // the previous line's reads of stage are done
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+      const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
+      const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
+      const int ln = (jr - 1) + 16 * kq2;
+      stage[((i + jr + k) % R) * 64 + ln] = buf[n].x;
+      stage[((i + 2 + jr + k) % R) * 64 + ln] = buf[n].y;
+    }
+    stage[((j + kr) % R) * 64 + l] = gx0;
+    stage[((NC + 1 + j + kr) % R) * 64 + l] = gx1;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < R; s++) ring[r][s] = stage[s * 64 + l];
+  }
+
+  // per line: j + k; G index of the y ghost at step 0 (lanes of the low half
+  // of the row read face j = 0 as lane j = 1 needs it, the others face j = 17
+  // as lane j = 16 needs it; the slack keeps every step's index inside G)
+  const int jk0 = j + 4 * kq + 1;                   // line r: jk0 + r
+  const int gy0 = (j <= 8 ? kLexGPad - 18 : kLexGFace + kLexGPad - 33) + 15 * (4 * kq + 1);   // line r: + 15 r
+  // z ghosts: lanes of group 0 (line 0, k = 1) read face k = 0, group 3
+  // (line 3, k = 16) face k = 17
+  const int gz = kq < 2 ? 2 * kLexGFace + kLexGPad + 15 * j - 18 : 3 * kLexGFace + kLexGPad + 15 * j - 33;
+  const int lane_lo = (l + 48) & 63, lane_hi = (l + 16) & 63;
+
+  double rf[PF][4];
+#pragma unroll
+  for (int p = 0; p < PF; p++)
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      rf[(T0 + p) % PF][r] = __builtin_nontemporal_load(rb + ((T0 + p) & 15) * 256 + r * 64 + l);
+
+#pragma unroll 1
+  for (int m = 0; m < 3; m++) {
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int t = R * m + s;
+      if (t < T0 || t > T1) continue;                 // wave-uniform
+      const int sm = (s + R - 1) % R, sp = (s + 1) % R;
+      double gv[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) gv[r] = G[gy0 + 15 * r + t];
+      const double gzv = G[gz + t];
+      const double zlo_n = __shfl(ring[3][sm], lane_lo, 64);
+      const double zhi_n = __shfl(ring[0][sp], lane_hi, 64);
+      const double zlo = kq == 0 ? gzv : zlo_n;
+      const double zhi = kq == 3 ? gzv : zhi_n;
+      double nv[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        Nbr7 st;
+        st.c = ring[r][s];
+        st.xm = ring[r][sm];
+        st.xp = ring[r][sp];
+        st.ym = dpp_row_prev(ring[r][sm], gv[r]);
+        st.yp = dpp_row_next(ring[r][sp], gv[r]);
+        st.zm = r > 0 ? ring[r - 1][sm] : zlo;
+        st.zp = r < 3 ? ring[r + 1][sp] : zhi;
+        nv[r] = gs_value<OP>(K, st, rf[s % PF][r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        if ((unsigned)(t - jk0 - r - 1) < (unsigned)NC) ring[r][s] = nv[r];
+      // unconditional (past the last step it reads this box's copy again,
+      // unused): a conditional load would be waited for at once
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        rf[s % PF][r] = __builtin_nontemporal_load(rb + ((t + PF) & 15) * 256 + r * 64 + l);
+      // keep the scheduler from interleaving steps (that raises the register
+      // pressure past the ring's budget)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // the interior back, through stage in the stored order (the box pointer
+  // made opaque: otherwise the store addresses are shared with the loads'
+  // and held across the sweep, which spills)
+  double* ub = u;
+  asm volatile("" : "+s"(ub));
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < R; s++) stage[s * 64 + l] = ring[r][s];
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+      const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
+      const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
+      const int ln = (jr - 1) + 16 * kq2;
+      st_nt(ub + e * HV + FH * (k - 1) + 2 * l, stage[((i + jr + k) % R) * 64 + ln],
+            stage[((i + 2 + jr + k) % R) * 64 + ln]);
+    }
+  }
+}
+
 template <int OP>
 __device__ __forceinline__ double apply_op(const LevelView& L, const OpCoef<OP>& K, int b, int i, int j,
                                            int k) {
@@ -959,11 +1165,18 @@ static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
 #endif
 bool gs_lex_plane_ok(int nc, int op) { return nc == 16 && (op == OP_LPL || op == OP_HELM); }
 
-void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st) {
+void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg) {
   if (L.n == 0) return;
   if (L.nc != 16) throw std::runtime_error("launch_rhs_lex: 16^3 boxes only");
-  k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
+  if (reg)
+    k_rhs_reg<<<L.n, 256, 0, st>>>(L, rl);
+  else
+    k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
 }
+
+#ifndef OMG_GS_REG_PF
+#define OMG_GS_REG_PF 3
+#endif
 
 template <int OP>
 static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hipStream_t st) {
@@ -971,10 +1184,18 @@ static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hi
   k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
 }
 
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl) {
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg) {
   if (L.n == 0) return;
   if (rl) {
     if (!gs_lex_plane_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no plane-order kernel for this level");
+    if (reg) {
+      // one wave per box, one box per workgroup (8 per CU by their LDS)
+      if (op == OP_HELM)
+        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl);
+      else
+        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl);
+      return;
+    }
     if (op == OP_HELM)
       gs_lex_plane<OP_HELM>(L, lambda, rl, st);
     else

@@ -1,10 +1,12 @@
-"""Lexicographic GS over compacted hyperplanes (k_gs_lex_plane), bit for bit
-against the C oracle on every stored cell.  The kernel reads rhs from a
-plane-order copy, so the copy must follow every change of rhs: between
-cycles through the API, and inside a cycle (update_coarse rewrites the rhs of
-the levels below).  It serves 16^3 levels of at least 2048 boxes, hence the
-256^3 cases; OMG_NO_GS_PLANE=1 (read when a context is created) gives the
-line-per-thread kernel, which must agree as well."""
+"""Lexicographic GS with the box in a register ring (k_gs_lex_reg) and over
+compacted hyperplanes (k_gs_lex_plane), bit for bit against the C oracle on
+every stored cell.  Both read rhs from a copy (ring order / plane order), so
+the copy must follow every change of rhs: between cycles through the API, and
+inside a cycle (update_coarse rewrites the rhs of the levels below).  They
+serve 16^3 levels of at least 2048 boxes, hence the 256^3 cases;
+OMG_GS_LEX_PLANE=1 selects the plane kernel and OMG_NO_GS_PLANE=1 the
+line-per-thread kernel (both read when a context is created), which must
+agree as well."""
 import numpy as np
 import pytest
 
@@ -30,7 +32,7 @@ GS_CASES = ["16 256 256 256 1 v gs lpl 0 d0 sol 1 lb 0",
             "16 64 64 64 2 v gs lpl 0 d0 sol 1 lb 0"]
 
 
-@pytest.mark.parametrize("env", [(), ("OMG_NO_GS_PLANE",)], ids=["plane", "lines"])
+@pytest.mark.parametrize("env", [(), ("OMG_GS_LEX_PLANE",), ("OMG_NO_GS_PLANE",)], ids=["ring", "plane", "lines"])
 @pytest.mark.parametrize("args", GS_CASES)
 def test_gs_rhs_changes_between_cycles(args, env, monkeypatch):
     """V-cycles, then a new rhs on the finest level (upload) and on a level
