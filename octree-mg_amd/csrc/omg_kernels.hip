@@ -625,11 +625,19 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
 #ifndef OMG_GS_REG_WPS
 #define OMG_GS_REG_WPS 2
 #endif
+// timing-only (wrong results): 1 = no sweep (rotation in and out only),
+// 2 = no phi loads or stores (the sweep on whatever LDS holds)
+#ifndef OMG_T_RING
+#define OMG_T_RING 0
+#endif
 template <int OP, int PF>
 __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl) {
   constexpr int NC = 16, H = 8, HV = 2048, FH = 128, FS = 256, R = kLexRing, T0 = 3, T1 = 3 * NC;
   static_assert(R % PF == 0, "the rhs ring index must repeat with the register ring");
-  __shared__ double stage[R * 64];          // one line of every lane, slot-major
+  // stage rows of 65 doubles: the four lanes that scatter one row's cells
+  // into different slots then hit different banks
+  constexpr int SR = 65;
+  __shared__ double stage[R * SR];          // one line of every lane, slot-major
   __shared__ double G[4 * kLexGFace];       // y/z ghost faces, plain [c][a] with slack
   const int l = threadIdx.x, kq = l >> 4, j = (l & 15) + 1;
   const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
@@ -665,7 +673,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
 #pragma unroll
     for (int n = 0; n < 8; n++) {
       const int k = 4 * (n >> 1) + r + 1, e = n & 1;
-      buf[n] = ld_nt(u + e * HV + FH * (k - 1) + 2 * l);
+      buf[n] = OMG_T_RING == 2 ? v2d{0.0, 0.0} : ld_nt(u + e * HV + FH * (k - 1) + 2 * l);
     }
     const int kr = 4 * kq + r + 1;
     const double gx0 = u[2 * HV + ((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
@@ -676,14 +684,14 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
       const int ln = (jr - 1) + 16 * kq2;
-      stage[((i + jr + k) % R) * 64 + ln] = buf[n].x;
-      stage[((i + 2 + jr + k) % R) * 64 + ln] = buf[n].y;
+      stage[((i + jr + k) % R) * SR + ln] = buf[n].x;
+      stage[((i + 2 + jr + k) % R) * SR + ln] = buf[n].y;
     }
-    stage[((j + kr) % R) * 64 + l] = gx0;
-    stage[((NC + 1 + j + kr) % R) * 64 + l] = gx1;
+    stage[((j + kr) % R) * SR + l] = gx0;
+    stage[((NC + 1 + j + kr) % R) * SR + l] = gx1;
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < R; s++) ring[r][s] = stage[s * 64 + l];
+    for (int s = 0; s < R; s++) ring[r][s] = stage[s * SR + l];
   }
 
   // per line: j + k; G index of the y ghost at step 0 (lanes of the low half
@@ -704,7 +712,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       rf[(T0 + p) % PF][r] = __builtin_nontemporal_load(rb + ((T0 + p) & 15) * 256 + r * 64 + l);
 
 #pragma unroll 1
-  for (int m = 0; m < 3; m++) {
+  for (int m = 0; m < 3 && OMG_T_RING != 1; m++) {
 #pragma unroll
     for (int s = 0; s < R; s++) {
       const int t = R * m + s;
@@ -754,15 +762,16 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   for (int r = 0; r < 4; r++) {
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < R; s++) stage[s * 64 + l] = ring[r][s];
+    for (int s = 0; s < R; s++) stage[s * SR + l] = ring[r][s];
     __syncthreads();
 #pragma unroll
     for (int n = 0; n < 8; n++) {
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
       const int ln = (jr - 1) + 16 * kq2;
-      st_nt(ub + e * HV + FH * (k - 1) + 2 * l, stage[((i + jr + k) % R) * 64 + ln],
-            stage[((i + 2 + jr + k) % R) * 64 + ln]);
+      if (OMG_T_RING != 2)
+        st_nt(ub + e * HV + FH * (k - 1) + 2 * l, stage[((i + jr + k) % R) * SR + ln],
+              stage[((i + 2 + jr + k) % R) * SR + ln]);
     }
   }
 }
@@ -1174,8 +1183,10 @@ void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg) {
     k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
 }
 
+// rhs prefetch depth in steps (a divisor of the ring's 18): 1 measured
+// fastest (973 against 999 us for 3; 9 and 18 at one wave per SIMD slower)
 #ifndef OMG_GS_REG_PF
-#define OMG_GS_REG_PF 3
+#define OMG_GS_REG_PF 1
 #endif
 
 template <int OP>
