@@ -180,6 +180,10 @@ __global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) 
 #ifndef OMG_GS_PF
 #define OMG_GS_PF 4
 #endif
+// y ghosts read once per face (1) or once per line for both shifts (0)
+#ifndef OMG_GS_REG_G2
+#define OMG_GS_REG_G2 0
+#endif
 // timing-only (wrong results): 1 = no sweep, 2 = no rhs loads, 3 = no box load
 #ifndef OMG_T_LEXW
 #define OMG_T_LEXW 0
@@ -625,8 +629,13 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
 #ifndef OMG_GS_REG_WPS
 #define OMG_GS_REG_WPS 2
 #endif
+// y ghosts read once per face (1) or once per line for both shifts (0)
+#ifndef OMG_GS_REG_G2
+#define OMG_GS_REG_G2 0
+#endif
 // timing-only (wrong results): 1 = no sweep (rotation in and out only),
-// 2 = no phi loads or stores (the sweep on whatever LDS holds)
+// 2 = no phi loads or stores (the sweep on whatever LDS holds), 3 = every
+// step's rhs from the box's first block (cache-hot)
 #ifndef OMG_T_RING
 #define OMG_T_RING 0
 #endif
@@ -698,7 +707,14 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   // of the row read face j = 0 as lane j = 1 needs it, the others face j = 17
   // as lane j = 16 needs it; the slack keeps every step's index inside G)
   const int jk0 = j + 4 * kq + 1;                   // line r: jk0 + r
+#if OMG_GS_REG_G2
+  // two reads per line, face j = 0 (the value lane j = 1 keeps in the lower
+  // shift) and face j = 17 (lane j = 16, upper shift): each shift then
+  // writes into its own loaded register, no copies
+  const int gya = kLexGPad - 18 + 15 * (4 * kq + 1), gyb = kLexGFace + kLexGPad - 33 + 15 * (4 * kq + 1);
+#else
   const int gy0 = (j <= 8 ? kLexGPad - 18 : kLexGFace + kLexGPad - 33) + 15 * (4 * kq + 1);   // line r: + 15 r
+#endif
   // z ghosts: lanes of group 0 (line 0, k = 1) read face k = 0, group 3
   // (line 3, k = 16) face k = 17
   const int gz = kq < 2 ? 2 * kLexGFace + kLexGPad + 15 * j - 18 : 3 * kLexGFace + kLexGPad + 15 * j - 33;
@@ -718,9 +734,18 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       const int t = R * m + s;
       if (t < T0 || t > T1) continue;                 // wave-uniform
       const int sm = (s + R - 1) % R, sp = (s + 1) % R;
+#if OMG_GS_REG_G2
+      double gva[4], gvb[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        gva[r] = G[gya + 15 * r + t];
+        gvb[r] = G[gyb + 15 * r + t];
+      }
+#else
       double gv[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) gv[r] = G[gy0 + 15 * r + t];
+#endif
       const double gzv = G[gz + t];
       const double zlo_n = __shfl(ring[3][sm], lane_lo, 64);
       const double zhi_n = __shfl(ring[0][sp], lane_hi, 64);
@@ -733,8 +758,13 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
         st.c = ring[r][s];
         st.xm = ring[r][sm];
         st.xp = ring[r][sp];
+#if OMG_GS_REG_G2
+        st.ym = dpp_row_prev(ring[r][sm], gva[r]);
+        st.yp = dpp_row_next(ring[r][sp], gvb[r]);
+#else
         st.ym = dpp_row_prev(ring[r][sm], gv[r]);
         st.yp = dpp_row_next(ring[r][sp], gv[r]);
+#endif
         st.zm = r > 0 ? ring[r - 1][sm] : zlo;
         st.zp = r < 3 ? ring[r + 1][sp] : zhi;
         nv[r] = gs_value<OP>(K, st, rf[s % PF][r]);
@@ -746,7 +776,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       // unused): a conditional load would be waited for at once
 #pragma unroll
       for (int r = 0; r < 4; r++)
-        rf[s % PF][r] = __builtin_nontemporal_load(rb + ((t + PF) & 15) * 256 + r * 64 + l);
+        rf[s % PF][r] = __builtin_nontemporal_load(rb + (OMG_T_RING == 3 ? 0 : ((t + PF) & 15) * 256) + r * 64 + l);
       // keep the scheduler from interleaving steps (that raises the register
       // pressure past the ring's budget)
       __builtin_amdgcn_sched_barrier(0);
