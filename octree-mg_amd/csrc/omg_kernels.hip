@@ -180,10 +180,6 @@ __global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) 
 #ifndef OMG_GS_PF
 #define OMG_GS_PF 4
 #endif
-// y ghosts read once per face (1) or once per line for both shifts (0)
-#ifndef OMG_GS_REG_G2
-#define OMG_GS_REG_G2 0
-#endif
 // timing-only (wrong results): 1 = no sweep, 2 = no rhs loads, 3 = no box load
 #ifndef OMG_T_LEXW
 #define OMG_T_LEXW 0
@@ -608,8 +604,16 @@ __device__ __forceinline__ double dpp_row_next(double v, double old) {
   return __hiloint2double(hi, lo);
 }
 
-// rhs of every 16^3 box in ring order: rl[b*4096 + ((i+j+k) & 15)*256 + r*64 + l]
+// ring-order rhs blocks rotated by the box index (1) or not (0)
+#ifndef OMG_GS_REG_SW
+#define OMG_GS_REG_SW 1
+#endif
+
+// rhs of every 16^3 box in ring order:
+// rl[b*4096 + ((i+j+k+b) & 15)*256 + (r/2)*128 + 2*l + r%2]
 // for cell (i, j, k) of lane l = (j-1) + 16*((k-1)/4), line r = (k-1) % 4;
+// the step blocks rotated by the box index, so that boxes at the same step
+// (32 KB apart) spread over the memory channels;
 // a bijection (each line has one cell per value of (i+j+k) mod 16)
 __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict__ rl) {
   using TL = Tl<16>;
@@ -620,14 +624,24 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
   __syncthreads();
   double* o = rl + (long long)b * 4096;
   for (int d = threadIdx.x; d < 4096; d += blockDim.x) {
-    const int s = d >> 8, r = (d >> 6) & 3, l = d & 63;
+    // lines 2 rp and 2 rp + 1 of lane l side by side: one 16-B load per lane
+    // and line pair
+    const int s = d >> 8, r = 2 * ((d >> 7) & 1) + (d & 1), l = (d >> 1) & 63;
     const int j = (l & 15) + 1, k = 4 * (l >> 4) + r + 1, i = ((s - j - k - 1) & 15) + 1;
-    o[d] = F[TL::oint(i, j, k)];
+    o[(((s + OMG_GS_REG_SW * b) & 15) << 8) | (d & 255)] = F[TL::oint(i, j, k)];
   }
 }
 
 #ifndef OMG_GS_REG_WPS
 #define OMG_GS_REG_WPS 2
+#endif
+// rhs copy read non-temporally (1) or with the default policy (0)
+#ifndef OMG_GS_REG_RNT
+#define OMG_GS_REG_RNT 0
+#endif
+// phi streams (rotation in and out) non-temporal (1) or default policy (0)
+#ifndef OMG_GS_REG_PNT
+#define OMG_GS_REG_PNT 1
 #endif
 // y ghosts read once per face (1) or once per line for both shifts (0)
 #ifndef OMG_GS_REG_G2
@@ -635,7 +649,8 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
 #endif
 // timing-only (wrong results): 1 = no sweep (rotation in and out only),
 // 2 = no phi loads or stores (the sweep on whatever LDS holds), 3 = every
-// step's rhs from the box's first block (cache-hot)
+// step's rhs from the box's first block (cache-hot), 4 = rhs loaded but not
+// waited for (its values unused)
 #ifndef OMG_T_RING
 #define OMG_T_RING 0
 #endif
@@ -682,7 +697,8 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
 #pragma unroll
     for (int n = 0; n < 8; n++) {
       const int k = 4 * (n >> 1) + r + 1, e = n & 1;
-      buf[n] = OMG_T_RING == 2 ? v2d{0.0, 0.0} : ld_nt(u + e * HV + FH * (k - 1) + 2 * l);
+      const double* src = u + e * HV + FH * (k - 1) + 2 * l;
+      buf[n] = OMG_T_RING == 2 ? v2d{0.0, 0.0} : (OMG_GS_REG_PNT ? ld_nt(src) : *reinterpret_cast<const v2d*>(src));
     }
     const int kr = 4 * kq + r + 1;
     const double gx0 = u[2 * HV + ((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
@@ -721,11 +737,20 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   const int lane_lo = (l + 48) & 63, lane_hi = (l + 16) & 63;
 
   double rf[PF][4];
+  double sink = 0.0;   // OMG_T_RING == 4
+  // the four lines' rhs of step t: two 16-B loads
+  auto ld_rhs = [&](int t, double* out) {
 #pragma unroll
-  for (int p = 0; p < PF; p++)
+    for (int h = 0; h < 2; h++) {
+      const v2d* p = reinterpret_cast<const v2d*>(rb + (OMG_T_RING == 3 ? 0 : ((t + OMG_GS_REG_SW * b) & 15) * 256) +
+                                                  h * 128 + 2 * l);
+      const v2d x = OMG_GS_REG_RNT ? __builtin_nontemporal_load(p) : *p;
+      out[2 * h] = x.x;
+      out[2 * h + 1] = x.y;
+    }
+  };
 #pragma unroll
-    for (int r = 0; r < 4; r++)
-      rf[(T0 + p) % PF][r] = __builtin_nontemporal_load(rb + ((T0 + p) & 15) * 256 + r * 64 + l);
+  for (int p = 0; p < PF; p++) ld_rhs(T0 + p, rf[(T0 + p) % PF]);
 
 #pragma unroll 1
   for (int m = 0; m < 3 && OMG_T_RING != 1; m++) {
@@ -767,22 +792,22 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
 #endif
         st.zm = r > 0 ? ring[r - 1][sm] : zlo;
         st.zp = r < 3 ? ring[r + 1][sp] : zhi;
-        nv[r] = gs_value<OP>(K, st, rf[s % PF][r]);
+        nv[r] = gs_value<OP>(K, st, OMG_T_RING == 4 ? 0.0 : rf[s % PF][r]);
+        if (OMG_T_RING == 4) sink += rf[s % PF][r];
       }
 #pragma unroll
       for (int r = 0; r < 4; r++)
         if ((unsigned)(t - jk0 - r - 1) < (unsigned)NC) ring[r][s] = nv[r];
       // unconditional (past the last step it reads this box's copy again,
       // unused): a conditional load would be waited for at once
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        rf[s % PF][r] = __builtin_nontemporal_load(rb + (OMG_T_RING == 3 ? 0 : ((t + PF) & 15) * 256) + r * 64 + l);
+      ld_rhs(t + PF, rf[s % PF]);
       // keep the scheduler from interleaving steps (that raises the register
       // pressure past the ring's budget)
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 
+  if (OMG_T_RING == 4 && sink == 12345.678) u[0] = sink;
   // the interior back, through stage in the stored order (the box pointer
   // made opaque: otherwise the store addresses are shared with the loads'
   // and held across the sweep, which spills)
@@ -799,9 +824,14 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
       const int ln = (jr - 1) + 16 * kq2;
-      if (OMG_T_RING != 2)
-        st_nt(ub + e * HV + FH * (k - 1) + 2 * l, stage[((i + jr + k) % R) * SR + ln],
-              stage[((i + 2 + jr + k) % R) * SR + ln]);
+      if (OMG_T_RING != 2) {
+        double* dst = ub + e * HV + FH * (k - 1) + 2 * l;
+        const double x0 = stage[((i + jr + k) % R) * SR + ln], x1 = stage[((i + 2 + jr + k) % R) * SR + ln];
+        if (OMG_GS_REG_PNT)
+          st_nt(dst, x0, x1);
+        else
+          *reinterpret_cast<v2d*>(dst) = v2d{x0, x1};
+      }
     }
   }
 }
