@@ -23,7 +23,9 @@ Modes (the domain for N ranks):
 With N > 1 in weak mode the line also carries "c3_strong": the 512^3 problem
 split over the same N GPUs, timed the same way.  Every line carries
 "c4_refined": the one-level-refined octree of BASELINE's C4 (test_refinement,
-128^3 base, box 16, n_levels 2) split over the N ranks.
+128^3 base, box 16, n_levels 2) split over the N ranks.  On one GPU it also
+carries "gs_lex": C2 (256^3) with the reference tests' default smoother,
+lexicographic GS, and that sweep's fraction of 8 TB/s.
 
 value = finest-level cells x V-cycles / s over all ranks (the BASELINE metric).
 roofline: the red-black smoother kernel on the finest level, algorithmic 12 B
@@ -54,6 +56,7 @@ HBM_PEAK_GBS = 8000.0
 BOX = 16
 REPLICATE_CELLS = int(os.environ.get("OMG_REPLICATE_CELLS", 64 * 16 ** 3))
 C4_ARGS = "16 128 128 128 10 v gsrb lpl 0 sol sol 2 lb 0"   # omg_golden / tests.mgdriver form
+GS_ARGS = "16 256 256 256 10 v gs lpl 0 d0 sol 1 lb 0"      # C2 with lexicographic GS
 METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512^3"
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
@@ -311,6 +314,34 @@ def run_c4(omg, dist, world, steps=10, warmup=3):
     return out
 
 
+def run_gs(omg, dist, world, steps=10, warmup=3):
+    """C2 with the reference tests' default smoother, lexicographic GS
+    ("C2-gs": 256^3, box 16, Dirichlet, n_cycle 2+2), one GPU:
+    its cell-updates/s and the finest-level sweep against 8 TB/s (24 B per
+    cell per sweep: phi in, phi out, rhs)."""
+    from tests import mgdriver as D
+    cfg = D.parse(GS_ARGS)
+    be = D.DeviceBackend(cfg)
+    D.setup_problem(be)
+    mg = be.mg
+    timer = Timer(dist, mg.ctx)
+    dt = timer.time(lambda: omg.mg_fas_vcycle(mg), steps, warmup)
+    hi = mg.highest_lvl
+    cells = float(len(mg.lvls[hi].leaves)) * mg.box_size_lvl[hi] ** 3
+    profile_cycle(omg, mg, timer, lambda: omg.mg_fas_vcycle(mg))
+    n, ms, upd = mg.ctx.kernel_stats(f"smoother_gs@{hi}")
+    fr = None
+    if n and ms > 0:
+        fr = {"kernel": "k_gs_lex_reg (register-ring lexicographic GS)", "launches": n,
+              "avg_launch_us": ms * 1e3 / n, "achieved_GBs": 24.0 * upd / (ms * 1e-3) / 1e9,
+              "frac": 24.0 * upd / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    out = {"workload": "C2-gs: 256^3, box 16, Dirichlet, lexicographic GS V-cycle (n_cycle_down=up=2)",
+           "value": cells * steps / dt, "unit": "cell-updates/s", "ms_per_step": dt * 1e3 / steps,
+           "steps": steps, "warmup": warmup, "smoother_lvl_hi": fr}
+    omg.mg_deallocate_storage(mg)
+    return out
+
+
 def host_cores():
     """Physical cores of the host (lscpu), and the CPUs this job may use."""
     phys = None
@@ -448,6 +479,8 @@ def main():
                                   "steps": a.steps, "warmup": a.warmup, "roofline": s.get("roofline"),
                                   "comm": s["comm"]}
         extra["c4_refined"] = run_c4(omg, dist, world)
+        if world == 1:
+            extra["gs_lex"] = run_gs(omg, dist, world)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
