@@ -511,12 +511,26 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream, !c->gs_lex_plane);
       L->rhs_lex_ok = true;
     }
+    // the register ring also writes the boxes' new x boundary layers, so the
+    // fill after each sweep stages 12 KB per box instead of 32 (no
+    // refinement boundaries on the level; OMG_NO_FILL_XL: the plain fill)
+    const bool xlf = plane && !c->gs_lex_plane && L->d_xlay && !L->has_rb && !c->no_fill_tile && !c->no_fill_xl;
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr, !c->gs_lex_plane);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr, !c->gs_lex_plane,
+                      xlf ? L->d_xlay : nullptr);
       }
-      fill_gc_lvl(c, lvl, 1);
+      if (xlf) {
+        L->phi_gc_ok = true;
+        if (L->n) {
+          Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc, lvl);
+          launch_fill_tile_xl(L->sweep_view(), bc_for(c, lvl, 1), L->d_sendbuf, L->d_xlay, c->stream);
+        }
+        finish_halo(c, L, 1);
+      } else {
+        fill_gc_lvl(c, lvl, 1);
+      }
     }
     return;
   }
@@ -979,6 +993,7 @@ void ensure_rhs_lex(omg_ctx* c) {
     Level& L = kv.second;
     if (L.d_rhs_lex || L.n < kGsPlaneMinBoxes || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
+    dmalloc(&L.d_xlay, sizeof(double) * L.n * 2 * L.nc * L.nc);
     L.rhs_lex_ok = false;
   }
 }
@@ -1811,6 +1826,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
+    dfree(L.d_xlay);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
@@ -2189,6 +2205,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
     c->gs_lex_plane = env_flag("OMG_GS_LEX_PLANE");
+    c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only

@@ -135,6 +135,7 @@ struct Level {
   double* d_scratch_rhs = nullptr;   // leaf sums of rhs for the next get_sum
   double* d_rhs_lex = nullptr;       // rhs in plane order for the lexicographic smoother (ensure_rhs_lex)
   bool rhs_lex_ok = false;           // d_rhs_lex equals rhs (dropped by every rhs writer)
+  double* d_xlay = nullptr;          // x boundary layers of the last register-ring sweep (k_fill_tile_xl)
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
   int* d_int = nullptr;
   int n_bnd = 0, n_int = 0;
@@ -252,6 +253,7 @@ struct omg_ctx {
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
   bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring
+  bool no_fill_xl = false;             // OMG_NO_FILL_XL: the plain tiled fill after register-ring sweeps
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

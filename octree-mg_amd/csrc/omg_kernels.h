@@ -45,8 +45,10 @@ void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours
 // rl: rhs copy (launch_rhs_lex) for the register-ring kernel (reg) or the
 // compacted-plane kernel, on gs_lex_plane_ok levels; null: the
 // line-per-thread kernels
+// xl (register ring only, may be null): the swept boxes' new x boundary
+// layers, 512 doubles per box, for launch_fill_tile_xl
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr,
-                   bool reg = true);
+                   bool reg = true, double* xl = nullptr);
 bool gs_lex_plane_ok(int nc, int op);
 // the copy in ring order (reg) or in plane order
 void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg = true);
@@ -125,6 +127,10 @@ bool tiled_nc(int nc);
 // the ghost fill of phi for a level without refinement boundaries, box sizes
 // 4, 8, 16 (false: use launch_fill_gc)
 bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipStream_t st);
+// the same fill right after a register-ring GS sweep of a 16^3 level without
+// refinement boundaries: boxes without a physical face read only their
+// boundary layers (y/z from phi, x from the sweep's xl)
+void launch_fill_tile_xl(const LevelView& L, const GcBC& bc, double* sendbuf, const double* xl, hipStream_t st);
 // the last down-smoothing substep (colour 0) + residual + restriction in one
 // pass (k_smooth_resid); false: not available for this op / box size
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,

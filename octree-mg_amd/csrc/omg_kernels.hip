@@ -655,7 +655,8 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
 #define OMG_T_RING 0
 #endif
 template <int OP, int PF>
-__global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl) {
+__global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl,
+                                                                 double* __restrict__ xl) {
   constexpr int NC = 16, H = 8, HV = 2048, FH = 128, FS = 256, R = kLexRing, T0 = 3, T1 = 3 * NC;
   static_assert(R % PF == 0, "the rhs ring index must repeat with the register ring");
   // stage rows of 65 doubles: the four lanes that scatter one row's cells
@@ -819,6 +820,14 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
 #pragma unroll
     for (int s = 0; s < R; s++) stage[s * SR + l] = ring[r][s];
     __syncthreads();
+    // the new x boundary layers (i = 1, i = 16) of line r, for the ghost
+    // fill that follows (k_fill_tile_xl): xl[b][face][(j-1) + 16 (k-1)]
+    if (xl) {
+      const int kr = 4 * kq + r + 1;
+      double* xo = xl + (long long)b * 512 + (j - 1) + NC * (kr - 1);
+      xo[0] = stage[((1 + j + kr) % R) * SR + l];
+      xo[256] = stage[((NC + j + kr) % R) * SR + l];
+    }
 #pragma unroll
     for (int n = 0; n < 8; n++) {
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
@@ -1255,16 +1264,16 @@ static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hi
   k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
 }
 
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg) {
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg, double* xl) {
   if (L.n == 0) return;
   if (rl) {
     if (!gs_lex_plane_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no plane-order kernel for this level");
     if (reg) {
       // one wave per box, one box per workgroup (8 per CU by their LDS)
       if (op == OP_HELM)
-        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl);
+        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl, xl);
       else
-        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl);
+        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl, xl);
       return;
     }
     if (op == OP_HELM)

@@ -893,6 +893,57 @@ __global__ void __launch_bounds__(BS) k_fill_tile(LevelView L, GcBC bc, double* 
   tile_face_fill<NC>(L, b, sb, 3, bc, sendbuf);
 }
 
+// k_fill_tile after a register-ring GS sweep.  tile_face_fill reads only the
+// boundary layers of a box whose faces are same-GPU or remote neighbours (the
+// second layers only for physical faces), so such a box stages 12 KB instead
+// of its 32 KB interior: the k = 1 and k = 16 planes and the j = 1 and j = 16
+// rows from phi, the i = 1 and i = 16 layers (strided in the colour-split
+// layout) from the sweep's copy xl.  Boxes with a physical face load the
+// whole interior as k_fill_tile does.  Same values, same pushes.
+template <int NC, int BS>
+__global__ void __launch_bounds__(BS) k_fill_tile_xl(LevelView L, GcBC bc, double* sendbuf,
+                                                     const double* __restrict__ xl) {
+  using TL = Tl<NC>;
+  constexpr int HV = TL::HV, H = NC / 2, FH = H * NC;
+  __shared__ double sb[2 * HV];
+  const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
+  const double* u = L.phi + (long long)b * L.stride;
+  bool phys = false;
+#pragma unroll
+  for (int nb = 0; nb < 6; nb++) phys |= L.nbk[(long long)b * 6 + nb] == NB_PHYS;
+  if (phys) {
+    for (int q = threadIdx.x; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
+  } else {
+    const int t = threadIdx.x;
+    // planes k = 1, NC of both colours: 4 x FH doubles
+    for (int q = t; q < 2 * FH; q += BS) {   // double pairs
+      const int e = q / FH, w = q % FH, pl = w / (FH / 2), r2 = w % (FH / 2);
+      const int off = e * HV + (pl ? FH * (NC - 1) : 0) + 2 * r2;
+      *reinterpret_cast<v2d*>(sb + off) = *reinterpret_cast<const v2d*>(u + off);
+    }
+    // rows j = 1, NC of every plane, both colours: 4 x NC rows of H doubles
+    for (int q = t; q < 4 * NC * (H / 2); q += BS) {
+      const int r2 = q % (H / 2), row = q / (H / 2), k = row % NC, jj = (row / NC) & 1, e = row / (2 * NC);
+      const int off = e * HV + H * ((jj ? NC - 1 : 0) + NC * k) + 2 * r2;
+      *reinterpret_cast<v2d*>(sb + off) = *reinterpret_cast<const v2d*>(u + off);
+    }
+    // x layers i = 1, NC from xl
+    const double* xb = xl + (long long)b * 512;
+    for (int q = t; q < 2 * NC * NC; q += BS) {
+      const int f = q / (NC * NC), c = q % (NC * NC), j = c % NC + 1, k = c / NC + 1;
+      sb[TL::oint(f ? NC : 1, j, k)] = xb[q];
+    }
+  }
+  __syncthreads();
+  tile_face_fill<NC>(L, b, sb, 3, bc, sendbuf);
+}
+
+void launch_fill_tile_xl(const LevelView& L, const GcBC& bc, double* sendbuf, const double* xl, hipStream_t st) {
+  if (L.n == 0) return;
+  if (L.nc != 16) throw std::runtime_error("launch_fill_tile_xl: 16^3 boxes only");
+  k_fill_tile_xl<16, 512><<<L.n, 512, 0, st>>>(L, bc, sendbuf, xl);
+}
+
 bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipStream_t st) {
   if (L.n == 0) return true;
   const dim3 g(L.n);
