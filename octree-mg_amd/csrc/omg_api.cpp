@@ -991,7 +991,8 @@ void ensure_rhs_lex(omg_ctx* c) {
   if (c->host_only || c->smoother == OMG_SMOOTHER_GSRB || c->no_gs_plane) return;
   for (auto& kv : c->levels) {
     Level& L = kv.second;
-    if (L.d_rhs_lex || L.n < kGsPlaneMinBoxes || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
+    static const int min_boxes = getenv("OMG_GS_RING_MIN") ? atoi(getenv("OMG_GS_RING_MIN")) : kGsPlaneMinBoxes;
+    if (L.d_rhs_lex || L.n < min_boxes || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
     dmalloc(&L.d_xlay, sizeof(double) * L.n * 2 * L.nc * L.nc);
     L.rhs_lex_ok = false;
