@@ -609,6 +609,30 @@ __device__ __forceinline__ double dpp_row_next(double v, double old) {
 #define OMG_GS_REG_SW 1
 #endif
 
+// z crossings between lane groups by ds_bpermute (0) or by the gfx950 row
+// swaps (1): the 16-lane rows hold the lane groups kq = 0, 1, 3, 2, so that
+// every crossing (kq 0-1, 1-2, 2-3) is a v_permlane16_swap or
+// v_permlane32_swap partner
+#ifndef OMG_GS_REG_PERM
+#define OMG_GS_REG_PERM 1
+#endif
+// lane group of 16-lane row x, and the row of lane group x (an involution)
+__device__ __forceinline__ int lex_grp(int x) { return OMG_GS_REG_PERM && x >= 2 ? 5 - x : x; }
+// the value of v in the lane of the partner row: x16 swaps rows 0-1, 2-3,
+// x32 rows 0-2, 1-3
+__device__ __forceinline__ double row_partner(double v, bool x32) {
+  // both swaps in every lane (the partner lanes must be active), then select
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const int row = threadIdx.x >> 4;
+  const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const auto a16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double p32 = row >= 2 ? __hiloint2double((int)b32[0], (int)a32[0]) : __hiloint2double((int)b32[1], (int)a32[1]);
+  const double p16 = (row & 1) ? __hiloint2double((int)b16[0], (int)a16[0]) : __hiloint2double((int)b16[1], (int)a16[1]);
+  return x32 ? p32 : p16;
+}
+
 // rhs of every 16^3 box in ring order:
 // rl[b*4096 + ((i+j+k+b) & 15)*256 + (r/2)*128 + 2*l + r%2]
 // for cell (i, j, k) of lane l = (j-1) + 16*((k-1)/4), line r = (k-1) % 4;
@@ -627,7 +651,7 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
     // lines 2 rp and 2 rp + 1 of lane l side by side: one 16-B load per lane
     // and line pair
     const int s = d >> 8, r = 2 * ((d >> 7) & 1) + (d & 1), l = (d >> 1) & 63;
-    const int j = (l & 15) + 1, k = 4 * (l >> 4) + r + 1, i = ((s - j - k - 1) & 15) + 1;
+    const int j = (l & 15) + 1, k = 4 * lex_grp(l >> 4) + r + 1, i = ((s - j - k - 1) & 15) + 1;
     o[(((s + OMG_GS_REG_SW * b) & 15) << 8) | (d & 255)] = F[TL::oint(i, j, k)];
   }
 }
@@ -664,7 +688,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   constexpr int SR = 65;
   __shared__ double stage[R * SR];          // one line of every lane, slot-major
   __shared__ double G[4 * kLexGFace];       // y/z ghost faces, plain [c][a] with slack
-  const int l = threadIdx.x, kq = l >> 4, j = (l & 15) + 1;
+  const int l = threadIdx.x, kq = lex_grp(l >> 4), j = (l & 15) + 1;
   const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
   double* __restrict__ u = boxp(L, 1, b);
   const double* __restrict__ rb = rl + (long long)b * (NC * NC * NC);
@@ -709,7 +733,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
     for (int n = 0; n < 8; n++) {
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
-      const int ln = (jr - 1) + 16 * kq2;
+      const int ln = (jr - 1) + 16 * lex_grp(kq2);
       stage[((i + jr + k) % R) * SR + ln] = buf[n].x;
       stage[((i + 2 + jr + k) % R) * SR + ln] = buf[n].y;
     }
@@ -773,8 +797,15 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       for (int r = 0; r < 4; r++) gv[r] = G[gy0 + 15 * r + t];
 #endif
       const double gzv = G[gz + t];
+#if OMG_GS_REG_PERM
+      // z crossings: group kq takes line 3 of group kq - 1 and line 0 of
+      // group kq + 1; pairs 0-1 and 2-3 are x16 partners, 1-2 x32 partners
+      const double zlo_n = row_partner(ring[3][sm], kq == 2);
+      const double zhi_n = row_partner(ring[0][sp], kq == 1);
+#else
       const double zlo_n = __shfl(ring[3][sm], lane_lo, 64);
       const double zhi_n = __shfl(ring[0][sp], lane_hi, 64);
+#endif
       const double zlo = kq == 0 ? gzv : zlo_n;
       const double zhi = kq == 3 ? gzv : zhi_n;
       double nv[4];
@@ -832,7 +863,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
     for (int n = 0; n < 8; n++) {
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
-      const int ln = (jr - 1) + 16 * kq2;
+      const int ln = (jr - 1) + 16 * lex_grp(kq2);
       if (OMG_T_RING != 2) {
         double* dst = ub + e * HV + FH * (k - 1) + 2 * l;
         const double x0 = stage[((i + jr + k) % R) * SR + ln], x1 = stage[((i + 2 + jr + k) % R) * SR + ln];
