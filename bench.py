@@ -305,6 +305,22 @@ def run_c4(omg, dist, world, steps=10, warmup=3):
     if world == 1 and n and ms > 0:
         fr = {"avg_launch_us": ms * 1e3 / n, "achieved_GBs": 24.0 * upd / (ms * 1e-3) / 1e9,
               "frac": 24.0 * upd / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if world == 1 and n:
+        # the same launches back to back: smooth_boxes on the finest level,
+        # 10 cycles = 20 substeps (one launch each, the fill fused), timed as
+        # one block; a 12-us kernel timed by its own event pair reads several
+        # us long (compare the kernel trace, profiles/r03/v14_trace_C4_by_grid.txt)
+        k = 10
+        mg.ctx.call("smooth_boxes", hi, 1)
+        mg.ctx.call("synchronize")
+        t0 = time.perf_counter()
+        mg.ctx.call("smooth_boxes", hi, k)
+        mg.ctx.call("synchronize")
+        tb = (time.perf_counter() - t0) / (2 * k)
+        upd1 = upd / n
+        fr["back_to_back"] = {"launches": 2 * k, "avg_launch_us": tb * 1e6,
+                              "achieved_GBs": 24.0 * upd1 / tb / 1e9,
+                              "frac": 24.0 * upd1 / tb / 1e9 / HBM_PEAK_GBS}
     out = {"workload": "C4: test_refinement 2 16 128 128 128 (one refined level, box 16), GSRB, "
                        "callback Dirichlet u",
            "value": cells * steps / dt, "unit": "cell-updates/s (leaf cells)", "ms_per_step": dt * 1e3 / steps,
