@@ -119,7 +119,14 @@ int omg_level_size(omg_ctx *ctx, int lvl, int *n_boxes, int *nc);
 
 /* Bulk copy of variable iv of all my_ids boxes at lvl, in my_ids order,
  * (nc+2)^3 doubles per box as mg%boxes(id)%cc(:,:,:,iv) stores them
- * (src/m_data_structures.f90:209-221), host memory (blocking). */
+ * (src/m_data_structures.f90:209-221), host memory (blocking).
+ * Multi-rank: an upload of phi (iv = 1) is collective, like every other call
+ * that writes the device state: each rank calls it for the level, with its own
+ * boxes, possibly none.  A stand-alone omg_fas_vcycle decides on every rank
+ * alike, without communication, whether its ghost fill can be skipped; a phi
+ * upload made on some ranks only would make that decision differ
+ * (OMG_CHECK_COLLECTIVE=1 detects it: the decision is then also agreed over
+ * the transport and a mismatch is an error). */
 int omg_upload_level(omg_ctx *ctx, int lvl, int iv, const double *host);
 int omg_download_level(omg_ctx *ctx, int lvl, int iv, double *host);
 
@@ -212,6 +219,14 @@ int omg_comm_info(omg_ctx *ctx, int *n_ranks, int *transport);
 /* Stream / timing helpers for benchmarks. */
 int omg_synchronize(omg_ctx *ctx);
 void *omg_stream(omg_ctx *ctx);                 /* the hipStream_t all work runs on */
+/* Diagnostics (no reference counterpart): the number of times the host has
+ * waited for one of the context's streams so far (a multi-rank stand-alone
+ * V-cycle over RCCL waits only when max_res is requested, m_multigrid.f90:
+ * 226-234; the loopback transport also waits to gather the periodic mean on
+ * the host), and the priority of the halo-overlap stream (the greatest of
+ * hipDeviceGetStreamPriorityRange). */
+int omg_host_sync_count(omg_ctx *ctx, long long *n);
+int omg_comm_stream_priority(omg_ctx *ctx, int *priority);
 /* Per-kernel HIP-event timing (off by default): when on, every launch of the
  * named kernel families is bracketed by events on the stream it runs on, and
  * kept per family and per family@level.  "comm" / "comm_overlap" are the

@@ -55,6 +55,14 @@ struct OmgError : std::runtime_error {
     if (r_ != ncclSuccess) throw OmgError(std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+// Every place the host waits for a context stream goes through here, so the
+// waits of a call can be counted (omg_host_sync_count: a multi-rank stand-alone
+// V-cycle makes none unless max_res is requested).
+inline void host_sync(omg_ctx* c, hipStream_t st) {
+  c->n_host_syncs++;
+  HIPCHK(hipStreamSynchronize(st));
+}
+
 template <typename F>
 int guarded(F&& f) {
   try {
@@ -611,7 +619,7 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     c->max_deferred = true;
     return 0.0;
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  host_sync(c, c->stream);
   return c->h_scalar[0];
 }
 
@@ -859,9 +867,18 @@ double allreduce(omg_ctx* c, double v, bool is_max) {
     HIPCHK(hipMemcpyAsync(d, &c->h_scalar[1], 8, hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclAllGather(d, d + 1, 1, ncclDouble, (ncclComm_t)c->nccl, c->stream));
     HIPCHK(hipMemcpyAsync(all.data(), d + 1, 8 * c->n_ranks, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
   }
-  if (is_max) return *std::max_element(all.begin(), all.end());
+  if (is_max) {
+    // the device max is on IEEE bits (amax): NaN and Inf propagate; so must
+    // the combination over ranks (std::max_element skips a NaN past all[0])
+    double m = all[0];
+    for (double x : all) {
+      if (std::isnan(x)) return x;
+      m = x > m ? x : m;
+    }
+    return m;
+  }
   // MPI_Allreduce(MPI_SUM) as MPICH 3.3.2 computes it on one node
   // (m_multigrid.f90:255): a binomial-tree reduce to rank 0 in rank order,
   // ((a0+a1)+(a2+a3))+a4 ..., then a broadcast.  Pinned by the golden runs
@@ -894,7 +911,7 @@ void leaf_box_sums(omg_ctx* c, int iv, int ch, hipStream_t st) {
   for (int l = 1; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
-    Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l);
+    Prof p(c, "box_sums", (double)L->leaves.size() * L->nc * L->nc * L->nc, l, st);
     launch_box_sums(L->sweep_view(), iv, L->d_leaves, (int)L->leaves.size(), leaf_scratch(L, ch), st);
   }
 }
@@ -905,7 +922,7 @@ void leaf_chain(omg_ctx* c, int ch, hipStream_t st) {
   for (int l = 1; l <= c->highest; l++) {
     Level* L = level_ptr(c, l);
     if (!L || L->leaves.empty()) continue;
-    Prof p(c, "seq_sum", (double)L->leaves.size(), l);
+    Prof p(c, "seq_sum", (double)L->leaves.size(), l, st);   // (timed on the stream it runs on)
     launch_seq_sum(leaf_scratch(L, ch), (int)L->leaves.size(), L->dr[0] * L->dr[1] * L->dr[2], acc, first, st);
     first = false;
   }
@@ -934,7 +951,7 @@ void mean_device(omg_ctx* c, int ch) {
     all = red_acc(c, ch);
   } else if (c->loop) {
     HIPCHK(hipMemcpyAsync(c->h_scalar + 4, red_acc(c, ch), 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
     std::vector<double> v = loop_allgather(c, c->h_scalar[4]);
     for (int r = 0; r < n; r++) c->h_scalar[8 + r] = v[r];
     HIPCHK(hipMemcpyAsync(all, c->h_scalar + 8, 8 * n, hipMemcpyHostToDevice, c->stream));
@@ -948,7 +965,7 @@ void mean_device(omg_ctx* c, int ch) {
 double get_sum(omg_ctx* c, int iv) {
   leaf_sum_device(c, iv, kChPhi);
   HIPCHK(hipMemcpyAsync(c->h_scalar + 2, red_acc(c, kChPhi), 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  host_sync(c, c->stream);
   return allreduce(c, c->h_scalar[2], false);
 }
 
@@ -987,12 +1004,23 @@ void drop_rhs_lex(omg_ctx* c) {
 // small levels the per-cycle copy costs more than it saves (C1: 0.255 ->
 // 0.293 ms with it on its 8^3 levels, profiles/r03/v7_README.txt)
 constexpr int kGsPlaneMinBoxes = 2048;
+// Called whenever the smoother or the operator changes (never inside a
+// capture): the buffers exist exactly on the levels the current methods use
+// them on, and are freed otherwise (a 512^3 level's are ~1.1 GiB).
 void ensure_rhs_lex(omg_ctx* c) {
-  if (c->host_only || c->smoother == OMG_SMOOTHER_GSRB || c->no_gs_plane) return;
+  if (c->host_only) return;
+  const bool want = c->smoother != OMG_SMOOTHER_GSRB && !c->no_gs_plane;
+  static const int min_boxes = getenv("OMG_GS_RING_MIN") ? atoi(getenv("OMG_GS_RING_MIN")) : kGsPlaneMinBoxes;
   for (auto& kv : c->levels) {
     Level& L = kv.second;
-    static const int min_boxes = getenv("OMG_GS_RING_MIN") ? atoi(getenv("OMG_GS_RING_MIN")) : kGsPlaneMinBoxes;
-    if (L.d_rhs_lex || L.n < min_boxes || !gs_lex_plane_ok(L.nc, OP_LPL)) continue;
+    if (!want || L.n < min_boxes || !gs_lex_plane_ok(L.nc, c->op)) {
+      if (L.d_rhs_lex || L.d_xlay) HIPCHK(hipStreamSynchronize(c->stream));   // (in use by queued sweeps)
+      dfree(L.d_rhs_lex);
+      dfree(L.d_xlay);
+      L.rhs_lex_ok = false;
+      continue;
+    }
+    if (L.d_rhs_lex) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
     dmalloc(&L.d_xlay, sizeof(double) * L.n * 2 * L.nc * L.nc);
     L.rhs_lex_ok = false;
@@ -1023,7 +1051,7 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
   if (iv == 1) {
     materialize_phi(c);
     for (auto& kv : c->levels)
-      if (!ghosts || kv.second.has_phys || kv.second.has_rb) kv.second.phi_gc_ok = false;
+      if (!ghosts || kv.second.any_phys || kv.second.any_rb) kv.second.phi_gc_ok = false;
   }
   if (iv == 2 && !ghosts) {
     // rhs: the sums may already be running on the side stream (see below)
@@ -1175,7 +1203,7 @@ void run_tail(omg_ctx* c, int top) {
   if (tail_timing) {   // diagnostics: phase times of the tail (100 MHz wall clock)
     long long h[64];
     HIPCHK(hipMemcpyAsync(h, c->d_tail_stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
     const int n = 4 * (A.n_lvls - 1) + 2 + 2 * (A.n_lvls - 1);
     std::fprintf(stderr, "tail us:");
     for (int i = 1; i < n; i++) std::fprintf(stderr, " %.1f", (h[i] - h[i - 1]) * 0.01);
@@ -1214,10 +1242,18 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   }
   if (c->subtract_mean && !has_highest) subtract_mean(c, 2, 0, full ? kInCycle : kPlain);
   if (standalone) {
-    // the fill is idempotent: skip it when the ghosts already equal its result
+    // the fill is idempotent: skip it when the ghosts already equal its result.
+    // Fills exchange halos, so every rank must decide alike; the decision is
+    // rank-invariant without communication: phi_gc_ok changes only in calls
+    // every rank makes (fills, cycles, restriction / prolongation, collective
+    // uploads of phi, see omg.h), and any_rb is a property of the global
+    // tree.  (Agreeing over the transport instead, as round 3 did, cost a
+    // host synchronisation per cycle.)  OMG_CHECK_COLLECTIVE checks it.
     Level* L = level_ptr(c, max_lvl);
-    bool need = !(L && L->phi_gc_ok && !L->has_rb);
-    if (c->n_ranks > 1) need = allreduce(c, need ? 1.0 : 0.0, true) > 0.5;   // fills exchange: agree
+    const bool need = !(L && L->phi_gc_ok && !L->any_rb);
+    if (c->n_ranks > 1 && c->check_collective && (allreduce(c, need ? 1.0 : 0.0, true) > 0.5) != need)
+      throw OmgError("mg_fas_vcycle: the stand-alone fill decision differs across ranks "
+                     "(an upload of phi was not made on every rank)");
     if (need) {
       if (L) materialize_level(c, L);
       fill_gc_lvl(c, max_lvl, 1);
@@ -1239,8 +1275,15 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     for (int id : ids)
       if (min_lvl > c->rep_lvl && c->rank_of[id - 1] != c->rank_of[ids[0] - 1])
         throw OmgError("Multiple CPUs for coarse grid (not implemented yet)");
-    double init_res = max_residual_lvl(c, min_lvl);
-    for (int i = 1; i <= c->max_coarse_cycles; i++) {
+    // a rank without the coarse boxes has nothing to do here: they all live on
+    // one rank, so their smoothing exchanges nothing (the reference's other
+    // ranks run empty loops until the owner's residual test, which they never
+    // see either, m_multigrid.f90:202-208); skipping it saves them a host wait
+    // per coarse sweep
+    const Level* Lmin = level_ptr(c, min_lvl);
+    const bool own_coarse = Lmin && Lmin->n > 0;
+    double init_res = own_coarse ? max_residual_lvl(c, min_lvl) : 0.0;
+    for (int i = 1; own_coarse && i <= c->max_coarse_cycles; i++) {
       smooth_boxes(c, min_lvl, c->n_cycle_up + c->n_cycle_down);
       double res = max_residual_lvl(c, min_lvl);
       if (res < c->res_rel * init_res || res < c->res_abs) break;
@@ -1341,6 +1384,9 @@ void graph_rollback(omg_ctx* c, int key) {
     c->graphs.erase(it);
   }
   phi_dirty_all(c);
+  // the captured body may have recorded the ring-order rhs copy (and marked
+  // it built) without the graph ever running
+  drop_rhs_lex(c);
   (void)hipGetLastError();
 }
 
@@ -1394,7 +1440,7 @@ double run_cycle(omg_ctx* c, int key, F&& body) {
   HIPCHK(hipGraphDestroy(g));
   if (!c->max_deferred) return 0.0;
   c->max_deferred = false;
-  HIPCHK(hipStreamSynchronize(c->stream));
+  host_sync(c, c->stream);
   return c->h_scalar[0];
 }
 
@@ -1408,8 +1454,10 @@ void set_operator(omg_ctx* c, int op, double lambda) {
   if ((op == OMG_VLAPLACIAN || op == OMG_VHELMHOLTZ) && c->n_vars < 5 && c->n_boxes > 0)
     throw OmgError("vlaplacian/vhelmholtz_set_methods: mg%n_extra_vars == 0");
   if (op == OMG_VLAPLACIAN) lambda = 0.0;
+  const bool changed = c->op != op;
   c->op = op;
   c->lambda = lambda;
+  if (changed && !c->capturing) ensure_rhs_lex(c);
 }
 
 // mg_apply_op (m_multigrid.f90:439-456): box_op on every box of every level
@@ -1460,7 +1508,11 @@ void diffusion_solve(omg_ctx* c, int op, double dt, double coeff, int order, dou
   double res = run_cycle(c, 2 + 2 + 4, [&] { return fas_fmg(c, true, true); });
   int n = 1;
   for (; n <= kDiffusionMaxIts; n++) {
-    check_finite_res(res, "diffusion_solve");
+    if (!std::isfinite(res)) {   // the outputs hold the state at the error (omg.h)
+      if (n_vcycles) *n_vcycles = n - 1;
+      if (res_out) *res_out = res;
+      check_finite_res(res, "diffusion_solve");
+    }
     if (res <= max_res) break;
     res = run_cycle(c, 1 + 2 + 4 + 8 * (c->lowest - 1 + 64),
                     [&] { return fas_vcycle(c, c->lowest - 1, true, true); });
@@ -1483,7 +1535,7 @@ void phi_bc_store(omg_ctx* c) {
     launch_phi_bc_store(L.view(), g, L.d_nba, c->stream);
     HIPCHK(hipMemcpyAsync(L.h_nba.data(), L.d_nba, sizeof(int) * L.h_nba.size(), hipMemcpyDeviceToHost,
                           c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
     for (int b = 0; b < L.n; b++)
       for (int nb = 1; nb <= 6; nb++)
         if (L.h_nbk[(size_t)b * 6 + nb - 1] == NB_PHYS)
@@ -1604,7 +1656,7 @@ void free_create_kernel(omg_ctx* c, omg_free_state* S, const double h[3]) {
   // PSolver's scal = hx*hy*hz/(n1*n2*n3) (psolver_main.f90:297)
   const double scal = h[0] * h[1] * h[2] / ((double)G.N[0] * (double)G.N[1] * (double)G.N[2]);
   launch_free_karray(d_F, fmax, d_w, G, scal, S->d_karray, c->stream);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  host_sync(c, c->stream);
   dfree(d_p0);
   dfree(d_w);
   dfree(d_nit);
@@ -1999,6 +2051,13 @@ void build_plan(omg_ctx* c) {
     L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
+    L.any_rb = L.any_phys = false;
+    for (int id : c->ids[l])
+      for (int nb = 1; nb <= 6; nb++) {
+        const int nid = T.nbr(id, nb);
+        L.any_rb |= nid == 0;
+        L.any_phys |= nid < 0;
+      }
     {
       // boxes with a face toward another GPU (halo overlap in smooth_boxes)
       std::vector<int> bnd, in;
@@ -2209,6 +2268,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
+    c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -2222,7 +2282,15 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     std::memset(c->h_tail, 0xff, sizeof(TailArgs));
     HIPCHK(hipMemset(c->d_maxslots, 0, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream_comm, hipStreamNonBlocking));
+    {
+      // the halo stream at the highest priority: its RCCL kernels are queued
+      // behind the boundary boxes while an interior substep of thousands of
+      // workgroups fills every CU; priority lets the dispatcher place them first
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIPCHK(hipStreamCreateWithPriority(&c->stream_comm, hipStreamNonBlocking, greatest));
+      c->comm_priority = greatest;
+    }
     HIPCHK(hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
@@ -2342,8 +2410,8 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
       }
     }
     if (!c->host_only) {
-      HIPCHK(hipStreamSynchronize(c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream2));
+      host_sync(c, c->stream);
+      host_sync(c, c->stream2);
     }
     c->rhs_cache_valid = false;
     c->phi_shift_pending = false;
@@ -2495,9 +2563,11 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
+    // (before the early return: a rank without boxes here still drops the
+    // flag, which the multi-rank stand-alone fill decision relies on)
+    if (iv == 1) L->phi_gc_ok = false;
     if (!L->n) return;
     const size_t s = L->nc + 2, box = s * s * s, n = box * L->n;
-    if (iv == 1) L->phi_gc_ok = false;
     double* st = stage(c, n);
     if (L->replicated) {
       // the host's boxes into their slots, then to every peer (collective)
@@ -2511,12 +2581,12 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
         exchange(c, L->repl, L->d_sendbuf, L->d_recvbuf, nullptr, lvl);
         launch_box_unpack(L->view(), iv, L->repl.d_recv_items, L->repl.n_recv, L->d_recvbuf, c->stream);
       }
-      HIPCHK(hipStreamSynchronize(c->stream));
+      host_sync(c, c->stream);
       return;
     }
     HIPCHK(hipMemcpyAsync(st, host, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
     launch_from_ref(L->view(), iv, st, c->stream);
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
   });
 }
 
@@ -2533,13 +2603,13 @@ int omg_download_level(omg_ctx* c, int lvl, int iv, double* host) {
     if (L->replicated) {   // the host's boxes only
       std::vector<double> full(n);
       HIPCHK(hipMemcpyAsync(full.data(), st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
+      host_sync(c, c->stream);
       for (size_t q = 0; q < L->host_local.size(); q++)
         std::memcpy(host + box * q, full.data() + box * L->host_local[q], sizeof(double) * box);
       return;
     }
     HIPCHK(hipMemcpyAsync(host, st, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    host_sync(c, c->stream);
   });
 }
 
@@ -2674,7 +2744,7 @@ int omg_free_planes(omg_ctx* c, int* fft_lvl, int* nx, double* planes, long long
     const size_t n = 2 * ((size_t)nx[1] * nx[2] + (size_t)nx[0] * nx[2] + (size_t)nx[0] * nx[1]);
     if (planes && cap >= (long long)n) {
       HIPCHK(hipMemcpyAsync(planes, S->d_planes, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
+      host_sync(c, c->stream);
     }
   });
 }
@@ -2696,12 +2766,20 @@ int omg_comm_info(omg_ctx* c, int* n_ranks, int* transport) {
 
 int omg_synchronize(omg_ctx* c) {
   return guarded([&] {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream2));
+    host_sync(c, c->stream);
+    host_sync(c, c->stream2);
   });
 }
 
 void* omg_stream(omg_ctx* c) { return (void*)c->stream; }
+
+int omg_host_sync_count(omg_ctx* c, long long* n) {
+  return guarded([&] { *n = c->n_host_syncs; });
+}
+
+int omg_comm_stream_priority(omg_ctx* c, int* priority) {
+  return guarded([&] { *priority = c->comm_priority; });
+}
 
 int omg_set_profiling(omg_ctx* c, int on) {
   return guarded([&] {

@@ -100,6 +100,10 @@ struct Level {
   double* d_phi = nullptr;              // phi (d_data's var 1)
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
   bool has_rb = false, has_remote = false, has_phys = false;
+  // the same flags over the level's boxes on EVERY rank (from the global
+  // tree): decisions that choose collective calls use these, never the local
+  // ones, so every rank takes the same branch (fas_vcycle's stand-alone fill)
+  bool any_rb = false, any_phys = false;
   bool all_parents = false;      // every box of this rank at this level is a parent
   bool prolong_smooth_ok = false;  // k_prolong_smooth can serve this level (see build_plan)
   bool shift_pending = false;    // phi -= mean still to apply (see subtract_mean)
@@ -241,7 +245,8 @@ struct omg_ctx {
   // scalars
   double* d_red = nullptr;             // device reductions (get_sum / subtract_mean)
   hipStream_t stream2 = nullptr;       // side stream (rhs sum chain)
-  hipStream_t stream_comm = nullptr;   // halo exchange overlapped with interior boxes
+  hipStream_t stream_comm = nullptr;   // halo exchange overlapped with interior boxes (highest priority)
+  int comm_priority = 0;               // its priority (hipDeviceGetStreamPriorityRange's greatest)
   hipEvent_t ev_bnd = nullptr, ev_comm = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_phi = nullptr;
   bool phi_mean_on_side = false;
@@ -282,6 +287,11 @@ struct omg_ctx {
   // OMG_DEBUG: ghost faces start as signalling NaN, unstored edge / corner
   // cells download as signalling NaN (the reference's DEBUG=1 -finit-real=snan)
   bool debug = false;
+  // OMG_CHECK_COLLECTIVE: multi-rank decisions that are made without
+  // communication (rank-invariant by construction) are also agreed over the
+  // transport and an error is raised when they differ (tests)
+  bool check_collective = false;
+  long long n_host_syncs = 0;          // host waits on a stream (host_sync; omg_host_sync_count)
   std::map<std::string, omg::KStat> stats;
   std::vector<omg::PendingEv> pending;
 };

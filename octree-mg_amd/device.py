@@ -62,6 +62,8 @@ SIGNATURES = {
     "omg_comm_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I)]),
     "omg_synchronize": (_I, [_P]),
     "omg_stream": (_P, [_P]),
+    "omg_host_sync_count": (_I, [_P, C.POINTER(_LL)]),
+    "omg_comm_stream_priority": (_I, [_P, C.POINTER(_I)]),
     "omg_set_profiling": (_I, [_P, _I]),
     "omg_kernel_stats": (_I, [_P, C.c_char_p, C.POINTER(_LL), C.POINTER(_D), C.POINTER(_D)]),
     "omg_reset_stats": (_I, [_P]),
@@ -181,6 +183,17 @@ class Context:
         n, t = _I(), _I()
         self.call("comm_info", C.byref(n), C.byref(t))
         return n.value, {0: "none", 1: "rccl", 2: "loopback"}[t.value]
+
+    def host_sync_count(self):
+        """Host waits on the context's streams so far (omg_host_sync_count)."""
+        n = _LL(0)
+        self.call("host_sync_count", C.byref(n))
+        return n.value
+
+    def comm_stream_priority(self):
+        p = _I(0)
+        self.call("comm_stream_priority", C.byref(p))
+        return p.value
 
     def kernel_stats(self, name):
         n, ms, cells = _LL(0), _D(0), _D(0)

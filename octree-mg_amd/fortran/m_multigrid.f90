@@ -474,8 +474,16 @@ contains
     integer                     :: i, id, nc, n
 
     n = size(mg%lvls(lvl)%my_ids)
-    if (n == 0) return
     nc = mg%box_size_lvl(lvl)
+    if (n == 0) then
+       ! uploads are collective (include/omg.h): a rank without boxes here
+       ! still makes the call
+       if (up) then
+          allocate(buf(1, 1, 1, 1))
+          call omg_ok(omg_upload_level(ctx, int(lvl, c_int), int(iv, c_int), buf), "upload_level")
+       end if
+       return
+    end if
     allocate(buf(0:nc+1, 0:nc+1, 0:nc+1, n))
     if (up) then
        do i = 1, n

@@ -128,7 +128,7 @@ class OracleBackend:
     def my_ids(self, lvl):
         return self.tree.lvls[lvl].ids
 
-    def collective(self, lvl):
+    def collective(self, lvl, iv=None):
         return False
 
     def set_level(self, lvl, iv, data):
@@ -198,12 +198,13 @@ class DeviceBackend:
     def my_ids(self, lvl):
         return self.mg.lvls[lvl].my_ids
 
-    def collective(self, lvl):
-        # uploads to a replicated level: every rank calls (omg_set_coarse_replication)
-        return lvl <= self.rep_lvl
+    def collective(self, lvl, iv=None):
+        # uploads to a replicated level: every rank calls (omg_set_coarse_replication);
+        # so do uploads of phi (the stand-alone fill decision, include/omg.h)
+        return lvl <= self.rep_lvl or iv == T.MG_IPHI
 
     def set_level(self, lvl, iv, data):
-        if len(self.my_ids(lvl)) or self.collective(lvl):
+        if len(self.my_ids(lvl)) or self.collective(lvl, iv):
             self.mg.set_level(lvl, iv, data)
 
     def get_level(self, lvl, iv):
@@ -259,7 +260,7 @@ def setup_problem(be):
         ids = be.my_ids(lvl)
         if len(ids):
             be.set_level(lvl, iv, make(ids))
-        elif be.collective(lvl):
+        elif be.collective(lvl, iv):
             be.set_level(lvl, iv, empty(lvl))
 
     if is_vop(cfg) or cfg["op"] == "ahelm":
@@ -408,14 +409,12 @@ def _owned_phi(be):
     return out
 
 
-def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0):
-    """The same configuration on n_ranks device contexts of this process (one
-    thread per rank, all on GPU 0), exchanging through the loopback transport
-    (omg_loopback_unique_id): the multi-rank path of libomg.so (plans, packing,
-    MPICH-order reductions) on a single GPU.  Returns the history with err /
-    res reduced by max over ranks, as omg_golden's MPI_Reduce(MAX), and the
-    sha256 of the final phi of every box gathered from its owner, in the
-    order phi_digest uses for a one-rank run (ids per level, lowest first)."""
+def run_loopback(args: str, n_ranks: int, body, n_its=None, timeout=600, rep_cells=0):
+    """Run body(be, rank, reduce) on n_ranks device contexts of this process
+    (one thread per rank, all on GPU 0) exchanging through the loopback
+    transport (omg_loopback_unique_id), each with the configuration's tree and
+    problem set up; reduce(e, r) is omg_golden's MPI_Reduce(MAX) of a pair.
+    Returns the per-rank results; the first rank error is raised."""
     import threading
     cfg = parse(args)
     if n_its is not None:
@@ -424,8 +423,6 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
     bar = threading.Barrier(n_ranks)
     slots = [None] * n_ranks
     out = [None] * n_ranks
-    phis = [None] * n_ranks
-    trees = [None] * n_ranks
     errors = []
 
     def worker(rank):
@@ -439,10 +436,8 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
         try:
             be = DeviceBackend(cfg, omg.Loopback(tag, rank, n_ranks), rep_cells)
             setup_problem(be)
-            out[rank] = _cycles(be, cfg, reduce)
+            out[rank] = body(be, rank, reduce)
             be.mg.ctx.call("synchronize")
-            phis[rank] = _owned_phi(be)
-            trees[rank] = be.tree
             omg.mg_deallocate_storage(be.mg)
         except BaseException as ex:  # noqa: BLE001  (re-raised in the caller)
             errors.append((rank, ex))
@@ -459,6 +454,30 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
         raise RuntimeError(msg or str(errors[0][1]))
     if any(t.is_alive() for t in th):
         raise TimeoutError("loopback run did not finish")
+    return out
+
+
+def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0):
+    """The same configuration on n_ranks device contexts of this process,
+    exchanging through the loopback transport (run_loopback): the multi-rank
+    path of libomg.so (plans, packing, MPICH-order reductions) on a single
+    GPU.  Returns the history with err / res reduced by max over ranks, as
+    omg_golden's MPI_Reduce(MAX), and the sha256 of the final phi of every box
+    gathered from its owner, in the order phi_digest uses for a one-rank run
+    (ids per level, lowest first)."""
+    cfg = parse(args)
+    if n_its is not None:
+        cfg["n_its"] = n_its
+
+    def body(be, rank, reduce):
+        hist = _cycles(be, cfg, reduce)
+        be.mg.ctx.call("synchronize")
+        return hist, _owned_phi(be), be.tree
+
+    res = run_loopback(args, n_ranks, body, n_its, timeout, rep_cells)
+    out = [r[0] for r in res]
+    phis = [r[1] for r in res]
+    trees = [r[2] for r in res]
     assert all(h == out[0] for h in out)
     tree = trees[0]
     h = hashlib.sha256()

@@ -39,3 +39,37 @@ def test_launcher_spawns_ranks_whose_plans_pair_up(n, mode, domain):
     assert len(boxes) == 1
     for r in out["ranks"]:
         assert r["halo_faces_recv_lvl_hi"] > 0 and 1 <= len(r["peers_lvl_hi"]) <= min(3, n - 1)
+
+
+def test_cpu_baseline_timeout_leaves_no_process(tmp_path):
+    """bench.py's cpu_baseline runs each `mpiexec -n P` in a session of its
+    own and kills that session's process group on timeout or exit: a
+    reference run that hangs leaves no hydra proxy or rank behind (round 3's
+    BENCH ended with one stray process: subprocess.run(timeout=...) killed
+    mpiexec only)."""
+    if not os.path.exists("/opt/conda/bin/mpiexec"):
+        pytest.skip("no MPICH mpiexec")
+    sys.path.insert(0, ROOT)
+    import bench
+    marker = "300.%06d" % (os.getpid() % 1000000)
+    fake = tmp_path / "fake_ref"
+    fake.write_text(f"#!/bin/bash\nsleep {marker} &\nsleep {marker}\n")
+    fake.chmod(0o755)
+
+    def alive():
+        n = 0
+        for pid in os.listdir("/proc"):
+            if not pid.isdigit():
+                continue
+            try:
+                with open(f"/proc/{pid}/cmdline", "rb") as f:
+                    cmd = f.read().replace(b"\0", b" ").decode(errors="replace")
+            except OSError:
+                continue
+            n += marker in cmd or str(fake) in cmd
+        return n
+
+    out = bench.cpu_baseline([16, 16, 16], ref=str(fake), timeout=3, plan=[(2, 1, 1)])
+    assert "TimeoutExpired" in out["by_ranks"]["2"]["error"]
+    assert out["value"] is None
+    assert alive() == 0

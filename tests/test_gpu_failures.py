@@ -17,7 +17,8 @@ import os
 import numpy as np
 import pytest
 
-from tests.mgdriver import DeviceBackend, T, _cycles, omg, parse, phi_digest, run_problem, setup_problem
+from tests.mgdriver import (DeviceBackend, T, _cycles, omg, parse, phi_digest, run_loopback, run_problem,
+                            setup_problem)
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
 
@@ -45,6 +46,26 @@ def test_non_finite_rhs_is_an_error(args, bad):
             be.fmg(False, True)
         else:
             be.vcycle(True)
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf])
+def test_non_finite_on_another_rank_is_an_error(bad):
+    """Two loopback ranks, the bad value in a box rank 1 owns: the max over
+    ranks propagates it like the device max does (round 3 combined the ranks
+    with std::max_element, which skips a NaN after the first rank)."""
+    args = "16 64 64 64 1 v gsrb lpl 0 d0 sol 1 lb 0"
+
+    def body(be, rank, reduce):
+        if rank == 1:   # (an rhs upload on one rank: allowed, only phi uploads are collective)
+            _poke(be, be.tree.highest_lvl, T.MG_IRHS, bad, box=len(be.my_ids(be.tree.highest_lvl)) - 1)
+        try:
+            be.vcycle(True)
+        except omg.device.OmgError as ex:
+            return str(ex)
+        return "no error"
+
+    for msg in run_loopback(args, 2, body):
+        assert "non-finite residual" in msg
 
 
 def test_max_residual_lvl_reports_nan():
@@ -113,12 +134,14 @@ def test_debug_poison_catches_an_unfilled_ghost(monkeypatch):
 
 
 @pytest.mark.parametrize("fail_at", [1, 2])
-@pytest.mark.parametrize("name", ["c1_gsrb_v", "u64_box16_gsrb_d0_one"])
+@pytest.mark.parametrize("name", ["c1_gsrb_v", "u64_box16_gsrb_d0_one", "c2_256_box16_gs_d0"])
 def test_graph_failure_rolls_back(name, fail_at, monkeypatch):
     """OMG_GRAPH_FAIL injects one failure into the first captured cycle: 1 before
     the cycle's host logic runs, 2 after it ran (host state changed, graph
     never launched).  The call fails, nothing on the device changed, and the
-    cycles after it reproduce the reference's history and final phi."""
+    cycles after it reproduce the reference's history and final phi.  The
+    256^3 GS case runs the register-ring sweep, whose ring-order rhs copy the
+    failed capture had marked built without running it."""
     monkeypatch.setenv("OMG_GRAPH", "1")
     monkeypatch.setenv("OMG_GRAPH_FAIL", str(fail_at))
     e = GOLDEN[name]

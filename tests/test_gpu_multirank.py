@@ -9,7 +9,7 @@ import os
 
 import pytest
 
-from tests.mgdriver import run_problem, run_problem_loopback
+from tests.mgdriver import omg, run_loopback, run_problem, run_problem_loopback
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
 MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if not e.get("big") for r in e["runs"] if int(r) > 1]
@@ -18,6 +18,14 @@ MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if not e.get("big") for 
 BIG_MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if e.get("big") for r in e["runs"] if int(r) > 1]
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _check_collective(monkeypatch):
+    """Every multi-rank run here also agrees, over the transport, on the
+    decisions the library makes without communication (the stand-alone fill
+    skip) and fails if a rank differs (OMG_CHECK_COLLECTIVE)."""
+    monkeypatch.setenv("OMG_CHECK_COLLECTIVE", "1")
 
 
 def _check(out, run):
@@ -75,3 +83,54 @@ def test_multirank_fused_down_step_phi_matches_oracle(name, ranks):
     orc = run_problem(e["args"], backend="oracle", n_ranks=ranks)
     assert orc["history"] == out["history"]
     assert out["phi_sha256"] == orc["phi_sha256"]
+
+
+# The bench's c4_refined configuration (GSRB, box 16, one refined level,
+# callback Dirichlet) at 3 and 4 ranks with the bench's coarse replication
+# bound (64 boxes of 16^3): refinement boundaries across ranks, history and
+# every box's final phi against the reference's own multi-rank runs.
+@pytest.mark.parametrize("ranks", [3, 4])
+def test_c4_refined_gsrb_bench_replication(ranks):
+    e = GOLDEN["c4_ref2_box16_gsrb"]
+    out = run_problem_loopback(e["args"], ranks, rep_cells=64 * 16 ** 3)
+    _check(out, e["runs"][str(ranks)])
+
+
+# C2 with lexicographic GS at its own size on 2 and 8 ranks: the register-ring
+# sweep and k_fill_tile_xl with faces on other ranks (packed into the halo
+# send buffer from the partly staged box).  Dirichlet histories and phi do not
+# depend on the rank count (each box reads only ghosts frozen since
+# the last fill), so the reference's one-rank run is the expected result.
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_c2_gs_ring_multirank_matches_reference(ranks):
+    e = GOLDEN["c2_256_box16_gs_d0"]
+    out = run_problem_loopback(e["args"], ranks)
+    _check(out, e["runs"]["1"])
+
+
+# Round 4: a multi-rank stand-alone V-cycle no longer waits for the GPU on the
+# host (round 3 agreed on the fill skip with an all-gather + stream
+# synchronisation every cycle).  Dirichlet (no periodic mean, which the
+# loopback transport gathers on the host), without max_res: zero waits per
+# cycle; with max_res: one (the residual read back, m_multigrid.f90:226-234).
+@pytest.mark.parametrize("args,ranks", [("16 64 64 64 3 v gsrb lpl 0 d0 sol 1 lb 0", 2),
+                                        ("16 128 128 128 3 v gsrb lpl 0 sol sol 2 lb 0", 4),
+                                        ("16 64 64 64 3 v gs lpl 0 d0 sol 1 lb 0", 8)])
+def test_multirank_vcycle_makes_no_host_wait(args, ranks, monkeypatch):
+    monkeypatch.delenv("OMG_CHECK_COLLECTIVE")   # (its agreement waits on the host by design)
+
+    def body(be, rank, reduce):
+        ctx = be.mg.ctx
+        omg.mg_fas_vcycle(be.mg)          # the first cycle fills (uploads dropped the ghosts)
+        n0 = ctx.host_sync_count()
+        for _ in range(3):
+            omg.mg_fas_vcycle(be.mg)
+        n1 = ctx.host_sync_count()
+        omg.mg_fas_vcycle(be.mg, max_res=True)
+        n2 = ctx.host_sync_count()
+        return n1 - n0, n2 - n1, ctx.comm_stream_priority()
+
+    for no_max, with_max, prio in run_loopback(args, ranks, body):
+        assert no_max == 0
+        assert with_max == 1
+        assert prio < 0   # the highest priority HIP offers (lower is higher)

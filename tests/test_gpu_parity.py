@@ -118,7 +118,9 @@ def test_smoother_with_stale_ghosts(args):
 
 
 @pytest.mark.parametrize("args", ["8 32 32 32 3 v gsrb ahelm 10 sol sol 1 lb 0",
-                                  "8 32 32 32 2 v gs ahelm 5 d0 sol 2 lb 0"])
+                                  "8 32 32 32 2 v gs ahelm 5 d0 sol 2 lb 0",
+                                  # box 16 (the tiled aniso kernels C5-aniso runs)
+                                  "16 128 128 128 2 v gsrb ahelm 10 sol sol 1 lb 0"])
 def test_ahelm_smoother_matches_oracle(args):
     """The aniso-Helmholtz V-cycle: the reference's 3D box_gs_ahelmh is broken
     (a0(4:5), m_ahelmholtz.f90:145 -> NaN), so the device is held bit for bit
