@@ -138,6 +138,46 @@ struct Tree {
   }
 };
 
+// Level::d_topo, the per-box face words the tiled kernels load once
+// (FaceTopo, omg_face.h), from the host tables; rebuilt when they change
+// (phi_bc_store rewrites the physical faces' codes)
+void pack_topo(Level& L) {
+  if (!L.n) return;
+  std::vector<int> w((size_t)L.n * 8, 0);
+  auto put = [](int kind, long long arg) {
+    if (arg < 0 || arg >= (1ll << 29)) throw OmgError("pack_topo: face argument out of range");
+    return (int)(((unsigned)kind << 29) | (unsigned)arg);
+  };
+  for (int b = 0; b < L.n; b++) {
+    unsigned nonlocal = 0;
+    for (int f = 0; f < 6; f++) {
+      const size_t i = (size_t)b * 6 + f;
+      const int kind = L.h_nbk[i];
+      long long arg = 0;
+      if (kind == NB_LOCAL) {
+        arg = L.h_nba[i];
+      } else if (kind == NB_PHYS) {
+        arg = -(long long)L.h_nba[i];
+      } else if (kind == NB_REMOTE) {
+        arg = L.h_sendpos[i];
+      } else if (kind == NB_RB) {
+        const RBRec& r = L.h_rb[L.h_nba[i]];
+        if (r.coarse_idx < 0 || r.coarse_idx >= (1 << 25)) throw OmgError("pack_topo: coarse index out of range");
+        arg = r.coarse_idx;
+        for (int d = 0; d < 3; d++) {
+          if (r.dix[d] != 0 && r.dix[d] != L.nc / 2) throw OmgError("pack_topo: child offset not 0 or nc/2");
+          arg |= (long long)(r.dix[d] != 0) << (25 + d);
+        }
+      }
+      if (kind != NB_LOCAL) nonlocal |= 1u << f;
+      w[(size_t)b * 8 + f] = put(kind, arg);
+    }
+    w[(size_t)b * 8 + 6] = (int)nonlocal;
+  }
+  dfree(L.d_topo);
+  L.d_topo = to_device(w);
+}
+
 Level* level_ptr(omg_ctx* c, int l) {
   auto it = c->levels.find(l);
   return it == c->levels.end() ? nullptr : &it->second;
@@ -1540,6 +1580,7 @@ void phi_bc_store(omg_ctx* c) {
       for (int nb = 1; nb <= 6; nb++)
         if (L.h_nbk[(size_t)b * 6 + nb - 1] == NB_PHYS)
           c->neighbors[(size_t)(L.ids[b] - 1) * 6 + nb - 1] = L.h_nba[(size_t)b * 6 + nb - 1];
+    pack_topo(L);
   }
   c->phi_bc_data_stored = 1;
 }
@@ -1876,6 +1917,7 @@ void free_levels(omg_ctx* c) {
   for (auto& kv : c->levels) {
     Level& L = kv.second;
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
+    dfree(L.d_topo);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
@@ -2084,6 +2126,8 @@ void build_plan(omg_ctx* c) {
     L.d_nbk = to_device(L.h_nbk);
     L.d_nba = to_device(L.h_nba);
     L.d_rb = to_device(L.h_rb);
+    L.h_sendpos = sendpos;
+    pack_topo(L);
     // parents / leaves (my_parents, my_leaves) as local indices
     for (int id : c->parents[l])
       if (owns(id)) L.parents.push_back(c->local_index[id]);

@@ -55,6 +55,32 @@ __device__ __forceinline__ void pair_stencil(const double* so, const double* gb,
 }
 
 
+// The face topology of one box (Level::d_topo): per face the kind (NbKind,
+// bits 29-31) and a 29-bit argument: NB_LOCAL the neighbour's local index,
+// NB_PHYS minus the boundary code of the neighbour slot, NB_REMOTE the halo
+// send slot, NB_RB the coarse neighbour's local index (bits 0-24) and the
+// child offset halves (bits 25-27: x, y, z), NB_RBREM none; word 6 = mask of
+// the non-local faces.  A box program loads it once, first: 32 B from a
+// uniform address before any store, i.e. two scalar loads that complete
+// while the bulk loads stream, so the epilogue's pushes and ghost fills find
+// every face's kind and target in registers (before round 4 they issued
+// dependent loads of nbk / nba after the update).
+struct FaceTopo {
+  int w[8];
+  __device__ __forceinline__ int kind(int f) const { return (int)((unsigned)w[f] >> 29); }
+  __device__ __forceinline__ int arg(int f) const { return w[f] & 0x1fffffff; }
+  __device__ __forceinline__ int phys_code(int f) const { return -arg(f); }
+  __device__ __forceinline__ unsigned nonlocal() const { return (unsigned)w[6]; }
+};
+__device__ __forceinline__ FaceTopo load_topo(const LevelView& L, int b) {
+  const int4* p = reinterpret_cast<const int4*>(L.topo) + 2 * (long long)b;
+  const int4 x = p[0], y = p[1];
+  FaceTopo t;
+  t.w[0] = x.x; t.w[1] = x.y; t.w[2] = x.z; t.w[3] = x.w;
+  t.w[4] = y.x; t.w[5] = y.y; t.w[6] = y.z; t.w[7] = y.w;
+  return t;
+}
+
 // Bijective blockIdx -> box map giving each XCD one contiguous run of boxes
 // (workgroups are dealt round-robin over the 8 XCDs), so Morton-close
 // neighbour boxes share an L2.  rev: each XCD walks its run backwards (the
@@ -97,17 +123,17 @@ __device__ __forceinline__ double phys_ghost(const LevelView& L, const GcBC& bc,
 // cells, in the same order).  get(i, j, k) reads our (final) interior value;
 // `faces` (bit f = face f+1) limits the push to some faces.
 template <int NC, class Get>
-__device__ __forceinline__ void face_push_local(const LevelView& L, int b, int colours, Get get,
+__device__ __forceinline__ void face_push_local(const LevelView& L, const FaceTopo& T, int colours, Get get,
                                                 unsigned faces = 0x3f) {
   using TL = Tl<NC>;
   constexpr int H = TL::H, PF = TL::FH / 2;   // 16-B pairs per face half
   const int ncol = (colours & 1) + ((colours >> 1) & 1);
   const int c_first = (colours & 1) ? 0 : 1;
+  faces &= ~T.nonlocal();
   for (int p = threadIdx.x; p < 6 * PF * ncol; p += blockDim.x) {
     const int f = p / (PF * ncol), rem = p % (PF * ncol);
     const int col = ncol == 2 ? rem / PF : c_first, r = rem % PF;
-    const long long fidx = (long long)b * 6 + f;
-    if (L.nbk[fidx] != NB_LOCAL || !(faces >> f & 1)) continue;
+    if (!(faces >> f & 1)) continue;
     const int nb = f + 1;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, x1 = low ? 1 : NC;
@@ -121,7 +147,7 @@ __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int c
       else v[s] = get(a, c, x1);
     }
     const int nbo = low ? nb + 1 : nb - 1;
-    v2d* dst = reinterpret_cast<v2d*>(L.phi + (long long)L.nba[fidx] * L.stride + 2 * TL::HV +
+    v2d* dst = reinterpret_cast<v2d*>(L.phi + (long long)T.arg(f) * L.stride + 2 * TL::HV +
                                       (nbo - 1) * TL::FS + col * TL::FH) + r;
     // default cache policy even in the streaming kernels: measured 5 % faster
     // per substep than non-temporal stores for these 1-KB face halves
@@ -133,19 +159,22 @@ __device__ __forceinline__ void face_push_local(const LevelView& L, int b, int c
 // (Tl<NC> layout): same-GPU faces pushed (colours mask), physical ghosts
 // recomputed, remote faces packed.  rb_ghost(arg, nb, a, c, x1, x2):
 // refinement-boundary faces (NB_RB) too, from the fine box's own boundary
-// cells and the coarse level (sides_rb); null: the level has none.
+// cells and the coarse level (sides_rb; arg = the FaceTopo argument); null:
+// the level has none.
 template <int NC, class RbGhost = std::nullptr_t>
-__device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const double* sb, int colours,
-                                               const GcBC& bc, double* sendbuf, const RbGhost& rb_ghost = nullptr) {
+__device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const FaceTopo& T, const double* sb,
+                                               int colours, const GcBC& bc, double* sendbuf,
+                                               const RbGhost& rb_ghost = nullptr) {
   using TL = Tl<NC>;
-  face_push_local<NC>(L, b, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
+  face_push_local<NC>(L, T, colours, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
+  if (!T.nonlocal()) return;
   double* u = L.phi + (long long)b * L.stride;
   for (int p = threadIdx.x; p < 6 * NC * NC; p += blockDim.x) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
     const long long fidx = (long long)b * 6 + nb - 1;
-    const int kind = L.nbk[fidx];
+    const int kind = T.kind(nb - 1);
     if (kind == NB_LOCAL) continue;
-    const int a = cell % NC + 1, c = cell / NC + 1, arg = L.nba[fidx];
+    const int a = cell % NC + 1, c = cell / NC + 1, arg = T.arg(nb - 1);
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, x1 = low ? 1 : NC, x2 = low ? 2 : NC - 1;
     int i1, j1, k1;
@@ -154,11 +183,11 @@ __device__ __forceinline__ void tile_face_fill(const LevelView& L, int b, const 
     else { i1 = a; j1 = c; k1 = x1; }
     const double v1 = sb[TL::oint(i1, j1, k1)];
     if (kind == NB_REMOTE) {
-      sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
+      sendbuf[(long long)arg * NC * NC + (a - 1) + NC * (c - 1)] = v1;
     } else if (kind == NB_PHYS) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const int gi = TL::ogh(nb, a, c);
-      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, sb[TL::oint(i2, j2, k2)]);
+      u[gi] = phys_ghost(L, bc, b, fidx, nb, -arg, a, c, gi, v1, sb[TL::oint(i2, j2, k2)]);
     } else if constexpr (!std::is_same<RbGhost, std::nullptr_t>::value) {
       if (kind == NB_RB) {
         const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;

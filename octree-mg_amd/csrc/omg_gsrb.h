@@ -74,9 +74,18 @@ __device__ __forceinline__ double rb_ghost_from(const RbCoarse& t, int a, int c,
   gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
   return 0.5 * gv + 0.75 * v1 - 0.25 * v2;
 }
-__device__ __forceinline__ double rb_ghost(const LevelView& L, const RbSide& R, int arg, int nb, int a, int c,
+// the RBRec of an NB_RB face from its FaceTopo argument (coarse index in bits
+// 0-24, child offset halves in bits 25-27; pack_topo)
+__device__ __forceinline__ RBRec rb_unpack(const LevelView& L, int targ) {
+  RBRec r;
+  r.coarse_idx = targ & 0x1ffffff;
+#pragma unroll
+  for (int d = 0; d < 3; d++) r.dix[d] = ((targ >> (25 + d)) & 1) * (L.nc >> 1);
+  return r;
+}
+__device__ __forceinline__ double rb_ghost(const LevelView& L, const RbSide& R, int targ, int nb, int a, int c,
                                            double v1, double v2) {
-  return rb_ghost_from(rb_coarse_load(L, R, R.rb[arg], nb, a, c), a, c, v1, v2);
+  return rb_ghost_from(rb_coarse_load(L, R, rb_unpack(L, targ), nb, a, c), a, c, v1, v2);
 }
 
 // Variable-coefficient operators read eps (var 5; vars 5..7 for the
@@ -175,25 +184,17 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   const long long boff = (long long)b * L.stride;
   double* __restrict__ u = L.phi + boff;
   const OpCoef<OP> K(L, lambda);
+  // the box's face kinds and targets (scalar loads, complete during the
+  // stream-in; the pushes and the ghost fill below read them from registers)
+  const FaceTopo T = load_topo(L, b);
 
-  // Refinement-boundary faces: the face kinds and records are issued first,
-  // the coarse operands after the stream-in (below), so the ghost fill after
-  // the substep finds them in registers instead of running three dependent
-  // loads (kind -> record -> coarse cells) at the end.
+  // Refinement-boundary faces: the coarse operands are issued right after
+  // the stream-in (below), so the ghost fill after the substep finds them in
+  // registers (the face's coarse box and child offset are in T: one level of
+  // loads instead of kind -> record -> coarse cells).
   constexpr bool RBP = RB && OMG_RB_PRE;
   constexpr int NF = 6 * NC * NC, NPF = RBP ? (NF + BS - 1) / BS : 1;
-  int rkind[NPF], rarg[NPF];
-  RBRec rrec[NPF];
   RbCoarse rt[NPF];
-  if constexpr (RBP) {
-#pragma unroll
-    for (int r = 0; r < NPF; r++) {
-      const int p = tid + BS * r;
-      const long long fidx = (long long)b * 6 + (p < NF ? p / (NC * NC) : 0);
-      rkind[r] = p < NF ? L.nbk[fidx] : NB_LOCAL;
-      rarg[r] = p < NF ? L.nba[fidx] : 0;
-    }
-  }
 
   // ---- stream in: colour 1-e, its ghost halves, colour e of rhs ----------
   if (!PRE) {
@@ -228,18 +229,15 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   const double2* fr = frs.v;
   if constexpr (RBP) {
 #pragma unroll
-    for (int r = 0; r < NPF; r++)
-      if (rkind[r] == NB_RB) rrec[r] = rbs->rb[rarg[r]];
-  }
-  __syncthreads();
-  if constexpr (RBP) {
-#pragma unroll
     for (int r = 0; r < NPF; r++) {
-      if (rkind[r] != NB_RB) continue;
-      const int p = tid + BS * r, cell = p % (NC * NC);
-      rt[r] = rb_coarse_load(L, *rbs, rrec[r], p / (NC * NC) + 1, cell % NC + 1, cell / NC + 1);
+      const int p = tid + BS * r;
+      if (p >= NF) continue;
+      const int f = p / (NC * NC), cell = p % (NC * NC);
+      if (T.kind(f) != NB_RB) continue;
+      rt[r] = rb_coarse_load(L, *rbs, rb_unpack(L, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
     }
   }
+  __syncthreads();
 
   // ---- colour e update ----------------------------------------------------
   // Each thread updates two neighbouring cells of one row (colour indices ih,
@@ -321,10 +319,12 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     const int idx = ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
     return ((i + j + k) & 1) == e ? se[idx] : so[idx];
   };
-  face_push_local<NC>(L, b, colours, cellv, (OMG_T_YZ & 1) ? 0x3u : 0x3fu);
-  auto fill_cell = [&](int p, int kind, int arg, const RbCoarse* rc) {
-    if (kind == NB_LOCAL) return;
+  face_push_local<NC>(L, T, colours, cellv, (OMG_T_YZ & 1) ? 0x3u : 0x3fu);
+  if (!T.nonlocal()) return;
+  auto fill_cell = [&](int p, const RbCoarse* rc) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
+    const int kind = T.kind(nb - 1), arg = T.arg(nb - 1);
+    if (kind == NB_LOCAL) return;
     const long long fidx = (long long)b * 6 + nb - 1;
     const int a = cell % NC + 1, c = cell / NC + 1;
     const bool low = nb & 1;
@@ -337,11 +337,11 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     else { i1 = a; j1 = c; k1 = x1; }
     const double v1 = cellv(i1, j1, k1);
     if (kind == NB_REMOTE) {
-      sendbuf[(long long)L.sendpos[fidx] * NC * NC + (a - 1) + NC * (c - 1)] = v1;
+      sendbuf[(long long)arg * NC * NC + (a - 1) + NC * (c - 1)] = v1;
     } else if (kind == NB_PHYS) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const int gi = off_gh(L, nb, a, c);
-      u[gi] = phys_ghost(L, bc, b, fidx, nb, arg, a, c, gi, v1, cellv(i2, j2, k2));
+      u[gi] = phys_ghost(L, bc, b, fidx, nb, -arg, a, c, gi, v1, cellv(i2, j2, k2));
     } else if (RB && kind == NB_RB) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const double v2 = cellv(i2, j2, k2);
@@ -351,13 +351,9 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   if constexpr (RBP) {
 #pragma unroll
     for (int r = 0; r < NPF; r++)
-      if (tid + BS * r < NF) fill_cell(tid + BS * r, rkind[r], rarg[r], &rt[r]);
+      if (tid + BS * r < NF) fill_cell(tid + BS * r, &rt[r]);
   } else {
-    for (int p = tid; p < NF; p += BS) {
-      const long long fidx = (long long)b * 6 + p / (NC * NC);
-      const int kind = L.nbk[fidx];
-      if (kind != NB_LOCAL) fill_cell(p, kind, L.nba[fidx], nullptr);
-    }
+    for (int p = tid; p < NF; p += BS) fill_cell(p, nullptr);
   }
 }
 

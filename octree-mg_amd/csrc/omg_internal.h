@@ -54,6 +54,7 @@ struct LevelView {
   const int8_t* nbk;     // [n*6]
   const int* nba;        // [n*6]
   const int* sendpos;    // [n*6] halo send slot of remote faces (or -1)
+  const int* topo;       // [n*8] packed face kinds + arguments (FaceTopo, omg_face.h; pack_topo)
   int rev;               // walk each XCD's run of boxes backwards (xcd_box)
 };
 
@@ -110,6 +111,11 @@ struct Level {
   int8_t* d_nbk = nullptr;
   int* d_nba = nullptr;
   int* d_sendpos = nullptr;
+  std::vector<int> h_sendpos;
+  // per box 8 words: the 6 faces' kind + argument packed (FaceTopo in
+  // omg_face.h, built by pack_topo from h_nbk / h_nba / h_sendpos / h_rb),
+  // word 6 = mask of the faces that are not same-GPU neighbours
+  int* d_topo = nullptr;
   std::vector<int8_t> h_nbk;
   std::vector<int> h_nba;
   // refinement boundary records (fine side)
@@ -172,6 +178,7 @@ struct Level {
     v.nbk = d_nbk;
     v.nba = d_nba;
     v.sendpos = d_sendpos;
+    v.topo = d_topo;
     v.rev = 0;
     return v;
   }

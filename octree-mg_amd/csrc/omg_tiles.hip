@@ -230,6 +230,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
   __shared__ double sb[TL::NST];
   const int tid = threadIdx.x, bq = xcd_box(blockIdx.x, gridDim.x, F.rev), b = list ? list[bq] : bq;
+  const FaceTopo T = load_topo(F, b);
   const long long boff = (long long)b * F.stride;
   double* __restrict__ u = F.phi + boff;
   const double* __restrict__ f = F.data + F.vstride + boff;
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
     const int d = (nb - 1) >> 1, nl = low ? NC : 1;
-    const long long noff = (long long)F.nba[(long long)b * 6 + nb - 1] * F.stride;
+    const long long noff = (long long)T.arg(nb - 1) * F.stride;
     const double* un = F.phi + noff;
     gdeep[g] = un[sr_int<NC>(d, low ? NC - 1 : 2, a, c)];
     grhs[g] = F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)];
@@ -319,7 +320,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   }
   __syncthreads();
   // our new colour-0 boundary cells to the neighbours' colour-0 ghost halves
-  face_push_local<NC>(F, b, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
+  face_push_local<NC>(F, T, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; });
   resid_restrict_core<NC, OP, BS>(F, Cv, lambda, nullptr, restrict_on, parent_local, dixp, b, sb, fr);
 }
 
@@ -389,11 +390,10 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
   double* cb = lds;                     // the parent's octant + one face layer around it
   double* sb = lds + prolong_cb<NC>();  // the corrected fine interior
   const int tid = threadIdx.x;
+  const FaceTopo T = load_topo(F, b);
   const int pb = parent_local[b], dp = dixp[b];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20;
-  bool only0 = skip1;
-#pragma unroll
-  for (int nb = 0; nb < 6; nb++) only0 = only0 && F.nbk[(long long)b * 6 + nb] == NB_LOCAL;
+  const bool only0 = skip1 && !T.nonlocal();
   const int npair = only0 ? HV / 2 : HV;
   double* __restrict__ u = F.phi + (long long)b * F.stride;
   v2d old[NR];
@@ -433,12 +433,12 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     // correction came from (fill_refinement_bnd + sides_rb, m_ghost_cells.f90:
     // 287-328, 769-861), now final for this up-step
     const RbSide rbs{Cv, rb};
-    tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf,
+    tile_face_fill<NC>(F, b, T, sb, only0 ? 1 : 3, bc, sendbuf,
                        [&](int arg, int nb, int a, int c, double v1, double v2) {
                          return rb_ghost(F, rbs, arg, nb, a, c, v1, v2);
                        });
   } else {
-    tile_face_fill<NC>(F, b, sb, only0 ? 1 : 3, bc, sendbuf);
+    tile_face_fill<NC>(F, b, T, sb, only0 ? 1 : 3, bc, sendbuf);
   }
 }
 
@@ -496,15 +496,17 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   double* sg = lds + 2 * HV;            // colour-0 ghost halves, 6 x FH
   double* cb = sg;                      // parent octant + face layer (res), until phase 3
   const int tid = threadIdx.x;
+  const FaceTopo T = load_topo(F, b);
   const int pb = parent_local[b], dp = dixp[b];
   const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
+  const FaceTopo TP = load_topo(Cv, pb);   // the parent's neighbours
   // The substep overwrites colour 1 without reading it (gs_value has no
   // centre term), so colour 1's corrected values are dead, except where a
   // physical face's colour-0 ghost takes its boundary cell x1 (bc_to_gc).
   // Boxes without a physical face prolong colour 0 only.
   bool phys = false;
 #pragma unroll
-  for (int nb = 0; nb < 6; nb++) phys |= F.nbk[(long long)b * 6 + nb] == NB_PHYS;
+  for (int nb = 0; nb < 6; nb++) phys |= T.kind(nb) == NB_PHYS;
   const int npair = phys ? HV : HV / 2;
   // all loads that do not depend on LDS first (colour 0; a physical-face box
   // reads its colour 1 when it corrects it)
@@ -541,8 +543,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     gv[g] = 0.0;
     if (q >= 6 * FH) continue;
     const int nb = q / FH + 1, rr = q % FH;
-    const long long fidx = (long long)b * 6 + nb - 1;
-    if (F.nbk[fidx] != NB_LOCAL) continue;
+    if (T.kind(nb - 1) != NB_LOCAL) continue;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
     const int c = rr / HN + 1, ah = rr % HN;
@@ -564,7 +565,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       defm |= 1u << g;
       const bool sib = low ? dix[d - 1] == HN : dix[d - 1] == 0;
       if (sib) continue;
-      const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
+      const int pn = TP.arg(nb - 1);
       const int da = d == 1 ? 1 : 0, dc = d == 3 ? 1 : 2;   // tangential dims of a and c
       const int pa = (a + 1) >> 1, pc = (c + 1) >> 1;
       const int oa_ = da == 0 ? dix[0] : dix[1], oc_ = dc == 1 ? dix[1] : dix[2];   // octant offsets
@@ -584,7 +585,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       continue;
     }
     int nd[3] = {dix[0], dix[1], dix[2]};
-    const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
+    const int pn = TP.arg(nb - 1);
     nd[d - 1] = 0;
     if (og_lds) {
       gv[g] = prolong_at<NC>(Cv, pn, nd, fi, fj, fk);
@@ -653,7 +654,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   // another GPU, push0 = the faces toward them): they read our corrected
   // colour 0 from their ghost halves
   if (push0 && push0[b])
-    face_push_local<NC>(F, b, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; }, push0[b]);
+    face_push_local<NC>(F, T, 1, [&](int i, int j, int k) { return sb[TL::oint(i, j, k)]; }, push0[b]);
   // ---- colour-0 ghost values the substep reads (physical faces from the
   // corrected boundary cells: bc_to_gc)
 #pragma unroll
@@ -662,7 +663,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     if (q >= 6 * FH) continue;
     const int nb = q / FH + 1, rr = q % FH;
     const long long fidx = (long long)b * 6 + nb - 1;
-    const int kind = F.nbk[fidx];
+    const int kind = T.kind(nb - 1);
     if (kind == NB_PHYS) {
       const bool low = nb & 1;
       const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
@@ -674,7 +675,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
       else { i1 = a; j1 = c; k1 = x1; }
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
-      gv[g] = phys_ghost(F, bc, b, fidx, nb, F.nba[fidx], a, c, TL::ogh(nb, a, c), sb[TL::oint(i1, j1, k1)],
+      gv[g] = phys_ghost(F, bc, b, fidx, nb, T.phys_code(nb - 1), a, c, TL::ogh(nb, a, c), sb[TL::oint(i1, j1, k1)],
                          sb[TL::oint(i2, j2, k2)]);
     }
     sg[(nb - 1) * FH + rr] = gv[g];
@@ -887,10 +888,11 @@ __global__ void __launch_bounds__(BS) k_fill_tile(LevelView L, GcBC bc, double* 
   constexpr int HV = Tl<NC>::HV;
   __shared__ double sb[2 * HV];
   const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
+  const FaceTopo T = load_topo(L, b);
   const double* u = L.phi + (long long)b * L.stride;
   for (int q = threadIdx.x; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
   __syncthreads();
-  tile_face_fill<NC>(L, b, sb, 3, bc, sendbuf);
+  tile_face_fill<NC>(L, b, T, sb, 3, bc, sendbuf);
 }
 
 // k_fill_tile after a register-ring GS sweep.  tile_face_fill reads only the
@@ -907,10 +909,11 @@ __global__ void __launch_bounds__(BS) k_fill_tile_xl(LevelView L, GcBC bc, doubl
   constexpr int HV = TL::HV, H = NC / 2, FH = H * NC;
   __shared__ double sb[2 * HV];
   const int b = xcd_box(blockIdx.x, gridDim.x, L.rev);
+  const FaceTopo T = load_topo(L, b);
   const double* u = L.phi + (long long)b * L.stride;
   bool phys = false;
 #pragma unroll
-  for (int nb = 0; nb < 6; nb++) phys |= L.nbk[(long long)b * 6 + nb] == NB_PHYS;
+  for (int nb = 0; nb < 6; nb++) phys |= T.kind(nb) == NB_PHYS;
   if (phys) {
     for (int q = threadIdx.x; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
   } else {
@@ -935,7 +938,7 @@ __global__ void __launch_bounds__(BS) k_fill_tile_xl(LevelView L, GcBC bc, doubl
     }
   }
   __syncthreads();
-  tile_face_fill<NC>(L, b, sb, 3, bc, sendbuf);
+  tile_face_fill<NC>(L, b, T, sb, 3, bc, sendbuf);
 }
 
 void launch_fill_tile_xl(const LevelView& L, const GcBC& bc, double* sendbuf, const double* xl, hipStream_t st) {
