@@ -563,6 +563,35 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // fill after each sweep stages 12 KB per box instead of 32 (no
     // refinement boundaries on the level; OMG_NO_FILL_XL: the plain fill)
     const bool xlf = plane && !c->gs_lex_plane && L->d_xlay && !L->has_rb && !c->no_fill_tile && !c->no_fill_xl;
+    // Round 4: an even number of ring sweeps on a level whose faces are
+    // same-GPU or physical runs with no fill in between: sweep n reads the
+    // ghost set sweep n-1 pushed into (the box storage's own faces for odd
+    // n, d_galt for even n, whose physical ghosts it forms at load), so the
+    // last sweep lands in the box storage and only the physical ghosts are
+    // left to form (k_phys_gc).  The reference fills after every sweep
+    // (m_multigrid.f90:412-423): the same values reach the same ghosts
+    // before every read.  OMG_NO_GS_DBL: the fill after every sweep.
+    if (xlf && L->d_galt && n_sub % 2 == 0 && L->n && !c->no_gs_dbl) {
+      const GcBC bc = bc_for(c, lvl, 1);
+      double* prim = L->d_phi + 2 * (long long)L->view().hv;
+      for (int n = 1; n <= n_sub; n++) {
+        const bool odd = n & 1;
+        GhostSets gs;
+        gs.in = odd ? prim : L->d_galt;
+        gs.in_stride = odd ? L->stride : 6 * (long long)stored_face(L->nc);
+        gs.out = odd ? L->d_galt : prim;
+        gs.out_stride = odd ? 6 * (long long)stored_face(L->nc) : L->stride;
+        gs.phys_load = !odd;
+        Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, L->d_rhs_lex, true, nullptr, &gs, &bc);
+      }
+      if (L->n_physbox) {
+        Prof p(c, "fill_gc", (double)L->n_physbox * 6 * L->nc * L->nc, lvl);
+        launch_phys_gc(L->view(), bc, L->d_physbox, L->n_physbox, c->stream);
+      }
+      L->phi_gc_ok = true;
+      return;
+    }
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
@@ -1057,12 +1086,14 @@ void ensure_rhs_lex(omg_ctx* c) {
       if (L.d_rhs_lex || L.d_xlay) HIPCHK(hipStreamSynchronize(c->stream));   // (in use by queued sweeps)
       dfree(L.d_rhs_lex);
       dfree(L.d_xlay);
+      dfree(L.d_galt);
       L.rhs_lex_ok = false;
       continue;
     }
     if (L.d_rhs_lex) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
     dmalloc(&L.d_xlay, sizeof(double) * L.n * 2 * L.nc * L.nc);
+    if (!L.has_remote && !L.has_rb) dmalloc(&L.d_galt, sizeof(double) * L.n * 6 * (size_t)stored_face(L.nc));
     L.rhs_lex_ok = false;
   }
 }
@@ -1922,6 +1953,8 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
+    dfree(L.d_galt);
+    dfree(L.d_physbox);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
@@ -2093,6 +2126,17 @@ void build_plan(omg_ctx* c) {
     L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
+    {
+      std::vector<int> pb;
+      for (int b = 0; b < L.n; b++)
+        for (int nb = 0; nb < 6; nb++)
+          if (L.h_nbk[(size_t)b * 6 + nb] == NB_PHYS) {
+            pb.push_back(b);
+            break;
+          }
+      L.n_physbox = (int)pb.size();
+      L.d_physbox = to_device(pb);
+    }
     L.any_rb = L.any_phys = false;
     for (int id : c->ids[l])
       for (int nb = 1; nb <= 6; nb++) {
@@ -2310,6 +2354,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
     c->gs_lex_plane = env_flag("OMG_GS_LEX_PLANE");
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
+    c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");

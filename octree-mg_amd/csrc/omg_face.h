@@ -66,18 +66,24 @@ __device__ __forceinline__ void pair_stencil(const double* so, const double* gb,
 // every face's kind and target in registers (before round 4 they issued
 // dependent loads of nbk / nba after the update).
 struct FaceTopo {
-  int w[8];
-  __device__ __forceinline__ int kind(int f) const { return (int)((unsigned)w[f] >> 29); }
-  __device__ __forceinline__ int arg(int f) const { return w[f] & 0x1fffffff; }
+  // two int4 values, not an int array: a runtime index into an array (even
+  // through a select chain, which the compiler folds into one address)
+  // keeps it in scratch memory (ScratchSize 36 in every tiled kernel)
+  int4 x, y;
+  __device__ __forceinline__ int word(int f) const {
+    const int a = f & 1 ? x.y : x.x, c = f & 1 ? x.w : x.z, e = f & 1 ? y.y : y.x;
+    return f < 2 ? a : (f < 4 ? c : e);
+  }
+  __device__ __forceinline__ int kind(int f) const { return (int)((unsigned)word(f) >> 29); }
+  __device__ __forceinline__ int arg(int f) const { return word(f) & 0x1fffffff; }
   __device__ __forceinline__ int phys_code(int f) const { return -arg(f); }
-  __device__ __forceinline__ unsigned nonlocal() const { return (unsigned)w[6]; }
+  __device__ __forceinline__ unsigned nonlocal() const { return (unsigned)y.z; }
 };
 __device__ __forceinline__ FaceTopo load_topo(const LevelView& L, int b) {
   const int4* p = reinterpret_cast<const int4*>(L.topo) + 2 * (long long)b;
-  const int4 x = p[0], y = p[1];
   FaceTopo t;
-  t.w[0] = x.x; t.w[1] = x.y; t.w[2] = x.z; t.w[3] = x.w;
-  t.w[4] = y.x; t.w[5] = y.y; t.w[6] = y.z; t.w[7] = y.w;
+  t.x = p[0];
+  t.y = p[1];
   return t;
 }
 

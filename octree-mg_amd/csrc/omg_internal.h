@@ -58,6 +58,9 @@ struct LevelView {
   int rev;               // walk each XCD's run of boxes backwards (xcd_box)
 };
 
+// doubles of one stored ghost face (both colour halves)
+inline int stored_face(int nc) { return 2 * ((nc + 1) / 2) * nc; }
+
 // stored doubles per box and variable for box size nc (2 colours + 6 faces)
 inline int stored_cells(int nc) {
   const int h = (nc + 1) / 2;
@@ -146,6 +149,11 @@ struct Level {
   double* d_rhs_lex = nullptr;       // rhs in plane order for the lexicographic smoother (ensure_rhs_lex)
   bool rhs_lex_ok = false;           // d_rhs_lex equals rhs (dropped by every rhs writer)
   double* d_xlay = nullptr;          // x boundary layers of the last register-ring sweep (k_fill_tile_xl)
+  // the second ghost-face set of phi for chains of register-ring sweeps (6
+  // faces per box, the stored face layout; GhostSets in omg_kernels.h)
+  double* d_galt = nullptr;
+  int* d_physbox = nullptr;          // boxes with a physical face (k_phys_gc after such a chain)
+  int n_physbox = 0;
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
   int* d_int = nullptr;
   int n_bnd = 0, n_int = 0;
@@ -266,6 +274,7 @@ struct omg_ctx {
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
   bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring
   bool no_fill_xl = false;             // OMG_NO_FILL_XL: the plain tiled fill after register-ring sweeps
+  bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

@@ -47,8 +47,27 @@ void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours
 // line-per-thread kernels
 // xl (register ring only, may be null): the swept boxes' new x boundary
 // layers, 512 doubles per box, for launch_fill_tile_xl
+// Two ghost-face sets for chains of register-ring sweeps (round 4): the
+// sweep reads its ghosts from `in` and pushes its new boundary layers into
+// the same-GPU neighbours' ghosts in `out` (per box `stride` doubles, the
+// six faces laid out as in the box storage from 2*HV on), so no fill pass
+// runs between sweeps; phys_load: the physical ghosts of `in` are formed at
+// load from the box's own (final) boundary cells, as the fill after the
+// previous sweep would have (bc_to_gc).  Levels whose faces are same-GPU or
+// physical only.
+struct GhostSets {
+  const double* in;
+  long long in_stride;
+  double* out;
+  long long out_stride;
+  int phys_load;
+};
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr,
-                   bool reg = true, double* xl = nullptr);
+                   bool reg = true, double* xl = nullptr, const GhostSets* gs = nullptr,
+                   const GcBC* bc = nullptr);
+// the physical ghosts of phi of the listed boxes (bc_to_gc from the boxes'
+// final boundary cells), after a chain of ghost-set sweeps
+void launch_phys_gc(const LevelView& L, const GcBC& bc, const int* boxes, int n_boxes, hipStream_t st);
 bool gs_lex_plane_ok(int nc, int op);
 // the copy in ring order (reg) or in plane order
 void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg = true);

@@ -678,9 +678,14 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
 #ifndef OMG_T_RING
 #define OMG_T_RING 0
 #endif
-template <int OP, int PF>
+// DBL: two ghost-face sets (GhostSets, omg_kernels.h): the ghosts come from
+// gs.in (the physical ones formed here from the box's own boundary cells when
+// gs.phys_load), and the new boundary layers go to the same-GPU neighbours'
+// ghosts in gs.out instead of a fill pass after the sweep.
+template <int OP, int PF, bool DBL>
 __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl,
-                                                                 double* __restrict__ xl) {
+                                                                 double* __restrict__ xl, GhostSets gs, GcBC bc) {
+  using TL = Tl<16>;
   constexpr int NC = 16, H = 8, HV = 2048, FH = 128, FS = 256, R = kLexRing, T0 = 3, T1 = 3 * NC;
   static_assert(R % PF == 0, "the rhs ring index must repeat with the register ring");
   // stage rows of 65 doubles: the four lanes that scatter one row's cells
@@ -693,11 +698,20 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   double* __restrict__ u = boxp(L, 1, b);
   const double* __restrict__ rb = rl + (long long)b * (NC * NC * NC);
   const OpCoef<OP> K(L, lambda);
+  FaceTopo T{};
+  if (DBL) T = load_topo(L, b);
+  // this box's ghost faces (face nb at gb + (nb-1)*FS, the stored layout)
+  const double* __restrict__ gb = DBL ? gs.in + (long long)b * gs.in_stride : u + 2 * HV;
+  const bool pl = DBL && gs.phys_load;
+  // physical ghost (a, c) of face nb (bc_to_gc) from the boundary cells x1, x2
+  auto phys = [&](int nb, int a, int c, double x1, double x2) {
+    return phys_ghost(L, bc, b, (long long)b * 6 + nb - 1, nb, T.phys_code(nb - 1), a, c, TL::ogh(nb, a, c), x1, x2);
+  };
 
   // y/z ghost faces (nb = 3..6: j = 0, j = 17, k = 0, k = 17; tangential
   // (a, c) = (i, k) or (i, j)) into G[f][c-1][a-1]
   {
-    const double* gf = u + 2 * HV + 2 * FS;
+    const double* gf = gb + 2 * FS;
 #pragma unroll
     for (int n = 0; n < 8; n++) {
       const int q = l + 64 * n;                      // double pair of faces 3..6
@@ -726,8 +740,8 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       buf[n] = OMG_T_RING == 2 ? v2d{0.0, 0.0} : (OMG_GS_REG_PNT ? ld_nt(src) : *reinterpret_cast<const v2d*>(src));
     }
     const int kr = 4 * kq + r + 1;
-    const double gx0 = u[2 * HV + ((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
-    const double gx1 = u[2 * HV + FS + ((NC + 1 + j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
+    const double gx0 = gb[((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
+    const double gx1 = gb[FS + ((NC + 1 + j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
     __syncthreads();                                 // the previous line's reads of stage are done
 #pragma unroll
     for (int n = 0; n < 8; n++) {
@@ -740,9 +754,44 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
     stage[((j + kr) % R) * SR + l] = gx0;
     stage[((NC + 1 + j + kr) % R) * SR + l] = gx1;
     __syncthreads();
+    if (pl) {
+      // physical ghosts from the boundary cells in stage: x faces (this
+      // lane's own line), y faces (the lines of the j = 1, 2 / 16, 15 lanes),
+      // z faces (planes k = 1, 2 / 16, 15 arrive in lines 0, 1 / 3, 2 of
+      // groups 0 / 3: the first layer is parked in G until the second comes)
+      if (T.kind(0) == NB_PHYS)
+        stage[((j + kr) % R) * SR + l] =
+            phys(1, j, kr, stage[((1 + j + kr) % R) * SR + l], stage[((2 + j + kr) % R) * SR + l]);
+      if (T.kind(1) == NB_PHYS)
+        stage[((NC + 1 + j + kr) % R) * SR + l] =
+            phys(2, j, kr, stage[((NC + j + kr) % R) * SR + l], stage[((NC - 1 + j + kr) % R) * SR + l]);
+      const int a = (l & 15) + 1, gq = l >> 4, kg = 4 * gq + r + 1, lg = 16 * lex_grp(gq);
+      if (T.kind(2) == NB_PHYS)
+        G[kLexGPad + NC * (kg - 1) + (a - 1)] =
+            phys(3, a, kg, stage[((a + 1 + kg) % R) * SR + lg], stage[((a + 2 + kg) % R) * SR + lg + 1]);
+      if (T.kind(3) == NB_PHYS)
+        G[kLexGFace + kLexGPad + NC * (kg - 1) + (a - 1)] =
+            phys(4, a, kg, stage[((a + NC + kg) % R) * SR + lg + 15], stage[((a + NC - 1 + kg) % R) * SR + lg + 14]);
+#pragma unroll
+      for (int ii = 0; ii < 4; ii++) {
+        const int i = 4 * (l >> 4) + ii + 1;   // (i, j) of the z faces
+        double* gz0 = G + 2 * kLexGFace + kLexGPad + NC * (j - 1) + (i - 1);
+        double* gz1 = G + 3 * kLexGFace + kLexGPad + NC * (j - 1) + (i - 1);
+        const int l3 = (j - 1) + 16 * lex_grp(3);
+        if (T.kind(4) == NB_PHYS) {
+          if (r == 0) *gz0 = stage[((i + j + 1) % R) * SR + (j - 1)];
+          if (r == 1) *gz0 = phys(5, i, j, *gz0, stage[((i + j + 2) % R) * SR + (j - 1)]);
+        }
+        if (T.kind(5) == NB_PHYS) {
+          if (r == 2) *gz1 = stage[((i + j + NC - 1) % R) * SR + l3];
+          if (r == 3) *gz1 = phys(6, i, j, stage[((i + j + NC) % R) * SR + l3], *gz1);
+        }
+      }
+    }
 #pragma unroll
     for (int s = 0; s < R; s++) ring[r][s] = stage[s * SR + l];
   }
+  if (pl) __syncthreads();   // the physical y/z ghosts in G
 
   // per line: j + k; G index of the y ghost at step 0 (lanes of the low half
   // of the row read face j = 0 as lane j = 1 needs it, the others face j = 17
@@ -851,9 +900,33 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
 #pragma unroll
     for (int s = 0; s < R; s++) stage[s * SR + l] = ring[r][s];
     __syncthreads();
+    if (DBL) {
+      // the new boundary layers of line r into the same-GPU neighbours'
+      // ghosts of the other set: x faces from this lane's line, y faces from
+      // the j = 1 / 16 lanes, z faces from planes k = 1 (line 0, group 0)
+      // and k = 16 (line 3, group 3)
+      const int kr = 4 * kq + r + 1;
+      auto push = [&](int f, int a, int c, double v) {   // toward face f+1's neighbour
+        const int nbo = (f & 1) ? f : f + 2;               // the neighbour's opposite face
+        gs.out[(long long)T.arg(f) * gs.out_stride + TL::ogh(nbo, a, c) - 2 * HV] = v;
+      };
+      if (T.kind(0) == NB_LOCAL) push(0, j, kr, stage[((1 + j + kr) % R) * SR + l]);
+      if (T.kind(1) == NB_LOCAL) push(1, j, kr, stage[((NC + j + kr) % R) * SR + l]);
+      const int a = (l & 15) + 1, gq = l >> 4, kg = 4 * gq + r + 1, lg = 16 * lex_grp(gq);
+      if (T.kind(2) == NB_LOCAL) push(2, a, kg, stage[((a + 1 + kg) % R) * SR + lg]);
+      if (T.kind(3) == NB_LOCAL) push(3, a, kg, stage[((a + NC + kg) % R) * SR + lg + 15]);
+      if ((r == 0 && T.kind(4) == NB_LOCAL) || (r == 3 && T.kind(5) == NB_LOCAL)) {
+        const int ln = (j - 1) + (r == 0 ? 0 : 16 * lex_grp(3)), k0 = r == 0 ? 1 : NC;
+#pragma unroll
+        for (int ii = 0; ii < 4; ii++) {
+          const int i = 4 * (l >> 4) + ii + 1;
+          push(r == 0 ? 4 : 5, i, j, stage[((i + j + k0) % R) * SR + ln]);
+        }
+      }
+    }
     // the new x boundary layers (i = 1, i = 16) of line r, for the ghost
     // fill that follows (k_fill_tile_xl): xl[b][face][(j-1) + 16 (k-1)]
-    if (xl) {
+    if (xl && !DBL) {
       const int kr = 4 * kq + r + 1;
       double* xo = xl + (long long)b * 512 + (j - 1) + NC * (kr - 1);
       xo[0] = stage[((1 + j + kr) % R) * SR + l];
@@ -1274,6 +1347,29 @@ static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
 #endif
 bool gs_lex_plane_ok(int nc, int op) { return nc == 16 && (op == OP_LPL || op == OP_HELM); }
 
+// bc_to_gc (m_ghost_cells.f90:665-766) of phi on the physical faces of the
+// listed boxes, from their stored boundary cells: what the fill after the last
+// sweep of a ghost-set chain would still have to do (the pushes covered the
+// same-GPU faces)
+__global__ void __launch_bounds__(256) k_phys_gc(LevelView L, GcBC bc, const int* __restrict__ boxes) {
+  const int b = boxes[blockIdx.x];
+  const FaceTopo T = load_topo(L, b);
+  double* u = boxp(L, 1, b);
+  const int nc = L.nc, n2 = nc * nc;
+  for (int p = threadIdx.x; p < 6 * n2; p += blockDim.x) {
+    const int f = p / n2, nb = f + 1, a = p % nc + 1, c = (p % n2) / nc + 1;
+    if (T.kind(f) != NB_PHYS) continue;
+    const bool low = nb & 1;
+    const int x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1, gi = off_gh(L, nb, a, c);
+    u[gi] = phys_ghost(L, bc, b, (long long)b * 6 + f, nb, T.phys_code(f), a, c, gi,
+                       u[off_face_cell(L, nb, x1, a, c)], u[off_face_cell(L, nb, x2, a, c)]);
+  }
+}
+
+void launch_phys_gc(const LevelView& L, const GcBC& bc, const int* boxes, int n_boxes, hipStream_t st) {
+  if (n_boxes > 0) k_phys_gc<<<n_boxes, 256, 0, st>>>(L, bc, boxes);
+}
+
 void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg) {
   if (L.n == 0) return;
   if (L.nc != 16) throw std::runtime_error("launch_rhs_lex: 16^3 boxes only");
@@ -1295,16 +1391,26 @@ static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hi
   k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
 }
 
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg, double* xl) {
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg, double* xl,
+                   const GhostSets* gs, const GcBC* bc) {
   if (L.n == 0) return;
   if (rl) {
     if (!gs_lex_plane_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no plane-order kernel for this level");
     if (reg) {
       // one wave per box, one box per workgroup (8 per CU by their LDS)
-      if (op == OP_HELM)
-        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl, xl);
-      else
-        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF><<<L.n, 64, 0, st>>>(L, lambda, rl, xl);
+      if (gs && !bc) throw std::runtime_error("launch_gs_lex: ghost sets need the boundary conditions");
+      const GhostSets g0{nullptr, 0, nullptr, 0, 0};
+      const GcBC b0{};
+      if (gs) {
+        if (op == OP_HELM)
+          k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
+        else
+          k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
+      } else if (op == OP_HELM) {
+        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
+      } else {
+        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
+      }
       return;
     }
     if (op == OP_HELM)

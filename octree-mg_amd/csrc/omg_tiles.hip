@@ -499,7 +499,6 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   const FaceTopo T = load_topo(F, b);
   const int pb = parent_local[b], dp = dixp[b];
   const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
-  const FaceTopo TP = load_topo(Cv, pb);   // the parent's neighbours
   // The substep overwrites colour 1 without reading it (gs_value has no
   // centre term), so colour 1's corrected values are dead, except where a
   // physical face's colour-0 ghost takes its boundary cell x1 (bc_to_gc).
@@ -543,7 +542,9 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     gv[g] = 0.0;
     if (q >= 6 * FH) continue;
     const int nb = q / FH + 1, rr = q % FH;
-    if (T.kind(nb - 1) != NB_LOCAL) continue;
+    // (per-lane loads here: they are issued before any store, and the kernel
+    // has no VGPRs to spare for the face words)
+    if (F.nbk[(long long)b * 6 + nb - 1] != NB_LOCAL) continue;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
     const int c = rr / HN + 1, ah = rr % HN;
@@ -565,7 +566,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       defm |= 1u << g;
       const bool sib = low ? dix[d - 1] == HN : dix[d - 1] == 0;
       if (sib) continue;
-      const int pn = TP.arg(nb - 1);
+      const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
       const int da = d == 1 ? 1 : 0, dc = d == 3 ? 1 : 2;   // tangential dims of a and c
       const int pa = (a + 1) >> 1, pc = (c + 1) >> 1;
       const int oa_ = da == 0 ? dix[0] : dix[1], oc_ = dc == 1 ? dix[1] : dix[2];   // octant offsets
@@ -585,7 +586,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       continue;
     }
     int nd[3] = {dix[0], dix[1], dix[2]};
-    const int pn = TP.arg(nb - 1);
+    const int pn = Cv.nba[(long long)pb * 6 + nb - 1];
     nd[d - 1] = 0;
     if (og_lds) {
       gv[g] = prolong_at<NC>(Cv, pn, nd, fi, fj, fk);

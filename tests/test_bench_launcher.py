@@ -72,4 +72,9 @@ def test_cpu_baseline_timeout_leaves_no_process(tmp_path):
     out = bench.cpu_baseline([16, 16, 16], ref=str(fake), timeout=3, plan=[(2, 1, 1)])
     assert "TimeoutExpired" in out["by_ranks"]["2"]["error"]
     assert out["value"] is None
+    import time
+    for _ in range(50):   # (SIGKILL is delivered asynchronously)
+        if alive() == 0:
+            break
+        time.sleep(0.1)
     assert alive() == 0

@@ -102,7 +102,9 @@ def test_per_operation_bitwise(args):
     _assert_same(dev, orc)
 
 
-@pytest.mark.parametrize("args", [OPS_CASES[0], OPS_CASES[1], "16 64 64 64 1 v gsrb helm 2 d0 sol 1 lb 0"])
+@pytest.mark.parametrize("args", [OPS_CASES[0], OPS_CASES[1], "16 64 64 64 1 v gsrb helm 2 d0 sol 1 lb 0",
+                                  # the register ring with two ghost sets (the first sweep reads the stale set)
+                                  "16 256 256 256 1 v gs lpl 0 d0 sol 1 lb 0"])
 def test_smoother_with_stale_ghosts(args):
     """smooth_boxes right after phi was overwritten (ghosts not refilled): the
     reference reads the stale ghosts in the first substep; so must we."""

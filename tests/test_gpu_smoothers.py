@@ -6,7 +6,10 @@ inside a cycle (update_coarse rewrites the rhs of the levels below).  They
 serve 16^3 levels of at least 2048 boxes, hence the 256^3 cases;
 OMG_GS_LEX_PLANE=1 selects the plane kernel and OMG_NO_GS_PLANE=1 the
 line-per-thread kernel (both read when a context is created), which must
-agree as well."""
+agree as well.  The ring runs an even number of sweeps with two ghost-face
+sets and no fill in between (round 4; each sweep pushes its boundary layers
+into the neighbours' other set, physical ghosts formed at load, k_phys_gc
+after the last sweep); OMG_NO_GS_DBL=1 keeps the fill after every sweep."""
 import numpy as np
 import pytest
 
@@ -32,7 +35,8 @@ GS_CASES = ["16 256 256 256 1 v gs lpl 0 d0 sol 1 lb 0",
             "16 64 64 64 2 v gs lpl 0 d0 sol 1 lb 0"]
 
 
-@pytest.mark.parametrize("env", [(), ("OMG_GS_LEX_PLANE",), ("OMG_NO_GS_PLANE",)], ids=["ring", "plane", "lines"])
+@pytest.mark.parametrize("env", [(), ("OMG_NO_GS_DBL",), ("OMG_GS_LEX_PLANE",), ("OMG_NO_GS_PLANE",)],
+                         ids=["ring", "ring-fill", "plane", "lines"])
 @pytest.mark.parametrize("args", GS_CASES)
 def test_gs_rhs_changes_between_cycles(args, env, monkeypatch):
     """V-cycles, then a new rhs on the finest level (upload) and on a level
@@ -53,6 +57,25 @@ def test_gs_rhs_changes_between_cycles(args, env, monkeypatch):
         assert dev.vcycle(True) == orc.vcycle(True)
         _assert_same(dev, orc, ivs=(1, 2, 3, 4))
     assert dev.fmg(True, True) == orc.fmg(True, True)
+    _assert_same(dev, orc, ivs=(1, 2, 3, 4))
+
+
+# two ghost sets with the other physical kinds: continuous (c0) and
+# mg_phi_bc_store's stored values (the physical ghost reads rhs's ghost slot)
+@pytest.mark.parametrize("args", ["16 256 256 256 1 v gs lpl 0 c0 sol 1 lb 0",
+                                  "16 256 256 256 1 v gs helm 1.5 sol sol 1 lb 0"])
+@pytest.mark.parametrize("stored", [False, True])
+def test_gs_ghost_sets_physical_kinds(args, stored, monkeypatch):
+    dev, orc = _pair(args, monkeypatch)
+    if stored:
+        dev.mg.ctx.call("phi_bc_store")
+        orc.o.phi_bc_store()
+    for n_cycle in (2, 1, 4):   # even: ghost sets, odd: a fill after every sweep
+        hi = dev.tree.highest_lvl
+        dev.mg.ctx.call("smooth_boxes", hi, n_cycle)
+        orc.o.smooth_boxes(hi, n_cycle)
+        _assert_same(dev, orc, ivs=(1, 2))
+    assert dev.vcycle(True) == orc.vcycle(True)
     _assert_same(dev, orc, ivs=(1, 2, 3, 4))
 
 

@@ -10,3 +10,8 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   > $O/new_tests.log 2>&1 || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+R=$PWD
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/trace_C4 -o run --output-format csv \
+   -- python3 $R/tools/configs_bench.py --no-cpu --only C4) > $O/trace_C4.log 2>&1 || exit 1
+f=$(find $O/trace_C4 -name "*kernel_trace.csv" | head -1)
+python3 tools/trace_by_grid.py $f > $O/trace_C4_by_grid.txt
