@@ -219,6 +219,22 @@ int omg_comm_info(omg_ctx *ctx, int *n_ranks, int *transport);
 /* Stream / timing helpers for benchmarks. */
 int omg_synchronize(omg_ctx *ctx);
 void *omg_stream(omg_ctx *ctx);                 /* the hipStream_t all work runs on */
+/* Custom refinement-boundary ghost cells: mg%bc(nb,iv)%refinement_bnd
+ * (src/m_data_structures.f90:241, interface mg_subr_rb :364-378), which
+ * fill_refinement_bnd calls instead of sides_rb (src/m_ghost_cells.f90:
+ * 321-325).  fn runs on the host after every ghost fill of variable iv on a
+ * level with refinement-boundary faces nb (the reference calls it once per
+ * fill too), with n records: ids[n] (global box ids), nbs[n] (= nb),
+ * cgc[n][nc*nc] (box_gc_for_fine_neighbor's coarse face, first index
+ * fastest) and cc[n][(nc+2)^3] (the box's variable iv as
+ * mg%boxes(id)%cc(:,:,:,iv) stores it: the interior and the other faces'
+ * ghosts current, edges and corners 0).  fn sets the ghost cells of face nb
+ * in cc; only those come back.  fn = NULL restores sides_rb.  A compat path:
+ * each such fill waits for the GPU and copies the boxes both ways. */
+typedef void (*omg_rb_fn)(void *user, int lvl, int iv, int n, const int *ids, const int *nbs, int nc,
+                          const double *cgc, double *cc);
+int omg_set_refinement_bnd(omg_ctx *ctx, int iv, int nb, omg_rb_fn fn, void *user);
+
 /* Diagnostics (no reference counterpart): the number of times the host has
  * waited for one of the context's streams so far (a multi-rank stand-alone
  * V-cycle over RCCL waits only when max_res is requested, m_multigrid.f90:

@@ -488,16 +488,109 @@ void phi_dirty_all(omg_ctx* c) {
   for (auto& kv : c->levels) kv.second.phi_gc_ok = false;
 }
 
-// halo exchange of the faces packed by the last fill/substep kernel, then
-// fill_buffered_nb (m_ghost_cells.f90:163-174, 424-454)
-void finish_rb(omg_ctx* c, Level* L, int iv);
-void finish_halo(omg_ctx* c, Level* L, int iv) {
-  if (c->n_ranks == 1) return;
-  if (L->halo.n_send || L->halo.n_recv) {
-    exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
-    launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+// Refinement-boundary faces whose ghosts a host callback sets instead of
+// sides_rb (mg%bc(nb,iv)%refinement_bnd, fill_refinement_bnd,
+// m_ghost_cells.f90:321-325): after a fill of the level has run on the device
+// (sides_rb included), the coarse faces and the boxes go to the host, the
+// callback sets the ghosts of face nb, and they come back.  Called once per
+// fill, as the reference calls it once per fill.
+void rb_host_fixup(omg_ctx* c, Level* L, int iv) {
+  if (!c->rbh_any) return;
+  auto it = L->rbh.find(iv);
+  if (it == L->rbh.end() || it->second.n == 0) return;
+  if (c->capturing) throw OmgError("refinement_bnd host callback inside a captured cycle");
+  RbHostFaces& R = it->second;
+  const int nc = L->nc, nc2 = nc * nc;
+  const size_t per = (size_t)(nc + 2) * (nc + 2) * (nc + 2);
+  launch_rbh_gather(L->view(), view_of(c, L->lvl - 1), iv, L->d_rb, R.d_items, R.d_slot, R.n, L->d_rbrecv, R.d_cgc,
+                    R.d_cc, c->stream);
+  HIPCHK(hipMemcpyAsync(R.h_cgc, R.d_cgc, sizeof(double) * R.n * nc2, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(R.h_cc, R.d_cc, sizeof(double) * R.n * per, hipMemcpyDeviceToHost, c->stream));
+  host_sync(c, c->stream);
+  for (int q0 = 0; q0 < R.n;) {   // one call per face direction (records sorted by face)
+    int q1 = q0;
+    while (q1 < R.n && R.nbs[q1] == R.nbs[q0]) q1++;
+    const int nb = R.nbs[q0];
+    auto fn = (omg_rb_fn)c->rb_fn[iv - 1][nb - 1];
+    fn(c->rb_user[iv - 1][nb - 1], L->lvl, iv, q1 - q0, R.ids.data() + q0, R.nbs.data() + q0, nc,
+       R.h_cgc + (size_t)q0 * nc2, R.h_cc + (size_t)q0 * per);
+    q0 = q1;
   }
-  finish_rb(c, L, iv);
+  HIPCHK(hipMemcpyAsync(R.d_cc, R.h_cc, sizeof(double) * R.n * per, hipMemcpyHostToDevice, c->stream));
+  launch_rbh_scatter(L->view(), iv, R.d_items, R.n, R.d_cc, c->stream);
+  host_sync(c, c->stream);   // (the pinned buffer is reused by the next fill)
+}
+
+void rbh_free(Level& L) {
+  for (auto& kv : L.rbh) {
+    RbHostFaces& R = kv.second;
+    dfree(R.d_items);
+    dfree(R.d_slot);
+    dfree(R.d_cgc);
+    dfree(R.d_cc);
+    if (R.h_cgc) (void)hipHostFree(R.h_cgc);
+    if (R.h_cc) (void)hipHostFree(R.h_cc);
+  }
+  L.rbh.clear();
+}
+
+// the records of every level with refinement boundaries, for the variables
+// and faces that have a host callback
+void rbh_build(omg_ctx* c) {
+  c->rbh_any = false;
+  for (int iv = 0; iv < kMaxVars; iv++)
+    for (int nb = 0; nb < 6; nb++) c->rbh_any |= c->rb_fn[iv][nb] != nullptr;
+  for (auto& kv : c->levels) {
+    Level& L = kv.second;
+    rbh_free(L);
+    if (!c->rbh_any || !L.has_rb || !L.n || c->host_only) continue;
+    // receive slot of every NB_RBREM face (its position in the rb exchange)
+    std::map<int, int> rslot;
+    {
+      int pos = 0;
+      for (auto& p : L.rbx.recv)
+        for (int f : p.items) rslot[f] = pos++;
+    }
+    for (int iv = 1; iv <= c->n_vars; iv++) {
+      RbHostFaces R;
+      for (int nb = 1; nb <= 6; nb++) {
+        if (!c->rb_fn[iv - 1][nb - 1]) continue;
+        for (int b = 0; b < L.n; b++) {
+          const int f = b * 6 + nb - 1, kind = L.h_nbk[f];
+          if (kind != NB_RB && kind != NB_RBREM) continue;
+          R.items.push_back(f);
+          R.slot.push_back(kind == NB_RBREM ? rslot.at(f) : -1);
+          R.ids.push_back(L.ids[b]);
+          R.nbs.push_back(nb);
+        }
+      }
+      R.n = (int)R.items.size();
+      if (!R.n) continue;
+      const size_t nc2 = (size_t)L.nc * L.nc, per = (size_t)(L.nc + 2) * (L.nc + 2) * (L.nc + 2);
+      R.d_items = to_device(R.items);
+      R.d_slot = to_device(R.slot);
+      dmalloc(&R.d_cgc, sizeof(double) * R.n * nc2);
+      dmalloc(&R.d_cc, sizeof(double) * R.n * per);
+      HIPCHK(hipHostMalloc(&R.h_cgc, sizeof(double) * R.n * nc2));
+      HIPCHK(hipHostMalloc(&R.h_cc, sizeof(double) * R.n * per));
+      L.rbh[iv] = std::move(R);
+    }
+  }
+}
+
+// halo exchange of the faces packed by the last fill/substep kernel, then
+// fill_buffered_nb (m_ghost_cells.f90:163-174, 424-454); rb_hook: the fill is
+// complete here (no full fill follows), so host refinement-boundary callbacks run
+void finish_rb(omg_ctx* c, Level* L, int iv);
+void finish_halo(omg_ctx* c, Level* L, int iv, bool rb_hook = true) {
+  if (c->n_ranks > 1) {
+    if (L->halo.n_send || L->halo.n_recv) {
+      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+      launch_unpack_faces(L->view(), iv, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+    }
+    finish_rb(c, L, iv);
+  }
+  if (rb_hook) rb_host_fixup(c, L, iv);
 }
 
 // refinement boundaries across ranks (buffer_refinement_boundaries,
@@ -646,6 +739,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
       finish_rb(c, L, 1);
       if (!L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
+      else rb_host_fixup(c, L, 1);
       continue;
     }
     if (L->n) {
@@ -653,8 +747,9 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
                         L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream);
     }
-    finish_halo(c, L, 1);
-    if (odd || !L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
+    const bool full_fill = odd || !L->phi_gc_ok;
+    finish_halo(c, L, 1, !full_fill);
+    if (full_fill) fill_gc_lvl(c, lvl, 1);
   }
 }
 
@@ -1435,7 +1530,7 @@ double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
 // V-cycle ends in the coarse tail (the level-by-level coarse solve reads its
 // residual back per sweep), no profiling.
 bool graph_ok(omg_ctx* c) {
-  return !c->no_graph && !c->capturing && c->n_ranks == 1 && !c->subtract_mean && !c->profiling &&
+  return !c->no_graph && !c->capturing && c->n_ranks == 1 && !c->subtract_mean && !c->profiling && !c->rbh_any &&
          !c->tail_timing && !c->no_tail && c->n_boxes > 0 && tail_top(c, c->highest) >= c->lowest;
 }
 
@@ -1949,6 +2044,7 @@ void free_levels(omg_ctx* c) {
     Level& L = kv.second;
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_topo);
+    rbh_free(L);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
@@ -2293,6 +2389,7 @@ void build_plan(omg_ctx* c) {
     }
   }
   ensure_rhs_lex(c);
+  rbh_build(c);
 }
 
 }  // namespace
@@ -2861,6 +2958,17 @@ int omg_synchronize(omg_ctx* c) {
 }
 
 void* omg_stream(omg_ctx* c) { return (void*)c->stream; }
+
+int omg_set_refinement_bnd(omg_ctx* c, int iv, int nb, omg_rb_fn fn, void* user) {
+  return guarded([&] {
+    if (iv < 1 || iv > kMaxVars || nb < 1 || nb > 6) throw OmgError("omg_set_refinement_bnd: bad iv/nb");
+    if (c->rb_fn[iv - 1][nb - 1] == (void*)fn && c->rb_user[iv - 1][nb - 1] == user) return;
+    if (!c->host_only) HIPCHK(hipStreamSynchronize(c->stream));   // (staging buffers in use)
+    c->rb_fn[iv - 1][nb - 1] = (void*)fn;
+    c->rb_user[iv - 1][nb - 1] = fn ? user : nullptr;
+    rbh_build(c);
+  });
+}
 
 int omg_host_sync_count(omg_ctx* c, long long* n) {
   return guarded([&] { *n = c->n_host_syncs; });

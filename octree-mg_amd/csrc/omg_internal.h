@@ -89,6 +89,21 @@ struct Transfer {          // one p2p pattern (halo, restrict, prolong)
   int send_ints = 1, recv_ints = 1;  // ints per item in the send / recv lists
 };
 
+// The faces of one level and variable whose refinement-boundary ghosts a host
+// callback sets (omg_set_refinement_bnd): records (b*6+nb-1) sorted by face,
+// the receive slot of NB_RBREM faces (-1: coarse neighbour on this rank), and
+// the staging buffers of the coarse faces and the boxes (reference layout).
+struct RbHostFaces {
+  std::vector<int> items, slot, ids, nbs;
+  int n = 0;
+  int* d_items = nullptr;
+  int* d_slot = nullptr;
+  double* d_cgc = nullptr;
+  double* d_cc = nullptr;
+  double* h_cgc = nullptr;   // pinned
+  double* h_cc = nullptr;    // pinned
+};
+
 struct Level {
   int lvl = 0, nc = 0, n = 0;
   long long stride = 0;
@@ -167,6 +182,7 @@ struct Level {
   size_t sendbuf_doubles = 0, recvbuf_doubles = 0;
   // per-leaf partial sums scratch
   double* d_scratch = nullptr;
+  std::map<int, RbHostFaces> rbh;    // by variable: faces with a host refinement_bnd callback
 
   LevelView view() const {
     LevelView v;
@@ -307,6 +323,11 @@ struct omg_ctx {
   // communication (rank-invariant by construction) are also agreed over the
   // transport and an error is raised when they differ (tests)
   bool check_collective = false;
+  // host refinement-boundary callbacks (omg_set_refinement_bnd), per variable
+  // and face: omg_rb_fn of include/omg.h and its user pointer
+  void* rb_fn[omg::kMaxVars][6] = {};
+  void* rb_user[omg::kMaxVars][6] = {};
+  bool rbh_any = false;
   long long n_host_syncs = 0;          // host waits on a stream (host_sync; omg_host_sync_count)
   std::map<std::string, omg::KStat> stats;
   std::vector<omg::PendingEv> pending;

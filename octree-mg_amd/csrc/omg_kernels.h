@@ -65,6 +65,12 @@ struct GhostSets {
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr,
                    bool reg = true, double* xl = nullptr, const GhostSets* gs = nullptr,
                    const GcBC* bc = nullptr);
+// custom refinement-boundary faces on the host (omg_set_refinement_bnd): per
+// record (item b*6+nb-1) the coarse face and the box in the reference layout,
+// and the callback's ghost face back
+void launch_rbh_gather(const LevelView& L, const LevelView& C, int iv, const RBRec* rb, const int* items,
+                       const int* rslot, int n, const double* rbrecv, double* cgc, double* cc, hipStream_t st);
+void launch_rbh_scatter(const LevelView& L, int iv, const int* items, int n, const double* cc, hipStream_t st);
 // the physical ghosts of phi of the listed boxes (bc_to_gc from the boxes'
 // final boundary cells), after a chain of ghost-set sweeps
 void launch_phys_gc(const LevelView& L, const GcBC& bc, const int* boxes, int n_boxes, hipStream_t st);

@@ -97,6 +97,64 @@ __global__ void __launch_bounds__(256) k_rb_unpack(LevelView L, int iv, const in
   }
 }
 
+// Custom refinement-boundary faces served on the host (omg_set_refinement_bnd,
+// the reference's mg%bc(nb,iv)%refinement_bnd, m_ghost_cells.f90:321-325).
+// Record q = fine box b, face nb (item b*6+nb-1): the coarse face gc that
+// box_gc_for_fine_neighbor gives (:500-577; from the local coarse neighbour,
+// or for NB_RBREM the face the refinement-boundary exchange delivered, slot
+// rslot[q]) and the box's variable iv in the reference layout (edges and
+// corners 0), for the host callback.
+__global__ void __launch_bounds__(256) k_rbh_gather(LevelView L, LevelView C, int iv, const RBRec* rb,
+                                                    const int* items, const int* rslot, int n,
+                                                    const double* rbrecv, double* cgc, double* cc) {
+  const int nc = L.nc, nc2 = nc * nc, s = nc + 2;
+  const long long per = (long long)s * s * s;
+  GRID_STRIDE(t, (long long)n * (nc2 + per)) {
+    if (t < (long long)n * nc2) {
+      const int q = (int)(t / nc2), cell = (int)(t % nc2);
+      const int b = items[q] / 6, nb = items[q] % 6 + 1;
+      const int a = cell % nc + 1, c = cell / nc + 1;
+      if (rslot[q] >= 0) {
+        cgc[t] = rbrecv[(long long)rslot[q] * nc2 + cell];
+        continue;
+      }
+      const RBRec R = rb[L.nba[(long long)b * 6 + nb - 1]];
+      const double* cu = boxp(C, iv, R.coarse_idx);
+      const int d = (nb + 1) >> 1;
+      const int t1 = (d == 1) ? 1 : 0, t2 = (d == 3) ? 1 : 2;
+      const int clayer = (nb & 1) ? nc : 1;   // the coarse face toward us
+      const int i = (a + 1) >> 1, j = (c + 1) >> 1;
+      auto T = [&](int p, int r) { return cu[off_face_cell(C, nb, clayer, R.dix[t1] + p, R.dix[t2] + r)]; };
+      const double tc = T(i, j);
+      const double g1 = 0.125 * (T(i + 1, j) - T(i - 1, j));
+      const double g2 = 0.125 * (T(i, j + 1) - T(i, j - 1));
+      double gv = ((a - 1) & 1) ? tc + g1 : tc - g1;
+      gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
+      cgc[t] = gv;
+    } else {
+      const long long u = t - (long long)n * nc2;
+      const int q = (int)(u / per), r = (int)(u % per);
+      const int b = items[q] / 6, i = r % s, j = (r / s) % s, k = r / (s * s);
+      const int nbnd = (i == 0 || i == s - 1) + (j == 0 || j == s - 1) + (k == 0 || k == s - 1);
+      cc[u] = nbnd >= 2 ? 0.0 : boxp(L, iv, b)[off_cell(L, i, j, k)];
+    }
+  }
+}
+
+// the callback's ghost cells of face nb of every record back into the boxes
+__global__ void __launch_bounds__(256) k_rbh_scatter(LevelView L, int iv, const int* items, int n,
+                                                     const double* cc) {
+  const int nc = L.nc, nc2 = nc * nc, s = nc + 2;
+  const long long per = (long long)s * s * s;
+  GRID_STRIDE(t, (long long)n * nc2) {
+    const int q = (int)(t / nc2), cell = (int)(t % nc2);
+    const int b = items[q] / 6, nb = items[q] % 6 + 1;
+    const int a = cell % nc + 1, c = cell / nc + 1, g = (nb & 1) ? 0 : nc + 1, d = (nb + 1) >> 1;
+    const int i = d == 1 ? g : a, j = d == 1 ? a : (d == 2 ? g : c), k = d == 3 ? g : c;
+    boxp(L, iv, b)[off_gh(L, nb, a, c)] = cc[(long long)q * per + i + (long long)s * (j + (long long)s * k)];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Gauss-Seidel substep over a level, generic box size: one workgroup per box.
 // Updates the cells of colour e (i+j+k ≡ e, the cells box_gs_* visits for
@@ -1461,6 +1519,18 @@ void launch_rb_pack(const LevelView& C, int iv, const int* items, int n, int nc,
   if (n == 0) return;
   const long long work = (long long)n * nc * nc;
   k_rb_pack<<<grid_for(work), 256, 0, st>>>(C, iv, items, n, nc, buf);
+}
+
+void launch_rbh_gather(const LevelView& L, const LevelView& C, int iv, const RBRec* rb, const int* items,
+                       const int* rslot, int n, const double* rbrecv, double* cgc, double* cc, hipStream_t st) {
+  if (n == 0) return;
+  const long long s = L.nc + 2, work = (long long)n * (L.nc * L.nc + s * s * s);
+  k_rbh_gather<<<grid_for(work), 256, 0, st>>>(L, C, iv, rb, items, rslot, n, rbrecv, cgc, cc);
+}
+
+void launch_rbh_scatter(const LevelView& L, int iv, const int* items, int n, const double* cc, hipStream_t st) {
+  if (n == 0) return;
+  k_rbh_scatter<<<grid_for((long long)n * L.nc * L.nc), 256, 0, st>>>(L, iv, items, n, cc);
 }
 
 void launch_rb_unpack(const LevelView& L, int iv, const int* items, int n, const double* recv, hipStream_t st) {

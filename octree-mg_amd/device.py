@@ -63,6 +63,7 @@ SIGNATURES = {
     "omg_synchronize": (_I, [_P]),
     "omg_stream": (_P, [_P]),
     "omg_host_sync_count": (_I, [_P, C.POINTER(_LL)]),
+    "omg_set_refinement_bnd": (_I, [_P, _I, _I, C.c_void_p, C.c_void_p]),
     "omg_comm_stream_priority": (_I, [_P, C.POINTER(_I)]),
     "omg_set_profiling": (_I, [_P, _I]),
     "omg_kernel_stats": (_I, [_P, C.c_char_p, C.POINTER(_LL), C.POINTER(_D), C.POINTER(_D)]),
@@ -136,8 +137,12 @@ class Context:
         except Exception:
             pass
 
+    after_call = None   # e.g. re-raise what a host callback raised during the call
+
     def call(self, name, *args):
         check(getattr(self.L, "omg_" + name)(self.h, *args))
+        if self.after_call is not None:
+            self.after_call()
 
     def plan_transfer(self, lvl, which, direction):
         """[(peer, key), ...] in wire order and the doubles per item of one

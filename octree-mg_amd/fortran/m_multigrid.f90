@@ -18,8 +18,10 @@
 !> Boundary conditions: mg%bc(nb, iv)%bc_type/bc_value go over as they are; a
 !> boundary_cond callback is tabulated on every physical face of every box of
 !> this rank at each call (the reference evaluates it at each ghost fill, with
-!> the same arguments).  Custom refinement_bnd callbacks, non-Cartesian
-!> geometry and NDIM /= 3 are rejected with error stop.  All five operators
+!> the same arguments).  A refinement_bnd callback runs on the host after
+!> each ghost fill of a level with such faces (rb_trampoline, through
+!> omg_set_refinement_bnd).  Non-Cartesian geometry and NDIM /= 3 are
+!> rejected with error stop.  All five operators
 !> of the reference run on the GPU (Laplacian, Helmholtz and their variable-
 !> coefficient forms via the generic kernels; aniso-Helmholtz likewise).
 module m_multigrid
@@ -42,6 +44,11 @@ module m_multigrid
   !> GPU between calls instead of round-tripping through mg%boxes(:)%cc.
   logical :: resident = .false.
   logical :: device_current = .false.
+
+  !> The mg_t of the call in progress, for the refinement_bnd callbacks the
+  !> device hands back to the host (rb_trampoline); set by every public entry
+  !> point that runs device work, null otherwise.
+  type(mg_t), pointer :: cb_mg => null()
 
   integer :: timer_device_vcycle = -1
   integer :: timer_device_fmg    = -1
@@ -123,7 +130,7 @@ contains
 
   !> Perform FAS-FMG cycle (m_multigrid.f90:84-147) on the GPU.
   subroutine mg_fas_fmg(mg, have_guess, max_res)
-    type(mg_t), intent(inout)       :: mg
+    type(mg_t), intent(inout), target :: mg
     logical, intent(in)             :: have_guess
     real(dp), intent(out), optional :: max_res
     real(c_double)                  :: res
@@ -131,11 +138,13 @@ contains
 
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
+    cb_mg => mg
     call sync_in(mg)
     want = merge(1_c_int, 0_c_int, present(max_res))
     call mg_timer_start(mg%timers(timer_device_fmg))
     call omg_ok(omg_fas_fmg(ctx, merge(1_c_int, 0_c_int, have_guess), want, res), &
          "mg_fas_fmg")
+    nullify(cb_mg)
     call omg_ok(omg_synchronize(ctx), "synchronize")
     call mg_timer_end(mg%timers(timer_device_fmg))
     call sync_out(mg)
@@ -144,7 +153,7 @@ contains
 
   !> Perform FAS V-cycle (m_multigrid.f90:150-243) on the GPU.
   subroutine mg_fas_vcycle(mg, highest_lvl, max_res, standalone)
-    type(mg_t), intent(inout)       :: mg
+    type(mg_t), intent(inout), target :: mg
     integer, intent(in), optional   :: highest_lvl
     real(dp), intent(out), optional :: max_res
     logical, intent(in), optional   :: standalone
@@ -153,6 +162,7 @@ contains
 
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
+    cb_mg => mg
     call sync_in(mg)
     hl = mg%lowest_lvl - 1              ! "absent" for the C side
     if (present(highest_lvl)) hl = highest_lvl
@@ -161,6 +171,7 @@ contains
     want = merge(1_c_int, 0_c_int, present(max_res))
     call mg_timer_start(mg%timers(timer_device_vcycle))
     call omg_ok(omg_fas_vcycle(ctx, hl, want, res, sa), "mg_fas_vcycle")
+    nullify(cb_mg)
     call omg_ok(omg_synchronize(ctx), "synchronize")
     call mg_timer_end(mg%timers(timer_device_vcycle))
     call sync_out(mg)
@@ -197,7 +208,7 @@ contains
   !> src/m_diffusion.f90:19-142 without a host round trip).  converged is
   !> .false. where the reference stops with "diffusion_solve: no convergence".
   subroutine mg_gpu_diffusion_solve(mg, dt, diffusion_coeff, order, max_res, converged)
-    type(mg_t), intent(inout) :: mg
+    type(mg_t), intent(inout), target :: mg
     real(dp), intent(in)      :: dt, diffusion_coeff, max_res
     integer, intent(in)       :: order
     logical, intent(out)      :: converged
@@ -206,10 +217,12 @@ contains
 
     call check_methods(mg)
     if (timer_device_vcycle == -1) call add_timers(mg)
+    cb_mg => mg
     call sync_in(mg)
     call mg_timer_start(mg%timers(timer_device_fmg))
     ierr = omg_diffusion_solve(ctx, int(mg%operator_type, c_int), real(dt, c_double), &
          real(diffusion_coeff, c_double), int(order, c_int), real(max_res, c_double), n_v, res)
+    nullify(cb_mg)
     converged = ierr == 0
     if (.not. converged .and. omg_error_message() /= "diffusion_solve: no convergence") &
          call omg_ok(ierr, "diffusion_solve")
@@ -226,7 +239,7 @@ contains
   !> its nx, for the host copy of the boundary callback.
   subroutine mg_gpu_poisson_free_3d(mg, new_rhs, max_fft_frac, fmgcycle, want, res, &
        fft_lvl, nx, planes)
-    type(mg_t), intent(inout)            :: mg
+    type(mg_t), intent(inout), target    :: mg
     logical, intent(in)                  :: new_rhs, fmgcycle, want
     real(dp), intent(in)                 :: max_fft_frac
     real(dp), intent(out)                :: res
@@ -245,9 +258,11 @@ contains
        rmin(:, id) = mg%boxes(id)%r_min
     end do
     call mg_timer_start(mg%timers(timer_device_fmg))
+    cb_mg => mg
     call omg_ok(omg_poisson_free_3d(ctx, merge(1_c_int, 0_c_int, new_rhs), &
          real(max_fft_frac, c_double), merge(1_c_int, 0_c_int, fmgcycle), &
          merge(1_c_int, 0_c_int, want), r, mg%r_min, rmin), "mg_poisson_free_3d")
+    nullify(cb_mg)
     call omg_ok(omg_synchronize(ctx), "synchronize")
     call mg_timer_end(mg%timers(timer_device_fmg))
     call omg_ok(omg_free_planes(ctx, lvl_c, nx_c, dummy, 0_c_long_long), "free_planes")
@@ -422,8 +437,13 @@ contains
     n_vars = mg_num_vars + mg%n_extra_vars
     do iv = 1, n_vars
        do nb = 1, mg_num_neighbors
-          if (associated(mg%bc(nb, iv)%refinement_bnd)) &
-               error stop "octree-mg GPU backend: custom refinement_bnd not supported"
+          if (associated(mg%bc(nb, iv)%refinement_bnd)) then
+             call omg_ok(omg_set_refinement_bnd(ctx, int(iv, c_int), int(nb, c_int), &
+                  c_funloc(rb_trampoline), c_null_ptr), "set_refinement_bnd")
+          else
+             call omg_ok(omg_set_refinement_bnd(ctx, int(iv, c_int), int(nb, c_int), &
+                  c_null_funptr, c_null_ptr), "set_refinement_bnd")
+          end if
           call omg_ok(omg_set_bc(ctx, int(iv, c_int), int(nb, c_int), &
                int(mg%bc(nb, iv)%bc_type, c_int), real(mg%bc(nb, iv)%bc_value, c_double)), &
                "set_bc")
@@ -558,5 +578,31 @@ contains
     call omg_ok(omg_set_bc_faces(ctx, int(iv, c_int), face_off, face_type, data, n_data), &
          "set_bc_faces")
   end subroutine tabulate_bc
+
+  !> The device's refinement_bnd hand-back (omg_set_refinement_bnd): for
+  !> each record, the box's variable iv (reference layout) goes into
+  !> mg%boxes(id)%cc for the callback, which the reference calls as
+  !> fill_refinement_bnd does (m_ghost_cells.f90:321-325); the ghosts it sets
+  !> come back in cc, and the host box keeps what it held before.
+  subroutine rb_trampoline(user, lvl, iv, n, ids, nbs, nc, cgc, cc) bind(C)
+    type(c_ptr), value            :: user
+    integer(c_int), value         :: lvl, iv, n, nc
+    integer(c_int), intent(in)    :: ids(n), nbs(n)
+    real(c_double), intent(in)    :: cgc(nc, nc, n)
+    real(c_double), intent(inout) :: cc(0:nc+1, 0:nc+1, 0:nc+1, n)
+    real(dp), allocatable         :: keep(:, :, :)
+    integer                       :: k, id, nb
+
+    if (.not. associated(cb_mg)) error stop "octree-mg GPU backend: refinement_bnd outside a call"
+    do k = 1, n
+       id = ids(k)
+       nb = nbs(k)
+       keep = cb_mg%boxes(id)%cc(:, :, :, iv)
+       cb_mg%boxes(id)%cc(:, :, :, iv) = cc(:, :, :, k)
+       call cb_mg%bc(nb, iv)%refinement_bnd(cb_mg%boxes(id), int(nc), int(iv), nb, cgc(:, :, k))
+       cc(:, :, :, k) = cb_mg%boxes(id)%cc(:, :, :, iv)
+       cb_mg%boxes(id)%cc(:, :, :, iv) = keep
+    end do
+  end subroutine rb_trampoline
 
 end module m_multigrid

@@ -19,6 +19,7 @@ module m_omg_capi
   public :: omg_fas_vcycle, omg_fas_fmg, omg_apply_op, omg_phi_bc_store
   public :: omg_synchronize, omg_diffusion_solve
   public :: omg_poisson_free_3d, omg_free_planes
+  public :: omg_set_refinement_bnd
 
   interface
      function omg_last_error() bind(C, name="omg_last_error") result(p)
@@ -94,6 +95,16 @@ module m_omg_capi
        real(c_double), value :: bc_value
        integer(c_int) :: ierr
      end function omg_set_bc
+
+     function omg_set_refinement_bnd(ctx, iv, nb, fn, user) &
+          bind(C, name="omg_set_refinement_bnd") result(ierr)
+       import :: c_ptr, c_int, c_funptr
+       type(c_ptr), value    :: ctx
+       integer(c_int), value :: iv, nb
+       type(c_funptr), value :: fn
+       type(c_ptr), value    :: user
+       integer(c_int) :: ierr
+     end function omg_set_refinement_bnd
 
      function omg_set_bc_faces(ctx, iv, face_off, face_type, data, n_data) &
           bind(C, name="omg_set_bc_faces") result(ierr)

@@ -33,11 +33,21 @@ from .tree import (MG_AHELMHOLTZ, MG_VHELMHOLTZ, MG_VLAPLACIAN, MG_BC_DIRICHLET,
 class BC:
     """mg_bc_t (reference: src/m_data_structures.f90:235-242)."""
 
-    def __init__(self, bc_type=MG_BC_DIRICHLET, bc_value=0.0, boundary_cond=None):
+    def __init__(self, bc_type=MG_BC_DIRICHLET, bc_value=0.0, boundary_cond=None, refinement_bnd=None):
         self.bc_type = bc_type
         self.bc_value = bc_value
         # boundary_cond(mg, id, nc, iv, nb) -> (bc_type, values[nc*nc], first index fastest)
         self.boundary_cond = boundary_cond
+        # refinement_bnd(mg, id, nc, iv, nb, cgc, cc): mg_subr_rb (:364-378);
+        # cgc [c-1, a-1] the coarse face (box_gc_for_fine_neighbor), cc
+        # [k, j, i] (0..nc+1) the box's variable iv, whose face-nb ghosts it
+        # sets in place (omg_set_refinement_bnd: called after every ghost fill)
+        self.refinement_bnd = refinement_bnd
+
+
+# omg_rb_fn (include/omg.h)
+_RB_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                     C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double))
 
 
 class MG(MGTree):
@@ -92,12 +102,38 @@ class MG(MGTree):
                self.max_coarse_cycles, self.residual_coarse_abs, self.residual_coarse_rel)
         c.call("set_subtract_mean", int(self.subtract_mean))
 
+    def _rb_trampoline(self, iv, nb, cb):
+        def fn(user, lvl, iv_, n, ids, nbs, nc, cgc, cc):
+            try:
+                s = nc + 2
+                g = np.ctypeslib.as_array(cgc, shape=(n, nc, nc))
+                a = np.ctypeslib.as_array(cc, shape=(n, s, s, s))
+                for q in range(n):
+                    cb(self, int(ids[q]), nc, iv_, int(nbs[q]), g[q], a[q])
+            except BaseException as ex:  # noqa: BLE001  (no exception may cross the C frame)
+                self._rb_error = ex
+        return _RB_FN(fn)
+
+    def _raise_rb_error(self):
+        ex = getattr(self, "_rb_error", None)
+        if ex is not None:
+            self._rb_error = None
+            raise ex
+
     def push_bc(self, ivs=None):
         """Send mg%bc to the device; boundary_cond callbacks are tabulated per
-        physical face of my boxes (they are pure functions of box geometry)."""
+        physical face of my boxes (they are pure functions of box geometry);
+        refinement_bnd callbacks are handed to omg_set_refinement_bnd."""
         c = self.ctx
         ivs = range(1, self.n_vars + 1) if ivs is None else ivs
+        if not hasattr(self, "_rb_keep"):
+            self._rb_keep = {}
+            c.after_call = self._raise_rb_error
         for iv in ivs:
+            for nb in range(1, 7):
+                cb = self.bc[nb][iv].refinement_bnd
+                fp = self._rb_keep[(iv, nb)] = self._rb_trampoline(iv, nb, cb) if cb else None
+                c.call("set_refinement_bnd", iv, nb, C.cast(fp, C.c_void_p) if fp else None, None)
             cbs = [self.bc[nb][iv].boundary_cond for nb in range(1, 7)]
             for nb in range(1, 7):
                 b = self.bc[nb][iv]

@@ -28,7 +28,10 @@
 !     rhs      sol (rhs = L u) | one (rhs = 1) | phi (phi = u incl. ghosts,
 !              rhs = 0: the initial state of a diffusion run)
 !     n_levels 1 = uniform, >1 = test_refinement's AMR tree
-!     lb       lb (mg_load_balance) | lbp (+ mg_load_balance_parents)
+!     lb       lb (mg_load_balance) | lbp (+ mg_load_balance_parents);
+!              a trailing "rb" (lbrb, lbprb) installs a custom refinement_bnd
+!              callback for phi (custom_rb: sides_rb's form with other
+!              coefficients, m_ghost_cells.f90:769-861)
 !     maxres   0 | 1  (request max_res from mg_fas_vcycle/mg_fas_fmg)
 !     dump     x, or a file: final phi interior of every box (ids order per
 !              level, lowest..highest, i fastest), raw float64; with more
@@ -138,7 +141,15 @@ program omg_golden
      call build_amr_tree(mg, n_levels, domain_size, box_size, dr, periodic)
   end if
   call mg_load_balance(mg)
-  if (trim(a_lb) == "lbp") call mg_load_balance_parents(mg)
+  if (a_lb(1:3) == "lbp") call mg_load_balance_parents(mg)
+  n = len_trim(a_lb)
+  if (n > 2) then
+     if (a_lb(n-1:n) == "rb") then
+        do ierr = 1, mg_num_neighbors
+           mg%bc(ierr, mg_iphi)%refinement_bnd => custom_rb
+        end do
+     end if
+  end if
   call mg_allocate_storage(mg)
 #ifdef OMG_GPU_RESIDENT
   ! GPU drop-in only (octree-mg_amd/fortran): data stays on the GPU between
@@ -379,6 +390,37 @@ contains
     end do
     close(u)
   end subroutine dump_phi_rank
+
+  !> A refinement-boundary method of the mg_subr_rb interface
+  !> (m_data_structures.f90:364-378): sides_rb's second-order form
+  !> 0.5 gc + 0.75 x1 - 0.25 x2 (m_ghost_cells.f90:769-861) with other
+  !> coefficients that also sum to one.
+  subroutine custom_rb(box, nc, iv, nb, cgc)
+    type(mg_box_t), intent(inout) :: box
+    integer, intent(in)           :: nc, iv, nb
+    real(dp), intent(in)          :: cgc(nc, nc)
+    integer                       :: a, c, x1, x2, g
+    if (mg_neighb_low(nb)) then
+       x1 = 1; x2 = 2; g = 0
+    else
+       x1 = nc; x2 = nc - 1; g = nc + 1
+    end if
+    do c = 1, nc
+       do a = 1, nc
+          select case (mg_neighb_dim(nb))
+          case (1)
+             box%cc(g, a, c, iv) = 0.4_dp * cgc(a, c) + 0.9_dp * box%cc(x1, a, c, iv) &
+                  - 0.3_dp * box%cc(x2, a, c, iv)
+          case (2)
+             box%cc(a, g, c, iv) = 0.4_dp * cgc(a, c) + 0.9_dp * box%cc(a, x1, c, iv) &
+                  - 0.3_dp * box%cc(a, x2, c, iv)
+          case default
+             box%cc(a, c, g, iv) = 0.4_dp * cgc(a, c) + 0.9_dp * box%cc(a, c, x1, iv) &
+                  - 0.3_dp * box%cc(a, c, x2, iv)
+          end select
+       end do
+    end do
+  end subroutine custom_rb
 
   subroutine sol_boundary_condition(box, nc, iv, nb, bc_type, bc)
     type(mg_box_t), intent(in) :: box

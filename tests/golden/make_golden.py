@@ -92,6 +92,12 @@ CONFIGS = {
     # callback Dirichlet, one refined level): k_gsrb_tile<16> with refinement
     # boundaries and the fused correction + fill on a refined level
     "c4_ref2_box16_gsrb": ("16 128 128 128 4 v gsrb lpl 0 sol sol 2 lb 0", True, [1, 3, 4]),
+    # a custom refinement_bnd callback (lb "lbrb": omg_golden.f90's custom_rb,
+    # sides_rb's form with other coefficients) on the refined trees: the
+    # drop-in runs it on the host after each device fill; at 3 ranks the
+    # coarse faces of some refinement boundaries arrive from another rank
+    "c4_ref2_box16_gsrb_rb": ("16 128 128 128 4 v gsrb lpl 0 sol sol 2 lbrb 0", True, [1, 3]),
+    "ref3_gs_rb": ("8 32 32 32 4 v gs lpl 0 sol sol 3 lbrb 0", True, [1, 3]),
     # §8(f) row 1: m_diffusion — one implicit time step per iteration from
     # phi = u (cycle d1 = backward Euler, d2 = Crank-Nicolson; the lambda
     # field is dt; helm: diffusion_solve with D = 0.5, vhelm: _vcoeff)
@@ -166,6 +172,8 @@ def main():
         entry = {"args": args, "runs": {}}
         if name in BIG:
             entry["big"] = True
+        if args.split()[12].endswith("rb"):
+            entry["custom_rb"] = True   # not in the C oracle (tests/test_oracle_golden.py)
         for r in ranks:
             with tempfile.TemporaryDirectory() as td:
                 fn = os.path.join(td, "phi.bin") if dump else None

@@ -73,9 +73,26 @@ def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0):
         for lvl in range(1, nl + 1):
             tree.set_refinement_boundaries(lvl)
     tree.load_balance()
-    if cfg["lb"] == "lbp":
+    if cfg["lb"].startswith("lbp"):
         tree.load_balance_parents()
     return tree
+
+
+def custom_rb(mg, id_, nc, iv, nb, cgc, cc, k=(0.4, 0.9, -0.3)):
+    """omg_golden.f90's custom_rb (a refinement_bnd callback: sides_rb's form
+    0.5 gc + 0.75 x1 - 0.25 x2, m_ghost_cells.f90:769-861, with other
+    coefficients); k = (0.5, 0.75, -0.25) restates sides_rb itself.
+    cgc[c-1, a-1], cc[k, j, i]."""
+    low = nb % 2 == 1
+    x1, x2, g = (1, 2, 0) if low else (nc, nc - 1, nc + 1)
+    d = (nb + 1) // 2
+    s = slice(1, nc + 1)
+    if d == 1:
+        cc[s, s, g] = k[0] * cgc + k[1] * cc[s, s, x1] + k[2] * cc[s, s, x2]
+    elif d == 2:
+        cc[s, g, s] = k[0] * cgc + k[1] * cc[s, x1, s] + k[2] * cc[s, x2, s]
+    else:
+        cc[g, s, s] = k[0] * cgc + k[1] * cc[x1, s, s] + k[2] * cc[x2, s, s]
 
 
 I_EPS = 5   # mg_iveps: the coefficient of the v-operators (vlpl / vhelm)
@@ -111,6 +128,8 @@ class OracleBackend:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle  # checker only
         self.cfg = cfg
+        if cfg["lb"].endswith("rb"):
+            raise NotImplementedError("the oracle has no custom refinement_bnd (its goldens pin the drop-in)")
         self.tree = build_tree(cfg, T.MGTree(), n_ranks)
         self.o = pyoracle.Oracle(self.tree, n_vars(cfg), n_ranks)
         op = OPS[cfg["op"]]
@@ -185,6 +204,9 @@ class DeviceBackend:
             faces[iv] = (off, typ, data)
 
         _apply_bc(cfg, mg, set_bc, set_faces)
+        if cfg["lb"].endswith("rb"):   # omg_golden's custom_rb on phi
+            for nb in range(1, 7):
+                mg.bc[nb][T.MG_IPHI].refinement_bnd = custom_rb
         omg.mg_allocate_storage(mg)
         for iv, (off, typ, data) in faces.items():
             mg.ctx.call("set_bc_faces", iv, off, typ, data, len(data))

@@ -229,3 +229,30 @@ def test_fmg_full_state_matches_oracle(args, have_guess):
     for _ in range(2):
         assert dev.fmg(have_guess, True) == orc.fmg(have_guess, True)
         _assert_same(dev, orc, ivs=(1, 2, 3, 4))
+
+
+def test_refinement_bnd_callback_restating_sides_rb():
+    """omg_set_refinement_bnd through the Python mirror: a host callback that
+    restates sides_rb (0.5 gc + 0.75 x1 - 0.25 x2, m_ghost_cells.f90:769-861)
+    must give the reference's own history and phi of the bench's refined
+    GSRB tree bit for bit (coarse faces, box copies, the ghosts coming back,
+    once per fill); the custom_rb goldens pin other coefficients."""
+    import functools
+
+    from tests.mgdriver import T, _cycles, custom_rb, phi_digest
+    e = GOLDEN["c4_ref2_box16_gsrb"]
+    cfg = parse(e["args"])
+    be = DeviceBackend(cfg)
+    calls = []
+
+    def sides_rb(mg, id_, nc, iv, nb, cgc, cc):
+        calls.append(nb)
+        custom_rb(mg, id_, nc, iv, nb, cgc, cc, k=(0.5, 0.75, -0.25))
+
+    for nb in range(1, 7):
+        be.mg.bc[nb][T.MG_IPHI].refinement_bnd = sides_rb
+    be.mg.push_bc([T.MG_IPHI])
+    setup_problem(be)
+    assert _cycles(be, cfg) == e["runs"]["1"]["history"]
+    assert phi_digest(be) == e["runs"]["1"]["phi_sha256"]
+    assert calls and set(calls) == set(range(1, 7))

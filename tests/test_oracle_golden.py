@@ -17,7 +17,9 @@ from tests.mgdriver import run_problem
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
 # "big" entries (the bench's 512^3 configuration) are checked against the
 # device only: the C oracle would take minutes and ~7 GB here
-CASES = [(n, r) for n, e in GOLDEN.items() if not e.get("big") for r in e["runs"]]
+# (custom_rb entries: a refinement_bnd callback the oracle does not restate;
+# the device and the Fortran drop-in are held to them)
+CASES = [(n, r) for n, e in GOLDEN.items() if not e.get("big") and not e.get("custom_rb") for r in e["runs"]]
 
 
 @pytest.mark.parametrize("name,ranks", CASES, ids=[f"{n}-r{r}" for n, r in CASES])
