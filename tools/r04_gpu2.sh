@@ -4,6 +4,9 @@ export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r04
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+  tests/test_fortran_dropin.py tests/test_gpu_multirank.py -k "_rb or refinement_bnd" > $O/s2_rb.log 2>&1 || { tail -30 $O/s2_rb.log; exit 1; }
+tail -1 $O/s2_rb.log
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_smoothers.py \
   tests/test_gpu_parity.py tests/test_gpu_multirank.py -k "not c3_512" > $O/s2_tests.log 2>&1 || { tail -30 $O/s2_tests.log; exit 1; }
 tail -1 $O/s2_tests.log
