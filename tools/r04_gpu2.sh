@@ -11,3 +11,6 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_parity.py tests/test_gpu_multirank.py -k "not c3_512" > $O/s2_tests.log 2>&1 || { tail -30 $O/s2_tests.log; exit 1; }
 tail -1 $O/s2_tests.log
 bash tools/r04_ab.sh s2 "C4 C2-gs perf-gs C3 C2" octree-mg_amd/_variants/libomg_r03.so
+R=$PWD
+(cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/$O/lat -o run --output-format csv -- $R/tools/lat_probe) > $O/lat.log 2>&1 || exit 1
+python3 tools/trace_by_grid.py $(find $O/lat -name "*kernel_trace.csv" | head -1) > $O/lat_by_grid.txt
