@@ -480,9 +480,17 @@ GcBC bc_for(omg_ctx* c, int lvl, int iv) {
   return g;
 }
 
+// The refinement-boundary ghosts of level lvl+1 are interpolated from level
+// lvl (its interior and tangential ghosts, box_gc_for_fine_neighbor,
+// m_ghost_cells.f90:500-577): every write of phi on lvl makes them stale.
+void rb_stale_above(omg_ctx* c, int lvl) {
+  if (Level* U = level_ptr(c, lvl + 1))
+    if (U->any_rb) U->phi_gc_ok = false;
+}
 // phi was written on a level: its ghost faces may no longer match a fill
 void phi_dirty(omg_ctx* c, int lvl) {
   if (Level* L = level_ptr(c, lvl)) L->phi_gc_ok = false;
+  rb_stale_above(c, lvl);
 }
 void phi_dirty_all(omg_ctx* c) {
   for (auto& kv : c->levels) kv.second.phi_gc_ok = false;
@@ -614,7 +622,10 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (lvl > c->highest) throw OmgError("fill_ghost_cells_lvl: lvl > highest_lvl");
   Level* L = level_ptr(c, lvl);
   if (!L) return;
-  if (iv == 1) L->phi_gc_ok = true;
+  if (iv == 1) {
+    L->phi_gc_ok = true;
+    rb_stale_above(c, lvl);   // (the ghosts it sets are read by lvl+1's interpolation)
+  }
   if (L->n) {
     Prof p(c, "fill_gc", (double)L->n * 6 * L->nc * L->nc, lvl);
     if (iv != 1 || L->has_rb || c->no_fill_tile ||
@@ -636,6 +647,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps - skip_last;
   if (!L) return;
+  if (n_sub >= 1) rb_stale_above(c, lvl);
   // a pending phi shift is subtracted by the first tiled substep while it
   // loads (the values it reads are dead afterwards); otherwise applied now
   // (not next to refinement boundaries: their ghosts read the coarse level)
@@ -945,6 +957,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
       (c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv)))
     return false;
   if (F->shift_pending) materialize_level(c, F);
+  rb_stale_above(c, lvl + 1);
   const bool split = F->has_remote;
   {
     const int n = split ? F->n_int : F->n;
@@ -996,6 +1009,7 @@ void correct_and_fill(omg_ctx* c, int lvl, bool then_gsrb = false, bool save_old
   Level* C = level_ptr(c, lvl);
   if (save_old && (then_gsrb || !correct_fill_fused(c, lvl)))
     throw OmgError("internal: old = phi fused into an unfused correction");
+  rb_stale_above(c, lvl + 1);
   if (correct_fill_fused(c, lvl)) {
     // every parent here has all its children on this GPU (no prolongation
     // traffic, every fine box has a local parent): the children form res
@@ -1148,6 +1162,7 @@ void materialize_level(omg_ctx* c, Level* L) {
   if (!L->shift_pending) return;
   phi_mean_ready(c);
   L->shift_pending = false;
+  rb_stale_above(c, L->lvl);
   if (L->n) {
     Prof p(c, "subtract", (double)L->n * L->nc * L->nc * L->nc, L->lvl);
     launch_subtract(L->view(), 1, red_mean(c, kChPhi), 1, c->stream);
@@ -1376,6 +1391,7 @@ void run_tail(omg_ctx* c, int top) {
     std::fprintf(stderr, "\n");
   }
   for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
+  rb_stale_above(c, top);
 }
 
 // Failure detection: the device max residual is an exact max of
@@ -1415,8 +1431,12 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     // uploads of phi, see omg.h), and any_rb is a property of the global
     // tree.  (Agreeing over the transport instead, as round 3 did, cost a
     // host synchronisation per cycle.)  OMG_CHECK_COLLECTIVE checks it.
+    // A level with refinement boundaries is consistent as long as the level
+    // below was not written since its last fill (rb_stale_above).  Those
+    // writes depend on per-rank state (pending mean shifts), so with more
+    // than one rank such a level is always refilled.
     Level* L = level_ptr(c, max_lvl);
-    const bool need = !(L && L->phi_gc_ok && !L->any_rb);
+    const bool need = !(L && L->phi_gc_ok && (!L->any_rb || c->n_ranks == 1));
     if (c->n_ranks > 1 && c->check_collective && (allreduce(c, need ? 1.0 : 0.0, true) > 0.5) != need)
       throw OmgError("mg_fas_vcycle: the stand-alone fill decision differs across ranks "
                      "(an upload of phi was not made on every rank)");
@@ -2751,7 +2771,7 @@ int omg_upload_level(omg_ctx* c, int lvl, int iv, const double* host) {
     if (iv < 1 || iv > c->n_vars) throw OmgError("bad variable index");
     // (before the early return: a rank without boxes here still drops the
     // flag, which the multi-rank stand-alone fill decision relies on)
-    if (iv == 1) L->phi_gc_ok = false;
+    if (iv == 1) phi_dirty(c, lvl);
     if (!L->n) return;
     const size_t s = L->nc + 2, box = s * s * s, n = box * L->n;
     double* st = stage(c, n);
