@@ -10,3 +10,4 @@ timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thre
   tests/test_gpu_parity.py tests/test_gpu_multirank.py -k "not c3_512 and not c0" > $O/s4_tests.log 2>&1 || { tail -30 $O/s4_tests.log; exit 1; }
 tail -1 $O/s4_tests.log
 bash tools/r04_ab.sh s4 "C4 C2-gs perf-gs C3 C2" octree-mg_amd/_variants/libomg_r03.so
+bash tools/r04_pmc_yz.sh > gpurun_out/r04/pmc_yz.txt 2>&1 || exit 1
