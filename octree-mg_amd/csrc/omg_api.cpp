@@ -852,8 +852,9 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
 // Whether the down-smoothing of level lvl can end in k_smooth_resid (its last
 // substep, colour 0, fused with update_coarse's residual + restriction):
 // red-black (two substeps per cycle, so the last one is colour 0),
-// Laplacian / Helmholtz, 16^3 or 8^3 boxes, no physical or refinement-boundary
-// face on the level (the recomputed ghosts read the neighbour box directly).
+// Laplacian / Helmholtz, 16^3 or 8^3 boxes.  Same-GPU faces: the recomputed
+// ghosts read the neighbour box directly; physical and refinement-boundary
+// faces (round 4; OMG_NO_FUSE_DOWN_BC: not fused): from the box's own cells.
 // On a level with faces on other GPUs only the boxes without such a face fuse
 // (n_int > 0); the others take the unfused substep + residual.
 bool smooth_resid_ok(omg_ctx* c, int lvl) {
@@ -861,8 +862,11 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
   const Level* C = level_ptr(c, lvl - 1);
   return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_substeps == 2 &&
          c->n_cycle_down >= 1 &&
-         (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) && !F->has_rb &&
-         !F->has_phys && (!F->has_remote || F->n_int);
+         (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) &&
+         !(c->no_fuse_down_bc && (F->has_rb || F->has_phys)) && (!F->has_remote || F->n_int) &&
+         // (refinement boundaries across ranks exchange coarse faces after every
+         // substep: no fusion there, decided alike on every rank)
+         !(F->any_rb && c->n_ranks > 1);
 }
 
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down
@@ -899,7 +903,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
       {
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
         if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                                 F->d_dix, c->stream, F->d_int, F->n_int))
+                                 F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb))
           throw OmgError("smooth_resid: not available for this level");
       }
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
@@ -911,7 +915,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                               F->d_dix, c->stream))
+                               F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb))
         throw OmgError("smooth_resid: not available for this level");
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
@@ -920,6 +924,10 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     }
     restrict_remote(c, 1, lvl);
     restrict_remote(c, 4, lvl);
+    // the fused step leaves the colour-1 halves of physical / refinement-
+    // boundary ghosts as they were before the substep (k_smooth_resid); the
+    // up-step's correction forms them again before anything reads them
+    if (fused && (F->any_phys || F->any_rb)) F->phi_gc_ok = false;
   } else {
     residual_lvl(c, lvl, nullptr);
     restrict_lvl(c, 1, lvl);
@@ -2472,6 +2480,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->gs_lex_plane = env_flag("OMG_GS_LEX_PLANE");
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
+    c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");

@@ -290,6 +290,7 @@ struct omg_ctx {
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
   bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring
   bool no_fill_xl = false;             // OMG_NO_FILL_XL: the plain tiled fill after register-ring sweeps
+  bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending

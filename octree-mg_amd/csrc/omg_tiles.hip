@@ -221,10 +221,18 @@ __device__ __forceinline__ v2d sr_ld(const double* p) {
 // layer, the neighbour's rhs and, at face edges, the neighbour's own ghosts.
 // Same operands, same gs_value: bit-identical to the neighbour's own update.
 // Levels whose faces are all same-GPU boxes, Laplacian / Helmholtz, NC 16/8.
-template <int NC, int OP, int BS>
+// Round 4: boxes with physical or refinement-boundary faces fuse too (RB:
+// the level has refinement-boundary faces, a separate instantiation).  Their
+// ghosts on such faces follow from the box's own final cells (bc_to_gc,
+// sides_rb with the coarse face), both colour halves, formed in LDS after the
+// update for the residual; only the colour-0 halves go to HBM.  The colour-1
+// halves must stay as the substep read them: a same-GPU neighbour's edge
+// tap (gedge) reads them in this launch.  The host marks the level's ghosts
+// stale; the correction of the up-step forms them again before any read.
+template <int NC, int OP, int BS, bool RB = false>
 __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, double lambda, int restrict_on,
                                                      const int* parent_local, const int* dixp,
-                                                     const int* list) {
+                                                     const int* list, GcBC bc) {
   using TL = Tl<NC>;
   constexpr int H = NC / 2, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS;
   constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
@@ -291,6 +299,9 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     reinterpret_cast<double2*>(sb)[q2] = make_double2(v0, v1);
     st_nt(u + 2 * q2, v0, v1);
   }
+  // physical / refinement-boundary faces read our second layer (colour 0,
+  // just updated by other threads)
+  if (T.nonlocal()) __syncthreads();
   // ---- the neighbours' new colour-0 boundary cells = our colour-0 ghosts ----
 #pragma unroll
   for (int g = 0; g < NG; g++) {
@@ -300,6 +311,28 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
     const int d = (nb - 1) >> 1;
+    const int kind = T.kind(nb - 1);
+    if (kind != NB_LOCAL) {
+      // both colour halves at this slot: (a, c) of colour 0 and (a1, c) of colour 1
+      const int a1 = 2 * ah + 1 + ((gl + c) & 1);
+      double gv[2];
+#pragma unroll
+      for (int col = 0; col < 2; col++) {
+        const int aa = col ? a1 : a;
+        const double x1 = sb[sr_int<NC>(d, low ? 1 : NC, aa, c)], x2 = sb[sr_int<NC>(d, low ? 2 : NC - 1, aa, c)];
+        if (kind == NB_PHYS)
+          gv[col] = phys_ghost(F, bc, b, (long long)b * 6 + nb - 1, nb, T.phys_code(nb - 1), aa, c,
+                               TL::ogh(nb, aa, c), x1, x2);
+        else if (RB)
+          gv[col] = rb_ghost(F, RbSide{Cv, nullptr}, T.arg(nb - 1), nb, aa, c, x1, x2);
+        else
+          gv[col] = 0.0;   // (unreachable: the host fuses no other face kind)
+      }
+      sb[2 * HV + (nb - 1) * FS + hi] = gv[0];
+      sb[2 * HV + (nb - 1) * FS + FH + hi] = gv[1];
+      u[2 * HV + (nb - 1) * FS + hi] = gv[0];
+      continue;
+    }
     const double across = sb[sr_int<NC>(d, low ? 1 : NC, a, c)];
     const bool ea = a == 1 || a == NC;
     // along the face normal, then the two tangential axes (t1 < t2)
@@ -961,22 +994,29 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
 
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
                          const int* parent_local, const int* dixp, hipStream_t st, const int* list,
-                         int n_list) {
+                         int n_list, const GcBC& bc, bool has_rb) {
   if (op != OP_LPL && op != OP_HELM) return false;
   const int n = list ? n_list : F.n;
   if (n == 0) return true;
   const dim3 g(n);
-#define OMG_SR(NC, BS)                                                                                   \
-  if (op == OP_LPL)                                                                                      \
-    k_smooth_resid<NC, OP_LPL, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list);   \
-  else                                                                                                   \
-    k_smooth_resid<NC, OP_HELM, BS><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list);
+#define OMG_SR_RB(NC, BS, RB)                                                                                    \
+  if (op == OP_LPL)                                                                                              \
+    k_smooth_resid<NC, OP_LPL, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc);  \
+  else                                                                                                           \
+    k_smooth_resid<NC, OP_HELM, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc);
+#define OMG_SR(NC, BS)           \
+  if (has_rb) {                  \
+    OMG_SR_RB(NC, BS, true)      \
+  } else {                       \
+    OMG_SR_RB(NC, BS, false)     \
+  }
   switch (F.nc) {
     case 16: OMG_SR(16, 512) return true;
     case 8: OMG_SR(8, 256) return true;
     default: return false;
   }
 #undef OMG_SR
+#undef OMG_SR_RB
 }
 
 bool tiled_nc(int nc) { return nc == 16 || nc == 8 || nc == 4 || nc == 2; }
