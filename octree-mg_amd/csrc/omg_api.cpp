@@ -903,7 +903,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
       {
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
         if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                                 F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb))
+                                 F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb, F->has_phys))
           throw OmgError("smooth_resid: not available for this level");
       }
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
@@ -915,7 +915,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                               F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb))
+                               F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb, F->has_phys))
         throw OmgError("smooth_resid: not available for this level");
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);

@@ -160,7 +160,7 @@ void launch_fill_tile_xl(const LevelView& L, const GcBC& bc, double* sendbuf, co
 // pass (k_smooth_resid); false: not available for this op / box size
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
                          const int* parent_local, const int* dixp, hipStream_t st, const int* list,
-                         int n_list, const GcBC& bc, bool has_rb);
+                         int n_list, const GcBC& bc, bool has_rb, bool has_phys);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st, const int* list = nullptr, int n_list = 0);

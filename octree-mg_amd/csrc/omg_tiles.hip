@@ -221,15 +221,16 @@ __device__ __forceinline__ v2d sr_ld(const double* p) {
 // layer, the neighbour's rhs and, at face edges, the neighbour's own ghosts.
 // Same operands, same gs_value: bit-identical to the neighbour's own update.
 // Levels whose faces are all same-GPU boxes, Laplacian / Helmholtz, NC 16/8.
-// Round 4: boxes with physical or refinement-boundary faces fuse too (RB:
-// the level has refinement-boundary faces, a separate instantiation).  Their
+// Round 4: boxes with physical or refinement-boundary faces fuse too (BCK:
+// 0 = the level has neither, 1 = physical faces, 2 = refinement-boundary
+// faces too; separate instantiations keep the plain kernel's registers).  Their
 // ghosts on such faces follow from the box's own final cells (bc_to_gc,
 // sides_rb with the coarse face), both colour halves, formed in LDS after the
 // update for the residual; only the colour-0 halves go to HBM.  The colour-1
 // halves must stay as the substep read them: a same-GPU neighbour's edge
 // tap (gedge) reads them in this launch.  The host marks the level's ghosts
 // stale; the correction of the up-step forms them again before any read.
-template <int NC, int OP, int BS, bool RB = false>
+template <int NC, int OP, int BS, int BCK = 0>
 __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, double lambda, int restrict_on,
                                                      const int* parent_local, const int* dixp,
                                                      const int* list, GcBC bc) {
@@ -301,7 +302,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   }
   // physical / refinement-boundary faces read our second layer (colour 0,
   // just updated by other threads)
-  if (T.nonlocal()) __syncthreads();
+  if (BCK && T.nonlocal()) __syncthreads();
   // ---- the neighbours' new colour-0 boundary cells = our colour-0 ghosts ----
 #pragma unroll
   for (int g = 0; g < NG; g++) {
@@ -312,7 +313,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
     const int d = (nb - 1) >> 1;
     const int kind = T.kind(nb - 1);
-    if (kind != NB_LOCAL) {
+    if (BCK && kind != NB_LOCAL) {
       // both colour halves at this slot: (a, c) of colour 0 and (a1, c) of colour 1
       const int a1 = 2 * ah + 1 + ((gl + c) & 1);
       double gv[2];
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
         if (kind == NB_PHYS)
           gv[col] = phys_ghost(F, bc, b, (long long)b * 6 + nb - 1, nb, T.phys_code(nb - 1), aa, c,
                                TL::ogh(nb, aa, c), x1, x2);
-        else if (RB)
+        else if (BCK == 2)
           gv[col] = rb_ghost(F, RbSide{Cv, nullptr}, T.arg(nb - 1), nb, aa, c, x1, x2);
         else
           gv[col] = 0.0;   // (unreachable: the host fuses no other face kind)
@@ -994,7 +995,7 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
 
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
                          const int* parent_local, const int* dixp, hipStream_t st, const int* list,
-                         int n_list, const GcBC& bc, bool has_rb) {
+                         int n_list, const GcBC& bc, bool has_rb, bool has_phys) {
   if (op != OP_LPL && op != OP_HELM) return false;
   const int n = list ? n_list : F.n;
   if (n == 0) return true;
@@ -1006,9 +1007,11 @@ bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double 
     k_smooth_resid<NC, OP_HELM, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc);
 #define OMG_SR(NC, BS)           \
   if (has_rb) {                  \
-    OMG_SR_RB(NC, BS, true)      \
+    OMG_SR_RB(NC, BS, 2)         \
+  } else if (has_phys) {         \
+    OMG_SR_RB(NC, BS, 1)         \
   } else {                       \
-    OMG_SR_RB(NC, BS, false)     \
+    OMG_SR_RB(NC, BS, 0)         \
   }
   switch (F.nc) {
     case 16: OMG_SR(16, 512) return true;
