@@ -780,6 +780,7 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
+void check_mid_err(omg_ctx* c);
 // max over levels lo..hi of max_residual_lvl (m_multigrid.f90:296-311), this
 // rank only: the levels' maxima fold into one word on the device, read back
 // with one synchronisation
@@ -796,6 +797,7 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     return 0.0;
   }
   host_sync(c, c->stream);
+  check_mid_err(c);
   return c->h_scalar[0];
 }
 
@@ -1328,6 +1330,152 @@ int tail_top(omg_ctx* c, int max_lvl) {
   return top;
 }
 
+// ---------------------------------------------------------------------------
+// The mid levels (MidArgs in omg_kernels.h): the levels top+1 .. mid_top right
+// above the coarse tail, each of at most kMidMaxBoxes boxes of 16^3 / 8^3,
+// all on this GPU, run as one launch for their down-steps and one for their
+// up-steps, P workgroups on one XCD with a barrier between steps.  Each
+// launch-per-step of the level-by-level path costs 4.5-6.5 us on MI355X even
+// for an empty kernel (profiles/r04); a barrier among the workgroups of one
+// XCD costs ~1 us.
+
+// whether the 8P-workgroup launch deals its workgroups round-robin over the
+// 8 XCDs, as the mid kernel's barrier needs (checked once per context)
+bool mid_placement_ok(omg_ctx* c) {
+  if (c->mid_state) return c->mid_state > 0;
+  const int n = 8 * kMidMaxBoxes;
+  int* d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(int) * n));
+  launch_xcc_probe(d, n, c->stream);
+  std::vector<int> h(n);
+  HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  host_sync(c, c->stream);
+  dfree(d);
+  bool ok = true;
+  for (int i = 0; i < n; i++) ok &= h[i] == i % 8;
+  if (!ok) std::fprintf(stderr, "omg: workgroups are not dealt round-robin over 8 XCDs; mid levels launch by launch\n");
+  if (ok) {
+    dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 1), true);
+    dmalloc(&c->d_mid_err, sizeof(int), true);
+    for (int k = 0; k < 2; k++) {
+      dmalloc(&c->d_mid[k], sizeof(MidArgs));
+      c->h_mid[k] = new MidArgs;
+      std::memset(c->h_mid[k], 0xff, sizeof(MidArgs));
+    }
+  }
+  c->mid_state = ok ? 1 : -1;
+  return ok;
+}
+
+// The highest level of the run top+1 .. that qualifies (INT_MIN: none), for a
+// cycle whose highest level is max_lvl (mid levels lie strictly below it)
+int mid_top(omg_ctx* c, int top, int max_lvl) {
+  if (c->no_mid || c->capturing || (c->op != OP_LPL && c->op != OP_HELM)) return INT_MIN;
+  const Level* T = level_ptr(c, top);
+  if (!T || (T->nc != 16 && T->nc != 8)) return INT_MIN;
+  int m = INT_MIN;
+  for (int l = top + 1; l < max_lvl && l - top + 1 <= kMidMaxLevels; l++) {
+    const Level* L = level_ptr(c, l);
+    const Level* C = level_ptr(c, l - 1);
+    if (!L || L->n < 1 || L->n > kMidMaxBoxes || L->n != (int)c->ids[l].size() || (L->nc != 16 && L->nc != 8) ||
+        L->has_rb || L->has_remote || L->n_pairs != L->n ||
+        !((size_t)L->n == 8 * C->parents.size() || C->nc * 2 == L->nc) || (int)C->parents.size() > kMidMaxBoxes)
+      break;
+    m = l;
+  }
+  if (m == INT_MIN || !level_ptr(c, m)->phi_gc_ok || !mid_placement_ok(c)) return INT_MIN;
+  return m;
+}
+
+// down: the down-steps of mid_top .. top+1 (smoothing, residual +
+// restriction, fill and coarse rhs of the level below, as update_coarse);
+// up: the up-steps of top+1 .. mid_top (correction + fill, smoothing)
+void run_mid(omg_ctx* c, int top, int mtop, bool down) {
+  MidArgs A;
+  std::memset(&A, 0, sizeof(A));   // padding too: compared bytewise below
+  A.n_lvls = mtop - top + 1;
+  A.lambda = c->lambda;
+  A.xcd = 0;
+  A.sync = c->d_mid_sync;
+  A.err = c->d_mid_err;
+  int P = 1;
+  for (int l = top; l <= mtop; l++) {
+    Level* L = level_ptr(c, l);
+    MidLevel& M = A.lv[l - top];
+    M.L = L->view();
+    M.bc = bc_for(c, l, 1);
+    M.parents = L->d_parents;
+    M.n_par = (int)L->parents.size();
+    M.parent_local = L->d_parent_local;
+    M.dixp = L->d_dix;
+    if (l > top) P = std::max(P, L->n);
+    P = std::max(P, M.n_par);
+  }
+  A.P = P;
+  const bool lex = c->smoother != OMG_SMOOTHER_GSRB;
+  auto step = [&](int kind, int l, int e = 0, int colours = 0) {
+    if (A.n_steps >= kMidMaxSteps) throw OmgError("internal: too many mid-level steps");
+    A.st[A.n_steps++] = MidStep{(short)kind, (short)(l - top), (short)e, (short)colours};
+  };
+  auto smooth = [&](int l, int n_cycle) {
+    if (lex) {
+      for (int n = 1; n <= n_cycle; n++) {
+        step(MS_LEX, l);
+        step(MS_FILL, l);
+      }
+    } else {
+      for (int n = 1; n <= 2 * n_cycle; n++) step(MS_SUB, l, n & 1, 1 << (n & 1));
+    }
+  };
+  if (down) {
+    for (int l = mtop; l > top; l--) {
+      Level* L = level_ptr(c, l);
+      if (L->shift_pending) materialize_level(c, L);
+      smooth(l, c->n_cycle_down);
+      Level* C = level_ptr(c, l - 1);
+      C->rhs_lex_ok = false;
+      if (C->shift_pending) {   // overwritten by the restriction where every box is a parent
+        if (C->all_parents) C->shift_pending = false;
+        else materialize_level(c, C);
+      }
+      step(MS_RESID, l);
+      step(MS_FILL, l - 1);
+      if (!C->parents.empty()) step(MS_CRHS, l - 1);
+      phi_dirty(c, l - 1);
+      C->phi_gc_ok = true;
+    }
+  } else {
+    for (int l = top + 1; l <= mtop; l++) {
+      Level* L = level_ptr(c, l);
+      if (L->shift_pending) materialize_level(c, L);
+      step(MS_PFILL, l, 0, !lex && c->n_cycle_up >= 1 && !c->no_skip1);
+      smooth(l, c->n_cycle_up);
+      L->phi_gc_ok = true;
+    }
+    rb_stale_above(c, mtop);
+  }
+  const int k = down ? 0 : 1;
+  if (std::memcmp(&A, c->h_mid[k], sizeof(MidArgs)) != 0) {
+    *c->h_mid[k] = A;
+    launch_store_mid(A, c->d_mid[k], c->stream);
+  }
+  Prof p(c, down ? "mid_down" : "mid_up", 0.0, mtop);
+  launch_mid(c->d_mid[k], P, lex, c->op, ++c->mid_seq, c->stream);
+}
+
+// A failure of the mid kernel (sticky flag) raised at the next host wait
+void check_mid_err(omg_ctx* c) {
+  if (c->mid_state <= 0) return;
+  int e = 0;
+  HIPCHK(hipMemcpy(&e, c->d_mid_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) {
+    c->no_mid = true;
+    HIPCHK(hipMemset(c->d_mid_err, 0, sizeof(int)));
+    throw OmgError(std::string("mid-level kernel failed (") + (e & 2 ? "workgroup off its XCD" : "barrier timeout") +
+                   "): results of the last cycles are invalid; mid levels now launch by launch");
+  }
+}
+
 // Levels lowest..top of the V-cycle (down-smoothing of top .. up-smoothing of
 // top) in one launch, bit-identical to the level-by-level path.
 void run_tail(omg_ctx* c, int top) {
@@ -1455,8 +1603,13 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   }
   const int top = tail_top(c, max_lvl);
   const bool tail = top >= min_lvl && !c->no_tail;
+  const int mtop = tail ? mid_top(c, top, max_lvl) : INT_MIN;
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
+    if (mtop != INT_MIN && l == mtop) {   // mtop .. top+1 in one launch
+      run_mid(c, top, mtop, true);
+      break;
+    }
     const bool fused = smooth_resid_ok(c, l);
     smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
     update_coarse(c, l, fused);
@@ -1484,6 +1637,10 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
   }
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
+    if (mtop != INT_MIN && l <= mtop) {   // top+1 .. mtop in one launch
+      if (l == top + 1) run_mid(c, top, mtop, false);
+      continue;
+    }
     if (prolong_smooth(c, l - 1)) {
       smooth_boxes(c, l, c->n_cycle_up, 2);
     } else {
@@ -2481,6 +2638,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
+    c->no_mid = env_flag("OMG_NO_MID");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");
@@ -2560,6 +2718,12 @@ int omg_ctx_destroy(omg_ctx* c) {
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_maxslots);
+    dfree(c->d_mid_sync);
+    dfree(c->d_mid_err);
+    for (int k = 0; k < 2; k++) {
+      dfree(c->d_mid[k]);
+      delete c->h_mid[k];
+    }
     for (auto& kv : c->graphs)
       if (kv.second) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -2983,6 +3147,7 @@ int omg_synchronize(omg_ctx* c) {
   return guarded([&] {
     host_sync(c, c->stream);
     host_sync(c, c->stream2);
+    check_mid_err(c);
   });
 }
 

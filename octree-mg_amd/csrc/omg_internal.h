@@ -240,6 +240,7 @@ struct omg_free_state;    // free-space boundary conditions (omg_api.cpp, omg_fr
 
 namespace omg {
 struct TailArgs;   // omg_kernels.h
+struct MidArgs;    // omg_kernels.h
 // slots of a multi-workgroup max-residual launch (launch_max, omg_device.h)
 constexpr int kMaxSlots = 256, kMaxSlotStride = 16;
 }
@@ -301,6 +302,14 @@ struct omg_ctx {
   // they change
   omg::TailArgs* d_tail = nullptr;
   omg::TailArgs* h_tail = nullptr;   // the last uploaded copy (host)
+  // the mid levels in one launch (run_mid, MidArgs in omg_kernels.h)
+  omg::MidArgs* d_mid[2] = {nullptr, nullptr};   // down / up programs (device)
+  omg::MidArgs* h_mid[2] = {nullptr, nullptr};   // the last uploaded copies
+  unsigned long long* d_mid_sync = nullptr;      // barrier words
+  int* d_mid_err = nullptr;                      // sticky failure flag of k_mid
+  unsigned long long mid_seq = 0;                // launches so far (the barrier words carry it)
+  int mid_state = 0;                             // 0 unchecked, 1 usable, -1 not (placement probe)
+  bool no_mid = false;                           // OMG_NO_MID: the mid levels launch by launch
   bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
   long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch

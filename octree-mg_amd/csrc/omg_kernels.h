@@ -144,6 +144,43 @@ struct TailArgs {
 };
 // how many of the tail's lowest levels qualify for the LDS-resident program
 constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3
+
+// The mid levels of the V-cycle, right above the coarse tail (levels of at
+// most kMidMaxBoxes boxes of 16^3 or 8^3, all on this GPU): their steps run
+// in ONE launch of P workgroups that all sit on one XCD (the launch has 8P
+// workgroups; the round-robin dealer puts every eighth on XCD `xcd`, the
+// others leave at once), one box per workgroup and step, with a barrier
+// among the P between steps.  The XCD's workgroups share one L2, so the
+// barrier needs no L2 write-back: stores drained (s_waitcnt), an arrival
+// word per workgroup, a release word, then the CU's L1 invalidated.  Each
+// step is one box program of the level-by-level path (same arithmetic).
+constexpr int kMidMaxLevels = 6, kMidMaxSteps = 112, kMidMaxBoxes = 64, kMidBS = 512;
+enum MidKind : short { MS_SUB = 0, MS_LEX = 1, MS_FILL = 2, MS_RESID = 3, MS_CRHS = 4, MS_PFILL = 5 };
+struct MidLevel {
+  LevelView L;
+  GcBC bc;
+  const int* parents;        // my_parents (local indices)
+  int n_par;
+  const int* parent_local;   // [n] parent at the level below (MS_RESID / MS_PFILL)
+  const int* dixp;
+};
+struct MidStep {
+  short kind, li;            // MidKind; level (lv index; MS_RESID restricts onto li-1, MS_PFILL corrects li from li-1)
+  short e, colours;          // MS_SUB: colour and pushed colours; MS_PFILL: skip1
+};
+struct MidArgs {
+  int n_lvls, n_steps, P, xcd;
+  double lambda;
+  MidLevel lv[kMidMaxLevels];
+  MidStep st[kMidMaxSteps];
+  unsigned long long* sync;  // arrival words (16 apart) of the P workgroups, then the release word
+  int* err;                  // sticky: 1 = a barrier timed out, 2 = a workgroup was not on `xcd`
+};
+void launch_store_mid(const MidArgs& A, MidArgs* d, hipStream_t st);
+// seq: this launch's number (monotonic per context; the barrier words carry it)
+void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long seq, hipStream_t st);
+// one-time check: where the workgroups of an 8P launch run (out[8P] = XCC ids)
+void launch_xcc_probe(int* out, int n, hipStream_t st);
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 void launch_store_tail(const TailArgs& A, TailArgs* d, hipStream_t st);   // *d = A in stream order
 

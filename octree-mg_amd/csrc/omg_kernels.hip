@@ -866,7 +866,9 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   // z ghosts: lanes of group 0 (line 0, k = 1) read face k = 0, group 3
   // (line 3, k = 16) face k = 17
   const int gz = kq < 2 ? 2 * kLexGFace + kLexGPad + 15 * j - 18 : 3 * kLexGFace + kLexGPad + 15 * j - 33;
+#if !OMG_GS_REG_PERM
   const int lane_lo = (l + 48) & 63, lane_hi = (l + 16) & 63;
+#endif
 
   double rf[PF][4];
   double sink = 0.0;   // OMG_T_RING == 4

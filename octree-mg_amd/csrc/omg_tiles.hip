@@ -1971,4 +1971,174 @@ void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// The mid levels in one launch (MidArgs, omg_kernels.h).
+__device__ __forceinline__ int xcc_id() {
+  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): the XCD this wave runs on
+  return __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15;
+}
+
+constexpr long long kMidSpin = 1ll << 21;   // polls before a barrier gives up (~0.2 s)
+
+// the barrier among the P workgroups of one XCD; false: give up (timeout)
+__device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned long long val) {
+  unsigned long long* sync = A.sync;
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) in every wave: this workgroup's stores are in L2
+  __syncthreads();
+  bool ok = true;
+  if (w == 0) {
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x;
+      long long it = 0;
+      while (true) {
+        const unsigned long long v =
+            l > 0 && l < A.P ? __hip_atomic_load(sync + 16 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : val;
+        if (__all(v >= val)) break;
+        if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (l == 0) {
+        if (!ok) atomicOr(A.err, 1);
+        __hip_atomic_store(sync + 16 * kMidMaxBoxes, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else if (threadIdx.x == 0) {
+    __hip_atomic_store(sync + 16 * w, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long it = 0;
+    while (__hip_atomic_load(sync + 16 * kMidMaxBoxes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < val) {
+      if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        atomicOr(A.err, 1);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __shared__ int okw;
+  if (threadIdx.x == 0) okw = ok;
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");   // this CU's L1: the other workgroups' stores come from L2
+  return okw != 0;
+}
+
+// one box program per step kind, each compiled on its own (__noinline__):
+// inlined into one kernel their register demands add up (256 VGPRs, spills
+// at the 128 the co-residency needs)
+template <int NC, int OP>
+__device__ __noinline__ void mid_sub(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  const MidLevel& M = A.lv[S.li];
+  gsrb_box<NC, OP, kMidBS, 0>(M.L, A.lambda, S.e, S.colours, M.bc, nullptr, nullptr, b, lds);
+}
+template <int NC, int OP>
+__device__ __noinline__ void mid_lex(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  gs_lex_box<OP, NC>(A.lv[S.li].L, A.lambda, b, lds);
+}
+template <int NC>
+__device__ __noinline__ void mid_fill(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  // k_fill_tile's box program: the interior into LDS, then the faces
+  const MidLevel& M = A.lv[S.li];
+  const FaceTopo T = load_topo(M.L, b);
+  const double* u = M.L.phi + (long long)b * M.L.stride;
+  for (int q = threadIdx.x; q < Tl<NC>::HV; q += kMidBS)
+    reinterpret_cast<v2d*>(lds)[q] = reinterpret_cast<const v2d*>(u)[q];
+  __syncthreads();
+  tile_face_fill<NC>(M.L, b, T, lds, 3, M.bc, nullptr);
+}
+template <int NC, int OP>
+__device__ __noinline__ void mid_resid(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  const MidLevel& M = A.lv[S.li];
+  resid_restrict_box<NC, OP, kMidBS>(M.L, A.lv[S.li - 1].L, A.lambda, nullptr, 1, M.parent_local, M.dixp, b, lds);
+}
+template <int NC, int OP>
+__device__ __noinline__ void mid_crhs(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  const MidLevel& M = A.lv[S.li];
+  coarse_rhs_box<NC, OP, kMidBS>(M.L, A.lambda, M.parents[b], lds);
+}
+template <int NC>
+__device__ __noinline__ void mid_pfill(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  const MidLevel& M = A.lv[S.li];
+  prolong_fill_box<NC, kMidBS, true>(A.lv[S.li - 1].L, M.L, 4, M.parent_local, M.dixp, M.bc, nullptr, b, lds,
+                                      S.colours != 0);
+}
+
+template <int NC, int OP, bool LEX>
+__device__ __forceinline__ void mid_box(const MidArgs& A, const MidStep& S, int b, double* lds) {
+  switch (S.kind) {
+    case MS_SUB: mid_sub<NC, OP>(A, S, b, lds); break;
+    case MS_LEX:
+      if constexpr (LEX) mid_lex<NC, OP>(A, S, b, lds);
+      break;
+    case MS_FILL: mid_fill<NC>(A, S, b, lds); break;
+    case MS_RESID: mid_resid<NC, OP>(A, S, b, lds); break;
+    case MS_CRHS: mid_crhs<NC, OP>(A, S, b, lds); break;
+    case MS_PFILL: mid_pfill<NC>(A, S, b, lds); break;
+  }
+}
+
+// (two workgroups per CU, so that the P <= 64 participants are resident on
+// the XCD's 32 CUs at once: 4 waves per SIMD, at most 128 VGPRs)
+template <int OP, bool LEX>
+__global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ dA, unsigned long long seq) {
+  extern __shared__ double lds[];
+  const MidArgs& A = *dA;
+  if ((int)(blockIdx.x & 7) != A.xcd) return;
+  const int w = blockIdx.x >> 3, P = A.P;
+  if (xcc_id() != A.xcd) {   // not the round-robin placement the barrier relies on
+    if (threadIdx.x == 0) atomicOr(A.err, 2);
+    return;
+  }
+  for (int s = 0; s < A.n_steps; s++) {
+    const MidStep S = A.st[s];
+    const MidLevel& M = A.lv[S.li];
+    const int n = S.kind == MS_CRHS ? M.n_par : M.L.n;
+    for (int b = w; b < n; b += P) {
+      if (M.L.nc == 16)
+        mid_box<16, OP, LEX>(A, S, b, lds);
+      else
+        mid_box<8, OP, LEX>(A, S, b, lds);
+      __syncthreads();
+    }
+    if (!mid_barrier(A, w, (seq << 8) | (unsigned long long)(s + 1))) return;
+  }
+}
+
+static_assert(sizeof(MidArgs) + 16 <= 4096, "MidArgs must fit the 4 KiB kernel-argument limit");
+__global__ void __launch_bounds__(256) k_store_mid(MidArgs A, MidArgs* d) {
+  const unsigned* s = reinterpret_cast<const unsigned*>(&A);
+  unsigned* o = reinterpret_cast<unsigned*>(d);
+  for (int i = threadIdx.x; i < (int)(sizeof(MidArgs) / 4); i += blockDim.x) o[i] = s[i];
+}
+
+void launch_store_mid(const MidArgs& A, MidArgs* d, hipStream_t st) { k_store_mid<<<1, 256, 0, st>>>(A, d); }
+
+void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long seq, hipStream_t st) {
+  // LDS: the largest box program (16^3 residual tile; lexicographic GS: the box in LDS)
+  const size_t lds = sizeof(double) * (lex ? gs_lex_lds<16>() : Tl<16>::NST);
+  const dim3 g(8 * P);
+#define OMG_MID(OPV, LX)                                                                     \
+  {                                                                                          \
+    static bool attr = false;                                                                \
+    if (!attr) {                                                                             \
+      (void)hipFuncSetAttribute((const void*)k_mid<OPV, LX>,                                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);       \
+      attr = true;                                                                           \
+    }                                                                                        \
+    k_mid<OPV, LX><<<g, kMidBS, lds, st>>>(dA, seq);                                         \
+  }
+  if (op == OP_HELM) {
+    if (lex) OMG_MID(OP_HELM, true) else OMG_MID(OP_HELM, false)
+  } else {
+    if (lex) OMG_MID(OP_LPL, true) else OMG_MID(OP_LPL, false)
+  }
+#undef OMG_MID
+}
+
+__global__ void k_xcc_probe(int* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
+}
+void launch_xcc_probe(int* out, int n, hipStream_t st) { k_xcc_probe<<<n, 64, 0, st>>>(out); }
+
 }  // namespace omg
