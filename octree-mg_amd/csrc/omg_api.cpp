@@ -671,9 +671,10 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // Round 4: an even number of ring sweeps on a level whose faces are
     // same-GPU or physical runs with no fill in between: sweep n reads the
     // ghost set sweep n-1 pushed into (the box storage's own faces for odd
-    // n, d_galt for even n, whose physical ghosts it forms at load), so the
-    // last sweep lands in the box storage and only the physical ghosts are
-    // left to form (k_phys_gc).  The reference fills after every sweep
+    // n, d_galt for even n; every sweep after the first forms the physical
+    // ghosts at load, since only the same-GPU faces are pushed), so the last
+    // sweep lands in the box storage and only its physical ghosts are left to
+    // form (k_phys_gc).  The reference fills after every sweep
     // (m_multigrid.f90:412-423): the same values reach the same ghosts
     // before every read.  OMG_NO_GS_DBL: the fill after every sweep.
     if (xlf && L->d_galt && n_sub % 2 == 0 && L->n && !c->no_gs_dbl) {
@@ -686,7 +687,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
         gs.in_stride = odd ? L->stride : 6 * (long long)stored_face(L->nc);
         gs.out = odd ? L->d_galt : prim;
         gs.out_stride = odd ? 6 * (long long)stored_face(L->nc) : L->stride;
-        gs.phys_load = !odd;
+        gs.phys_load = n > 1;
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
         launch_gs_lex(L->view(), c->op, c->lambda, c->stream, L->d_rhs_lex, true, nullptr, &gs, &bc);
       }

@@ -79,6 +79,76 @@ __device__ __forceinline__ bool xcd_barrier2(unsigned* arrive, unsigned* release
   return ok;
 }
 
+// v3: the flags through L2 only: plain stores (write through L1 into the
+// XCD's L2), polls as plain loads after invalidating this CU's L1
+__device__ __forceinline__ unsigned l2_load(const unsigned* p) {
+  asm volatile("buffer_inv sc0" ::: "memory");
+  return *(volatile const unsigned*)p;
+}
+__device__ __forceinline__ bool xcd_barrier3(unsigned* arrive, unsigned* release, int s, int P, unsigned round,
+                                             int* err) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    *(volatile unsigned*)(arrive + 16 * s) = round;
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+  if (s == 0 && threadIdx.x < 64) {
+    long long it = 0;
+    const int l = threadIdx.x;
+    while (true) {
+      const unsigned v = l < P ? l2_load(arrive + 16 * l) : round;
+      if (__all(v >= round)) break;
+      if (++it > kSpinLimit) {
+        if (l == 0) *err = 1;
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (l == 0) {
+      *(volatile unsigned*)release = round;
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+  } else if (threadIdx.x == 0) {
+    long long it = 0;
+    while (l2_load(release) < round) {
+      if (++it > kSpinLimit) {
+        *err = 1;
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");
+  return ok;
+}
+
+__global__ void __launch_bounds__(256) k_bar3(int P, int rounds, unsigned* ctr, double* data, long long* t,
+                                              int* err, int* bad) {
+  __shared__ int slot;
+  if (xcc_id() != 0) return;
+  if (threadIdx.x == 0) slot = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int s = slot;
+  if (s >= P) return;
+  unsigned* arrive = ctr + 64;
+  unsigned* release = ctr + 32;
+  long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int r = 0; r < rounds; r++) {
+    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = (double)(r * 100000 + s * 1000 + q);
+    if (!xcd_barrier3(arrive, release, s, P, 2 * r + 1, err)) return;
+    const int o = (s + 1) % P;
+    for (int q = threadIdx.x; q < 512; q += 256)
+      if (data[(long long)o * 512 + q] != (double)(r * 100000 + o * 1000 + q)) atomicAdd(bad, 1);
+    if (!xcd_barrier3(arrive, release, s, P, 2 * r + 2, err)) return;
+  }
+  if (threadIdx.x == 0 && s == 0) t[0] = __builtin_amdgcn_s_memrealtime() - t0;
+}
+
 __global__ void __launch_bounds__(256) k_bar2(int P, int rounds, unsigned* ctr, double* data, long long* t,
                                               int* err, int* bad) {
   __shared__ int slot;
@@ -91,11 +161,11 @@ __global__ void __launch_bounds__(256) k_bar2(int P, int rounds, unsigned* ctr, 
   unsigned* release = ctr + 32;
   long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int r = 0; r < rounds; r++) {
-    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = r * 1000.0 + s + q * 1e-3;
+    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = (double)(r * 100000 + s * 1000 + q);
     if (!xcd_barrier2(arrive, release, s, P, 2 * r + 1, err)) return;
     const int o = (s + 1) % P;
     for (int q = threadIdx.x; q < 512; q += 256)
-      if (data[(long long)o * 512 + q] != r * 1000.0 + o + q * 1e-3) atomicAdd(bad, 1);
+      if (data[(long long)o * 512 + q] != (double)(r * 100000 + o * 1000 + q)) atomicAdd(bad, 1);
     if (!xcd_barrier2(arrive, release, s, P, 2 * r + 2, err)) return;
   }
   if (threadIdx.x == 0 && s == 0) t[0] = __builtin_amdgcn_s_memrealtime() - t0;
@@ -111,12 +181,13 @@ __global__ void __launch_bounds__(256) k_bar(int P, int rounds, unsigned* ctr, d
   if (s >= P) return;
   unsigned* cnt = ctr + 16;
   long long t0 = __builtin_amdgcn_s_memrealtime();
+  // (the values are integers: exact whatever the compiler contracts)
   for (int r = 0; r < rounds; r++) {
-    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = r * 1000.0 + s + q * 1e-3;
+    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = (double)(r * 100000 + s * 1000 + q);
     if (!xcd_barrier(cnt, (unsigned)(P * (r + 1)), err)) return;
     const int o = (s + 1) % P;
     for (int q = threadIdx.x; q < 512; q += 256)
-      if (data[(long long)o * 512 + q] != r * 1000.0 + o + q * 1e-3) atomicAdd(bad, 1);
+      if (data[(long long)o * 512 + q] != (double)(r * 100000 + o * 1000 + q)) atomicAdd(bad, 1);
     if (!xcd_barrier(cnt + 16, (unsigned)(P * (r + 1)), err)) return;
   }
   if (threadIdx.x == 0 && s == 0) t[0] = __builtin_amdgcn_s_memrealtime() - t0;
@@ -147,7 +218,7 @@ int main() {
   (void)hipMalloc(&t, 8);
   (void)hipMalloc(&err, 4);
   (void)hipMalloc(&bad, 4);
-  for (int v = 1; v <= 2; v++)
+  for (int v = 1; v <= 3; v++)
   for (int P : {8, 32, 64}) {
     const int rounds = 200;
     (void)hipMemset(ctr, 0, 4096);
@@ -157,8 +228,10 @@ int main() {
     (void)hipMemset(ctr, 0, 4096 * 4);
     if (v == 1)
       k_bar<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
-    else
+    else if (v == 2)
       k_bar2<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
+    else
+      k_bar3<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
     (void)hipDeviceSynchronize();
     long long ht;
     int he, hb;
