@@ -1397,6 +1397,7 @@ void run_mid(omg_ctx* c, int top, int mtop, bool down) {
   A.n_lvls = mtop - top + 1;
   A.lambda = c->lambda;
   A.xcd = 0;
+  A.bar_l2 = !c->mid_bar_dev;
   A.sync = c->d_mid_sync;
   A.err = c->d_mid_err;
   int P = 1;
@@ -2640,6 +2641,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->no_mid = env_flag("OMG_NO_MID");
+    c->mid_bar_dev = env_flag("OMG_MID_BAR_DEV");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");

@@ -269,6 +269,9 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const int p = tid + BS * g;
     if (p >= 6 * FH || OMG_SR_NOLOAD) continue;
     const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
+    // (physical and refinement-boundary faces have no neighbour box: their
+    // argument is a BC code or a coarse box index, not a box of this level)
+    if (BCK && T.kind(nb - 1) != NB_LOCAL) continue;
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
     const int d = (nb - 1) >> 1, nl = low ? NC : 1;
@@ -1980,6 +1983,18 @@ __device__ __forceinline__ int xcc_id() {
 
 constexpr long long kMidSpin = 1ll << 21;   // polls before a barrier gives up (~0.2 s)
 
+// the flag words: all participants share one XCD, hence one L2, so
+// group-scope accesses (bypassing the CU's L1) suffice; device scope goes
+// further out (A.bar_l2 = 0, the A/B alternative)
+__device__ __forceinline__ unsigned long long mid_flag_ld(const MidArgs& A, const unsigned long long* p) {
+  return A.bar_l2 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                  : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mid_flag_st(const MidArgs& A, unsigned long long* p, unsigned long long v) {
+  if (A.bar_l2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // the barrier among the P workgroups of one XCD; false: give up (timeout)
 __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned long long val) {
   unsigned long long* sync = A.sync;
@@ -1991,8 +2006,7 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
       const int l = threadIdx.x;
       long long it = 0;
       while (true) {
-        const unsigned long long v =
-            l > 0 && l < A.P ? __hip_atomic_load(sync + 16 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : val;
+        const unsigned long long v = l > 0 && l < A.P ? mid_flag_ld(A, sync + 16 * l) : val;
         if (__all(v >= val)) break;
         if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           ok = false;
@@ -2002,13 +2016,13 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
       }
       if (l == 0) {
         if (!ok) atomicOr(A.err, 1);
-        __hip_atomic_store(sync + 16 * kMidMaxBoxes, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mid_flag_st(A, sync + 16 * kMidMaxBoxes, val);
       }
     }
   } else if (threadIdx.x == 0) {
-    __hip_atomic_store(sync + 16 * w, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mid_flag_st(A, sync + 16 * w, val);
     long long it = 0;
-    while (__hip_atomic_load(sync + 16 * kMidMaxBoxes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < val) {
+    while (mid_flag_ld(A, sync + 16 * kMidMaxBoxes) < val) {
       if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         atomicOr(A.err, 1);
         ok = false;
@@ -2020,7 +2034,10 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
   __shared__ int okw;
   if (threadIdx.x == 0) okw = ok;
   __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");   // this CU's L1: the other workgroups' stores come from L2
+  // invalidate this CU's L1, so that the other workgroups' stores are read
+  // from L2.  Device scope (sc1): the group-scope form (sc0) leaves L1 alone
+  // outside thread-group-split mode (tools/xcd_probe.hip measured stale reads)
+  asm volatile("buffer_inv sc1" ::: "memory");
   return okw != 0;
 }
 

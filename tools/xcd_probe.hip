@@ -36,7 +36,7 @@ __device__ __forceinline__ bool xcd_barrier(unsigned* cnt, unsigned target, int*
     }
   }
   __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");   // this CU's L1: later loads come from L2
+  asm volatile("buffer_inv sc1" ::: "memory");   // this CU's L1 (sc0, group scope, is a no-op here)
   return ok;
 }
 
@@ -75,15 +75,15 @@ __device__ __forceinline__ bool xcd_barrier2(unsigned* arrive, unsigned* release
     }
   }
   __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");
+  asm volatile("buffer_inv sc1" ::: "memory");
   return ok;
 }
 
 // v3: the flags through L2 only: plain stores (write through L1 into the
-// XCD's L2), polls as plain loads after invalidating this CU's L1
+// XCD's L2), polls as group-scope loads (L1 bypassed)
 __device__ __forceinline__ unsigned l2_load(const unsigned* p) {
-  asm volatile("buffer_inv sc0" ::: "memory");
-  return *(volatile const unsigned*)p;
+  // a group-scope load (sc0): misses this CU's L1, served by the XCD's L2
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ bool xcd_barrier3(unsigned* arrive, unsigned* release, int s, int P, unsigned round,
                                              int* err) {
@@ -123,7 +123,7 @@ __device__ __forceinline__ bool xcd_barrier3(unsigned* arrive, unsigned* release
     }
   }
   __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");
+  asm volatile("buffer_inv sc1" ::: "memory");
   return ok;
 }
 
