@@ -863,6 +863,12 @@ void prolong(omg_ctx* c, int lvl, int iv, int iv_to, int add) {
 bool smooth_resid_ok(omg_ctx* c, int lvl) {
   const Level* F = level_ptr(c, lvl);
   const Level* C = level_ptr(c, lvl - 1);
+  // (a host refinement_bnd callback sets phi's ghosts on some faces: the
+  // kernel's sides_rb would stand in for it)
+  if (F) {
+    const auto rbh = F->rbh.find(1);
+    if (rbh != F->rbh.end() && rbh->second.n) return false;
+  }
   return !c->no_fuse_down && F && C && F->n && c->smoother == OMG_SMOOTHER_GSRB && c->n_substeps == 2 &&
          c->n_cycle_down >= 1 &&
          (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) &&
@@ -1340,23 +1346,26 @@ int tail_top(omg_ctx* c, int max_lvl) {
 // for an empty kernel (profiles/r04); a barrier among the workgroups of one
 // XCD costs ~1 us.
 
-// whether the 8P-workgroup launch deals its workgroups round-robin over the
-// 8 XCDs, as the mid kernel's barrier needs (checked once per context)
+// whether a launch deals its workgroups round-robin over the 8 XCDs (from
+// any starting XCD), as the mid kernel's barrier needs (checked once per
+// context, after a one-workgroup launch has moved the starting XCD on)
 bool mid_placement_ok(omg_ctx* c) {
   if (c->mid_state) return c->mid_state > 0;
   const int n = 8 * kMidMaxBoxes;
   int* d = nullptr;
-  HIPCHK(hipMalloc(&d, sizeof(int) * n));
+  HIPCHK(hipMalloc(&d, sizeof(int) * (n + 1)));
+  launch_xcc_probe(d + n, 1, c->stream);
   launch_xcc_probe(d, n, c->stream);
   std::vector<int> h(n);
   HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
   host_sync(c, c->stream);
   dfree(d);
-  bool ok = true;
-  for (int i = 0; i < n; i++) ok &= h[i] == i % 8;
+  bool ok = h[0] >= 0 && h[0] < 8;
+  for (int i = 0; i < n; i++) ok &= h[i] == (h[0] + i) % 8;
   if (!ok) std::fprintf(stderr, "omg: workgroups are not dealt round-robin over 8 XCDs; mid levels launch by launch\n");
   if (ok) {
-    dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 1), true);
+    // arrival words, the release word, two registration words
+    dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 2), true);
     dmalloc(&c->d_mid_err, sizeof(int), true);
     for (int k = 0; k < 2; k++) {
       dmalloc(&c->d_mid[k], sizeof(MidArgs));
@@ -1378,9 +1387,9 @@ int mid_top(omg_ctx* c, int top, int max_lvl) {
   for (int l = top + 1; l < max_lvl && l - top + 1 <= kMidMaxLevels; l++) {
     const Level* L = level_ptr(c, l);
     const Level* C = level_ptr(c, l - 1);
-    if (!L || L->n < 1 || L->n > kMidMaxBoxes || L->n != (int)c->ids[l].size() || (L->nc != 16 && L->nc != 8) ||
+    if (!L || L->n < 1 || L->n > c->mid_max_boxes || L->n != (int)c->ids[l].size() || (L->nc != 16 && L->nc != 8) ||
         L->has_rb || L->has_remote || L->n_pairs != L->n ||
-        !((size_t)L->n == 8 * C->parents.size() || C->nc * 2 == L->nc) || (int)C->parents.size() > kMidMaxBoxes)
+        !((size_t)L->n == 8 * C->parents.size() || C->nc * 2 == L->nc) || (int)C->parents.size() > c->mid_max_boxes)
       break;
     m = l;
   }
@@ -1397,7 +1406,6 @@ void run_mid(omg_ctx* c, int top, int mtop, bool down) {
   A.n_lvls = mtop - top + 1;
   A.lambda = c->lambda;
   A.xcd = 0;
-  A.bar_l2 = !c->mid_bar_dev;
   A.sync = c->d_mid_sync;
   A.err = c->d_mid_err;
   int P = 1;
@@ -1473,7 +1481,8 @@ void check_mid_err(omg_ctx* c) {
   if (e) {
     c->no_mid = true;
     HIPCHK(hipMemset(c->d_mid_err, 0, sizeof(int)));
-    throw OmgError(std::string("mid-level kernel failed (") + (e & 2 ? "workgroup off its XCD" : "barrier timeout") +
+    throw OmgError(std::string("mid-level kernel failed (") +
+                   (e & 2 ? "workgroups not dealt round-robin over the XCDs" : "barrier timeout") +
                    "): results of the last cycles are invalid; mid levels now launch by launch");
   }
 }
@@ -2641,7 +2650,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->no_mid = env_flag("OMG_NO_MID");
-    c->mid_bar_dev = env_flag("OMG_MID_BAR_DEV");
+    if (const char* v = getenv("OMG_MID_MAX_BOXES")) c->mid_max_boxes = std::min(std::max(std::atoi(v), 1), kMidMaxBoxes);
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
     c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");

@@ -170,7 +170,6 @@ struct MidStep {
 };
 struct MidArgs {
   int n_lvls, n_steps, P, xcd;
-  int bar_l2;                // barrier flags: 1 = group-scope accesses (L2), 0 = device scope
   double lambda;
   MidLevel lv[kMidMaxLevels];
   MidStep st[kMidMaxSteps];

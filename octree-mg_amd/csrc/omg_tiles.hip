@@ -1983,16 +1983,14 @@ __device__ __forceinline__ int xcc_id() {
 
 constexpr long long kMidSpin = 1ll << 21;   // polls before a barrier gives up (~0.2 s)
 
-// the flag words: all participants share one XCD, hence one L2, so
-// group-scope accesses (bypassing the CU's L1) suffice; device scope goes
-// further out (A.bar_l2 = 0, the A/B alternative)
-__device__ __forceinline__ unsigned long long mid_flag_ld(const MidArgs& A, const unsigned long long* p) {
-  return A.bar_l2 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                  : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// the flag words: device-scope accesses (sc1: past this CU's L1, which
+// other CUs' stores never refresh; group-scope loads hit it and spin on a
+// stale value, tools/xcd_probe.hip v3)
+__device__ __forceinline__ unsigned long long mid_flag_ld(const MidArgs&, const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void mid_flag_st(const MidArgs& A, unsigned long long* p, unsigned long long v) {
-  if (A.bar_l2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void mid_flag_st(const MidArgs&, unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the barrier among the P workgroups of one XCD; false: give up (timeout)
@@ -2033,11 +2031,13 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
   }
   __shared__ int okw;
   if (threadIdx.x == 0) okw = ok;
-  __syncthreads();
   // invalidate this CU's L1, so that the other workgroups' stores are read
-  // from L2.  Device scope (sc1): the group-scope form (sc0) leaves L1 alone
-  // outside thread-group-split mode (tools/xcd_probe.hip measured stale reads)
-  asm volatile("buffer_inv sc1" ::: "memory");
+  // from L2: device scope (sc1); the group-scope form (sc0) leaves L1 alone
+  // outside thread-group-split mode (tools/xcd_probe.hip measured stale
+  // reads).  One wave issues it (L1 is the CU's) and waits for it; the
+  // workgroup barrier then releases the others.
+  if (threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   return okw != 0;
 }
 
@@ -2101,11 +2101,17 @@ template <int OP, bool LEX>
 __global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ dA, unsigned long long seq) {
   extern __shared__ double lds[];
   const MidArgs& A = *dA;
-  if ((int)(blockIdx.x & 7) != A.xcd) return;
+  // the participants: the P workgroups the dispatcher dealt to XCD A.xcd.
+  // Workgroups go round-robin over the 8 XCDs from wherever the previous
+  // dispatch stopped, so those are blockIdx = x0 + 8w, w = 0..P-1; each
+  // registers its slot (a slot taken twice: not that placement, error 2; a
+  // slot missing: the first barrier times out, error 1)
+  if (xcc_id() != A.xcd) return;
   const int w = blockIdx.x >> 3, P = A.P;
-  if (xcc_id() != A.xcd) {   // not the round-robin placement the barrier relies on
-    if (threadIdx.x == 0) atomicOr(A.err, 2);
-    return;
+  unsigned long long* reg = A.sync + 16 * (kMidMaxBoxes + 1) + (seq & 1);
+  if (threadIdx.x == 0) {
+    const unsigned long long bit = 1ull << w;
+    if (atomicOr(reg, bit) & bit) atomicOr(A.err, 2);
   }
   for (int s = 0; s < A.n_steps; s++) {
     const MidStep S = A.st[s];
@@ -2119,6 +2125,9 @@ __global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ d
       __syncthreads();
     }
     if (!mid_barrier(A, w, (seq << 8) | (unsigned long long)(s + 1))) return;
+    // every participant has registered: clear this launch's word for the
+    // launch after next (stream order keeps the launches apart)
+    if (s == 0 && w == 0 && threadIdx.x == 0) atomicExch(reg, 0ull);
   }
 }
 

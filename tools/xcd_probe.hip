@@ -36,7 +36,7 @@ __device__ __forceinline__ bool xcd_barrier(unsigned* cnt, unsigned target, int*
     }
   }
   __syncthreads();
-  asm volatile("buffer_inv sc1" ::: "memory");   // this CU's L1 (sc0, group scope, is a no-op here)
+  asm volatile("buffer_inv sc1" ::: "memory");   // this CU's L1, from every wave (v2/v3: one wave)
   return ok;
 }
 
@@ -74,8 +74,45 @@ __device__ __forceinline__ bool xcd_barrier2(unsigned* arrive, unsigned* release
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  if (threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  asm volatile("buffer_inv sc1" ::: "memory");
+  return ok;
+}
+
+// v4: v2 without the L1 invalidation; the payload is read with nt loads,
+// which bypass L1 (served by the XCD's L2)
+__device__ __forceinline__ bool xcd_barrier4(unsigned* arrive, unsigned* release, int s, int P, unsigned round,
+                                             int* err) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x == 0) __hip_atomic_store(arrive + 16 * s, round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (s == 0 && threadIdx.x < 64) {
+    long long it = 0;
+    const int l = threadIdx.x;
+    while (true) {
+      const unsigned v = l < P ? __hip_atomic_load(arrive + 16 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : round;
+      if (__all(v >= round)) break;
+      if (++it > kSpinLimit) {
+        if (l == 0) *err = 1;
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (l == 0) __hip_atomic_store(release, round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (threadIdx.x == 0) {
+    long long it = 0;
+    while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < round) {
+      if (++it > kSpinLimit) {
+        *err = 1;
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
   return ok;
 }
 
@@ -122,8 +159,8 @@ __device__ __forceinline__ bool xcd_barrier3(unsigned* arrive, unsigned* release
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  if (threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  asm volatile("buffer_inv sc1" ::: "memory");
   return ok;
 }
 
@@ -167,6 +204,28 @@ __global__ void __launch_bounds__(256) k_bar2(int P, int rounds, unsigned* ctr, 
     for (int q = threadIdx.x; q < 512; q += 256)
       if (data[(long long)o * 512 + q] != (double)(r * 100000 + o * 1000 + q)) atomicAdd(bad, 1);
     if (!xcd_barrier2(arrive, release, s, P, 2 * r + 2, err)) return;
+  }
+  if (threadIdx.x == 0 && s == 0) t[0] = __builtin_amdgcn_s_memrealtime() - t0;
+}
+
+__global__ void __launch_bounds__(256) k_bar4(int P, int rounds, unsigned* ctr, double* data, long long* t,
+                                              int* err, int* bad) {
+  __shared__ int slot;
+  if (xcc_id() != 0) return;
+  if (threadIdx.x == 0) slot = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int s = slot;
+  if (s >= P) return;
+  unsigned* arrive = ctr + 64;
+  unsigned* release = ctr + 32;
+  long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int r = 0; r < rounds; r++) {
+    for (int q = threadIdx.x; q < 512; q += 256) data[(long long)s * 512 + q] = (double)(r * 100000 + s * 1000 + q);
+    if (!xcd_barrier4(arrive, release, s, P, 2 * r + 1, err)) return;
+    const int o = (s + 1) % P;
+    for (int q = threadIdx.x; q < 512; q += 256)
+      if (__builtin_nontemporal_load(&data[(long long)o * 512 + q]) != (double)(r * 100000 + o * 1000 + q)) atomicAdd(bad, 1);
+    if (!xcd_barrier4(arrive, release, s, P, 2 * r + 2, err)) return;
   }
   if (threadIdx.x == 0 && s == 0) t[0] = __builtin_amdgcn_s_memrealtime() - t0;
 }
@@ -218,7 +277,7 @@ int main() {
   (void)hipMalloc(&t, 8);
   (void)hipMalloc(&err, 4);
   (void)hipMalloc(&bad, 4);
-  for (int v = 1; v <= 3; v++)
+  for (int v = 1; v <= 4; v++)
   for (int P : {8, 32, 64}) {
     const int rounds = 200;
     (void)hipMemset(ctr, 0, 4096);
@@ -230,8 +289,10 @@ int main() {
       k_bar<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
     else if (v == 2)
       k_bar2<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
-    else
+    else if (v == 3)
       k_bar3<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
+    else
+      k_bar4<<<8 * P, 256>>>(P, rounds, ctr, data, t, err, bad);
     (void)hipDeviceSynchronize();
     long long ht;
     int he, hb;
