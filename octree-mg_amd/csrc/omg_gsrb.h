@@ -370,7 +370,9 @@ constexpr int gs_lex_lds() { return (NC + 2) * (NC + 2) * (NC + 2) + NC * NC * N
 #ifndef OMG_T_LEX
 #define OMG_T_LEX 0
 #endif
-template <int OP, int NC>
+// NTL: every load non-temporal (past this CU's L1: the mid kernel reads data
+// other workgroups of the launch wrote, omg_tiles.hip k_mid)
+template <int OP, int NC, bool NTL = false>
 __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, int b, double* lds) {
   constexpr int S = NC + 2, S3 = S * S * S, N3 = NC * NC * NC;
   double* P = lds;         // phi(0:nc+1)^3, i fastest (edges and corners unused)
@@ -381,10 +383,13 @@ __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, in
   for (int q = threadIdx.x; q < S3 && OMG_T_LEX != 2; q += blockDim.x) {
     const int i = q % S, j = (q / S) % S, k = q / (S * S);
     const int nbd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
-    P[q] = nbd <= 1 ? u[off_cell(L, i, j, k)] : 0.0;
+    const double* up = u + off_cell(L, i, j, k);
+    P[q] = nbd <= 1 ? (NTL ? __builtin_nontemporal_load(up) : *up) : 0.0;
   }
-  for (int q = threadIdx.x; q < N3 && OMG_T_LEX != 2; q += blockDim.x)
-    R[q] = f[off_int(L, q % NC + 1, (q / NC) % NC + 1, q / (NC * NC) + 1)];
+  for (int q = threadIdx.x; q < N3 && OMG_T_LEX != 2; q += blockDim.x) {
+    const double* fp = f + off_int(L, q % NC + 1, (q / NC) % NC + 1, q / (NC * NC) + 1);
+    R[q] = NTL ? __builtin_nontemporal_load(fp) : *fp;
+  }
   __syncthreads();
   for (int d = 3; d <= 3 * NC && OMG_T_LEX != 1; d++) {
     for (int p = threadIdx.x; p < NC * NC; p += blockDim.x) {

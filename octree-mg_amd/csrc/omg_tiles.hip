@@ -373,9 +373,10 @@ constexpr int prolong_cb() { return ((NC / 2 + 2) * (NC / 2 + 2) * (NC / 2 + 2) 
 // the edge cells the parent stores, for the siblings' boundary cells).  Loads
 // are all issued before any store: the res stores alias the phi/old loads, so
 // an interleaved loop would serialise every load behind the previous store.
-template <int NC, int BS, bool SUB, bool EDGES = false>
+template <int NC, int BS, bool SUB, bool EDGES = false, bool NTL = false>
 __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, int pb, int dx, int dy, int dz,
                                                    double* cb) {
+  auto ld = [](const double* p) { return NTL ? __builtin_nontemporal_load(p) : *p; };
   constexpr int CB = NC / 2 + 2, N = CB * CB * CB, NQ = (N + BS - 1) / BS;
   const int tid = threadIdx.x;
   const int n1 = Cv.nc + 1;
@@ -395,10 +396,10 @@ __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, 
     const int o = off_cell(Cv, x, y, z);
     off[r] = o;
     if (SUB) {
-      rv[r] = boxp(Cv, 1, pb)[o] - boxp(Cv, 3, pb)[o];
+      rv[r] = ld(boxp(Cv, 1, pb) + o) - ld(boxp(Cv, 3, pb) + o);
       if (nbnd == 0 || (nbnd == 1 && nghost)) store |= 1u << r;
     } else {
-      rv[r] = boxp(Cv, iv, pb)[o];
+      rv[r] = ld(boxp(Cv, iv, pb) + o);
     }
   }
 #pragma unroll
@@ -417,7 +418,8 @@ __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, 
 // save_old: FMG's `old = phi` of this level (m_multigrid.f90:127-129) for the
 // interior, from the pre-correction values loaded here anyway (the caller
 // copies the ghost faces before the launch; needs !skip1: every pair loaded).
-template <int NC, int BS, bool SUB, bool RB = false>
+// NTL: the parent loads non-temporal too (the mid kernel, k_mid)
+template <int NC, int BS, bool SUB, bool RB = false, bool NTL = false>
 __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
                                                  const int* parent_local, const int* dixp, const GcBC& bc,
                                                  double* sendbuf, int b, double* lds, bool skip1,
@@ -439,7 +441,7 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     const int q2 = tid + BS * r;
     if (q2 < npair) old[r] = ld_nt(u + 2 * q2);
   }
-  load_parent_octant<NC, BS, SUB>(Cv, iv, pb, dx, dy, dz, cb);
+  load_parent_octant<NC, BS, SUB, false, NTL>(Cv, iv, pb, dx, dy, dz, cb);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < NR; r++) {
@@ -1982,6 +1984,9 @@ __device__ __forceinline__ int xcc_id() {
 }
 
 constexpr long long kMidSpin = 1ll << 21;   // polls before a barrier gives up (~0.2 s)
+#ifndef OMG_MID_INV
+#define OMG_MID_INV 0
+#endif
 
 // the flag words: device-scope accesses (sc1: past this CU's L1, which
 // other CUs' stores never refresh; group-scope loads hit it and spin on a
@@ -2031,12 +2036,14 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
   }
   __shared__ int okw;
   if (threadIdx.x == 0) okw = ok;
-  // invalidate this CU's L1, so that the other workgroups' stores are read
-  // from L2: device scope (sc1); the group-scope form (sc0) leaves L1 alone
-  // outside thread-group-split mode (tools/xcd_probe.hip measured stale
-  // reads).  One wave issues it (L1 is the CU's) and waits for it; the
-  // workgroup barrier then releases the others.
-  if (threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  // Every load of the box programs in this kernel is non-temporal: those
+  // bypass this CU's L1 (which other CUs' stores never refresh) and read the
+  // XCD's L2, where every participant's stores are once its vmcnt(0) wait
+  // above has passed.  OMG_MID_INV=1 instead invalidates L1 (device-scope
+  // buffer_inv, one wave; the group-scope form leaves L1 alone outside
+  // thread-group-split mode): 2.6 us per barrier at 8 workgroups on the
+  // XCD, 15.6 us at 64 (tools/xcd_probe.hip).
+  if (OMG_MID_INV && threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   return okw != 0;
 }
@@ -2047,11 +2054,11 @@ __device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned lo
 template <int NC, int OP>
 __device__ __noinline__ void mid_sub(const MidArgs& A, const MidStep& S, int b, double* lds) {
   const MidLevel& M = A.lv[S.li];
-  gsrb_box<NC, OP, kMidBS, 0>(M.L, A.lambda, S.e, S.colours, M.bc, nullptr, nullptr, b, lds);
+  gsrb_box<NC, OP, kMidBS, 2>(M.L, A.lambda, S.e, S.colours, M.bc, nullptr, nullptr, b, lds);
 }
 template <int NC, int OP>
 __device__ __noinline__ void mid_lex(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  gs_lex_box<OP, NC>(A.lv[S.li].L, A.lambda, b, lds);
+  gs_lex_box<OP, NC, true>(A.lv[S.li].L, A.lambda, b, lds);
 }
 template <int NC>
 __device__ __noinline__ void mid_fill(const MidArgs& A, const MidStep& S, int b, double* lds) {
@@ -2060,7 +2067,7 @@ __device__ __noinline__ void mid_fill(const MidArgs& A, const MidStep& S, int b,
   const FaceTopo T = load_topo(M.L, b);
   const double* u = M.L.phi + (long long)b * M.L.stride;
   for (int q = threadIdx.x; q < Tl<NC>::HV; q += kMidBS)
-    reinterpret_cast<v2d*>(lds)[q] = reinterpret_cast<const v2d*>(u)[q];
+    reinterpret_cast<v2d*>(lds)[q] = ld_nt(u + 2 * q);
   __syncthreads();
   tile_face_fill<NC>(M.L, b, T, lds, 3, M.bc, nullptr);
 }
@@ -2072,13 +2079,13 @@ __device__ __noinline__ void mid_resid(const MidArgs& A, const MidStep& S, int b
 template <int NC, int OP>
 __device__ __noinline__ void mid_crhs(const MidArgs& A, const MidStep& S, int b, double* lds) {
   const MidLevel& M = A.lv[S.li];
-  coarse_rhs_box<NC, OP, kMidBS>(M.L, A.lambda, M.parents[b], lds);
+  coarse_rhs_box<NC, OP, kMidBS, true>(M.L, A.lambda, M.parents[b], lds);
 }
 template <int NC>
 __device__ __noinline__ void mid_pfill(const MidArgs& A, const MidStep& S, int b, double* lds) {
   const MidLevel& M = A.lv[S.li];
-  prolong_fill_box<NC, kMidBS, true>(A.lv[S.li - 1].L, M.L, 4, M.parent_local, M.dixp, M.bc, nullptr, b, lds,
-                                      S.colours != 0);
+  prolong_fill_box<NC, kMidBS, true, false, true>(A.lv[S.li - 1].L, M.L, 4, M.parent_local, M.dixp, M.bc, nullptr,
+                                                   b, lds, S.colours != 0);
 }
 
 template <int NC, int OP, bool LEX>

@@ -256,3 +256,42 @@ def test_refinement_bnd_callback_restating_sides_rb():
     assert _cycles(be, cfg) == e["runs"]["1"]["history"]
     assert phi_digest(be) == e["runs"]["1"]["phi_sha256"]
     assert calls and set(calls) == set(range(1, 7))
+
+
+# the mid levels (<= OMG_MID_MAX_BOXES boxes right above the coarse tail) in
+# one launch per half-cycle (k_mid: workgroups of one XCD, a barrier between
+# box programs, every load non-temporal), with the cap at 8 (default) and 64
+MID_CASES = ["16 128 128 128 2 v gsrb lpl 0 sol sol 1 lb 0",
+             "16 128 128 128 2 v gs helm 2 d0 sol 1 lb 0",
+             "8 64 64 64 2 v gsrb lpl 0 per sol 1 lb 0",
+             "8 64 64 64 2 f gs lpl 0 n0 sol 1 lb 1",
+             "16 128 128 128 2 v gsrb lpl 0 sol sol 2 lb 0"]
+
+
+def _mid_launches(dev):
+    n = 0
+    for lvl in dev.levels():
+        for fam in ("mid_down", "mid_up"):
+            n += dev.mg.ctx.kernel_stats(f"{fam}@{lvl}")[0]
+    return n
+
+
+@pytest.mark.parametrize("cap", ["8", "64"])
+@pytest.mark.parametrize("args", MID_CASES)
+def test_mid_levels_match_oracle(args, cap, monkeypatch):
+    monkeypatch.setenv("OMG_MID_MAX_BOXES", cap)
+    cfg = parse(args)
+    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+    for be in (dev, orc):
+        setup_problem(be)
+    c = dev.mg.ctx
+    c.call("reset_stats")
+    c.call("set_profiling", 1)
+    for _ in range(2):
+        if cfg["cycle"] == "f":
+            assert dev.fmg(True, True) == orc.fmg(True, True)
+        else:
+            assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc, ivs=(1, 2, 3, 4))
+    c.call("set_profiling", 0)
+    assert _mid_launches(dev) > 0, "the mid kernel did not run"
