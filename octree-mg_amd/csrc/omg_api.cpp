@@ -873,9 +873,14 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
          c->n_cycle_down >= 1 &&
          (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) &&
          !(c->no_fuse_down_bc && (F->has_rb || F->has_phys)) && (!F->has_remote || F->n_int) &&
-         // (refinement boundaries across ranks exchange coarse faces after every
-         // substep: no fusion there, decided alike on every rank)
-         !(F->any_rb && c->n_ranks > 1);
+         // Physical / refinement-boundary faces fuse on one GPU only, decided
+         // alike on every rank.  On a split level the boxes with a remote face
+         // run the plain substep first, whose epilogue rewrites both colour
+         // halves of their physical ghosts, and the fused interior boxes' edge
+         // taps would then read colour-1 ghosts one substep too new; across
+         // ranks, refinement boundaries also exchange coarse faces after every
+         // substep.
+         !(c->n_ranks > 1 && (F->any_phys || F->any_rb));
 }
 
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down

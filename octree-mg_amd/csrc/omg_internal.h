@@ -311,9 +311,9 @@ struct omg_ctx {
   int mid_state = 0;                             // 0 unchecked, 1 usable, -1 not (placement probe)
   bool no_mid = false;                           // OMG_NO_MID: the mid levels launch by launch
   // levels of at most this many boxes run in the mid kernel (OMG_MID_MAX_BOXES,
-  // <= kMidMaxBoxes): its barrier's L1 invalidation grows with the workgroups
-  // per XCD (2.6 us at 8, 15.6 us at 64, profiles/r04/xcd_probe.txt)
-  int mid_max_boxes = 8;
+  // 1..kMidMaxBoxes, A/B runs); its barrier costs 1.4-1.8 us at 8-64
+  // workgroups on the XCD (tools/xcd_probe.hip v4)
+  int mid_max_boxes = 64;
   bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
   long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch
