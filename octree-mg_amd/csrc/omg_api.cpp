@@ -972,9 +972,13 @@ void correct_children(omg_ctx* c, int lvl) {
 bool prolong_smooth(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
+  // refinement-boundary faces: on one GPU, formed on the device (no host
+  // refinement_bnd for phi), 16^3 / 8^3 boxes
+  const bool rb_ok = F && !c->no_rb_fill_fuse && c->n_ranks == 1 && (F->nc == 16 || F->nc == 8) &&
+                     !(F->rbh.count(1) && F->rbh.at(1).n);
   if (c->no_fuse_up || !F || !C || !F->prolong_smooth_ok || c->smoother != OMG_SMOOTHER_GSRB ||
       (c->op != OP_LPL && c->op != OP_HELM) ||
-      c->n_cycle_up < 1 || F->has_rb || (F->has_remote && !F->n_int) || !gs_tiled(F->nc, c->op, F->has_rb) ||
+      c->n_cycle_up < 1 || (F->has_rb && !rb_ok) || (F->has_remote && !F->n_int) || !gs_tiled(F->nc, c->op, F->has_rb) ||
       !((size_t)F->n == 8 * C->parents.size() || C->nc * 2 == F->nc) ||
       (c->n_ranks > 1 && (F->prol.n_send || F->prol.n_recv)))
     return false;
@@ -986,7 +990,7 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
     Prof p(c, "prolong_smooth", (double)n * F->nc * F->nc * F->nc, lvl + 1);
     launch_prolong_smooth(C->view(), F->sweep_view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
                           bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, split ? F->d_int : nullptr, n,
-                          split ? F->d_push0 : nullptr, c->stream);
+                          split ? F->d_push0 : nullptr, c->stream, F->has_rb);
   }
   if (split) {
     // multi-GPU: boxes with a face on another GPU take the unfused pair,
@@ -1351,41 +1355,24 @@ int tail_top(omg_ctx* c, int max_lvl) {
 // for an empty kernel (profiles/r04); a barrier among the workgroups of one
 // XCD costs ~1 us.
 
-// whether a launch deals its workgroups round-robin over the 8 XCDs (from
-// any starting XCD), as the mid kernel's barrier needs (checked once per
-// context, after a one-workgroup launch has moved the starting XCD on)
-bool mid_placement_ok(omg_ctx* c) {
-  if (c->mid_state) return c->mid_state > 0;
-  const int n = 8 * kMidMaxBoxes;
-  int* d = nullptr;
-  HIPCHK(hipMalloc(&d, sizeof(int) * (n + 1)));
-  launch_xcc_probe(d + n, 1, c->stream);
-  launch_xcc_probe(d, n, c->stream);
-  std::vector<int> h(n);
-  HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
-  host_sync(c, c->stream);
-  dfree(d);
-  bool ok = h[0] >= 0 && h[0] < 8;
-  for (int i = 0; i < n; i++) ok &= h[i] == (h[0] + i) % 8;
-  if (!ok) std::fprintf(stderr, "omg: workgroups are not dealt round-robin over 8 XCDs; mid levels launch by launch\n");
-  if (ok) {
-    // arrival words, the release word, two registration words
-    dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 2), true);
-    dmalloc(&c->d_mid_err, sizeof(int), true);
-    for (int k = 0; k < 2; k++) {
-      dmalloc(&c->d_mid[k], sizeof(MidArgs));
-      c->h_mid[k] = new MidArgs;
-      std::memset(c->h_mid[k], 0xff, sizeof(MidArgs));
-    }
+// the mid kernel's device words and argument blocks (once per context)
+void mid_alloc(omg_ctx* c) {
+  if (c->d_mid_sync) return;
+  dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 4), true);
+  dmalloc(&c->d_mid_err, sizeof(int), true);
+  for (int k = 0; k < 2; k++) {
+    dmalloc(&c->d_mid[k], sizeof(MidArgs));
+    c->h_mid[k] = new MidArgs;
+    std::memset(c->h_mid[k], 0xff, sizeof(MidArgs));
   }
-  c->mid_state = ok ? 1 : -1;
-  return ok;
 }
 
 // The highest level of the run top+1 .. that qualifies (INT_MIN: none), for a
 // cycle whose highest level is max_lvl (mid levels lie strictly below it)
 int mid_top(omg_ctx* c, int top, int max_lvl) {
-  if (c->no_mid || c->capturing || (c->op != OP_LPL && c->op != OP_HELM)) return INT_MIN;
+  // (loopback: several contexts share the GPU, and two mid kernels waiting
+  // for their groups could hold each other's workgroup slots)
+  if (c->no_mid || c->capturing || (c->op != OP_LPL && c->op != OP_HELM) || c->loop) return INT_MIN;
   const Level* T = level_ptr(c, top);
   if (!T || (T->nc != 16 && T->nc != 8)) return INT_MIN;
   int m = INT_MIN;
@@ -1398,7 +1385,8 @@ int mid_top(omg_ctx* c, int top, int max_lvl) {
       break;
     m = l;
   }
-  if (m == INT_MIN || !level_ptr(c, m)->phi_gc_ok || !mid_placement_ok(c)) return INT_MIN;
+  if (m == INT_MIN || !level_ptr(c, m)->phi_gc_ok) return INT_MIN;
+  mid_alloc(c);
   return m;
 }
 
@@ -1410,7 +1398,6 @@ void run_mid(omg_ctx* c, int top, int mtop, bool down) {
   std::memset(&A, 0, sizeof(A));   // padding too: compared bytewise below
   A.n_lvls = mtop - top + 1;
   A.lambda = c->lambda;
-  A.xcd = 0;
   A.sync = c->d_mid_sync;
   A.err = c->d_mid_err;
   int P = 1;
@@ -1480,14 +1467,13 @@ void run_mid(omg_ctx* c, int top, int mtop, bool down) {
 
 // A failure of the mid kernel (sticky flag) raised at the next host wait
 void check_mid_err(omg_ctx* c) {
-  if (c->mid_state <= 0) return;
+  if (!c->d_mid_err) return;
   int e = 0;
   HIPCHK(hipMemcpy(&e, c->d_mid_err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     c->no_mid = true;
     HIPCHK(hipMemset(c->d_mid_err, 0, sizeof(int)));
-    throw OmgError(std::string("mid-level kernel failed (") +
-                   (e & 2 ? "workgroups not dealt round-robin over the XCDs" : "barrier timeout") +
+    throw OmgError(std::string("mid-level kernel failed (a wait timed out") +
                    "): results of the last cycles are invalid; mid levels now launch by launch");
   }
 }
@@ -2551,7 +2537,7 @@ void build_plan(omg_ctx* c) {
       T.child_offset(F.ids[b], d);
       for (int nb = 1; nb <= 6; nb++) {
         const int kind = F.h_nbk[(size_t)b * 6 + nb - 1];
-        if (kind == NB_PHYS) continue;
+        if (kind == NB_PHYS || kind == NB_RB) continue;   // (formed from the box's own cells)
         if (kind != NB_LOCAL) { F.prolong_smooth_ok = false; break; }
         const bool low = nb & 1;
         const bool sib = !one_child && (low ? d[(nb - 1) >> 1] == F.nc / 2 : d[(nb - 1) >> 1] == 0);

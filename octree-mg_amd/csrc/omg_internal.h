@@ -308,7 +308,6 @@ struct omg_ctx {
   unsigned long long* d_mid_sync = nullptr;      // barrier words
   int* d_mid_err = nullptr;                      // sticky failure flag of k_mid
   unsigned long long mid_seq = 0;                // launches so far (the barrier words carry it)
-  int mid_state = 0;                             // 0 unchecked, 1 usable, -1 not (placement probe)
   bool no_mid = false;                           // OMG_NO_MID: the mid levels launch by launch
   // levels of at most this many boxes run in the mid kernel (OMG_MID_MAX_BOXES,
   // 1..kMidMaxBoxes, A/B runs); its barrier costs 1.4-1.8 us at 8-64

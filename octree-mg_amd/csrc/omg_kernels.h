@@ -169,18 +169,18 @@ struct MidStep {
   short e, colours;          // MS_SUB: colour and pushed colours; MS_PFILL: skip1
 };
 struct MidArgs {
-  int n_lvls, n_steps, P, xcd;
+  int n_lvls, n_steps, P, pad_;
   double lambda;
   MidLevel lv[kMidMaxLevels];
   MidStep st[kMidMaxSteps];
-  unsigned long long* sync;  // arrival words (16 apart) of the P workgroups, then the release word
-  int* err;                  // sticky: 1 = a barrier timed out, 2 = a workgroup was not on `xcd`
+  // arrival words (16 apart) of the P workgroups, the release word, then two
+  // placement blocks (8 per-XCD ticket counters and the chosen XCD)
+  unsigned long long* sync;
+  int* err;                  // sticky: 1 = a wait timed out
 };
 void launch_store_mid(const MidArgs& A, MidArgs* d, hipStream_t st);
 // seq: this launch's number (monotonic per context; the barrier words carry it)
 void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long seq, hipStream_t st);
-// one-time check: where the workgroups of an 8P launch run (out[8P] = XCC ids)
-void launch_xcc_probe(int* out, int n, hipStream_t st);
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 void launch_store_tail(const TailArgs& A, TailArgs* d, hipStream_t st);   // *d = A in stream order
 
@@ -215,11 +215,12 @@ void launch_prolong_fill(const LevelView& C, const LevelView& F, int iv, const i
 // old = phi on the ghost faces (and padding) of every box: [2*hv, stride)
 void launch_copy_ghosts(const LevelView& L, hipStream_t st);
 // correct_children + fill + the first up-smoothing substep (colour 1) in one
-// pass; fine boxes with their parent here and no remote / refinement faces
-// (all, or the `list`); push0: per box, faces to push the corrected colour 0 to
+// pass; fine boxes with their parent here and no remote faces (all, or the
+// `list`); push0: per box, faces to push the corrected colour 0 to; rb: the
+// level has refinement-boundary faces (one GPU, 16^3 / 8^3 boxes)
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
                            const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
-                           const uint8_t* push0, hipStream_t st);
+                           const uint8_t* push0, hipStream_t st, bool rb = false);
 // update_coarse's parent loop, LDS-tiled; false when the box size / operator
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,

@@ -288,6 +288,22 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
       if (ea) gedge[g][1] = e; else gedge[g][0] = e;
     }
   }
+  // the coarse operands of refinement-boundary faces (sides_rb): the coarse
+  // boxes across them are leaves, which the restriction below never writes
+  constexpr int NF = 6 * NC * NC, NPF = (NF + BS - 1) / BS;
+  RbCoarse rt[BCK == 2 ? NPF : 1];
+  if constexpr (BCK == 2) {
+    if (T.nonlocal()) {
+#pragma unroll
+      for (int r = 0; r < NPF; r++) {
+        const int p = tid + BS * r;
+        if (p >= NF) continue;
+        const int f = p / (NC * NC), cell = p % (NC * NC);
+        if (T.kind(f) != NB_RB) continue;
+        rt[r] = rb_coarse_load(F, RbSide{Cv, nullptr}, rb_unpack(F, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
+      }
+    }
+  }
   if (OMG_SR_EARLY) bulk_loads();
   __syncthreads();
 
@@ -315,28 +331,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
     const int d = (nb - 1) >> 1;
-    const int kind = T.kind(nb - 1);
-    if (BCK && kind != NB_LOCAL) {
-      // both colour halves at this slot: (a, c) of colour 0 and (a1, c) of colour 1
-      const int a1 = 2 * ah + 1 + ((gl + c) & 1);
-      double gv[2];
-#pragma unroll
-      for (int col = 0; col < 2; col++) {
-        const int aa = col ? a1 : a;
-        const double x1 = sb[sr_int<NC>(d, low ? 1 : NC, aa, c)], x2 = sb[sr_int<NC>(d, low ? 2 : NC - 1, aa, c)];
-        if (kind == NB_PHYS)
-          gv[col] = phys_ghost(F, bc, b, (long long)b * 6 + nb - 1, nb, T.phys_code(nb - 1), aa, c,
-                               TL::ogh(nb, aa, c), x1, x2);
-        else if (BCK == 2)
-          gv[col] = rb_ghost(F, RbSide{Cv, nullptr}, T.arg(nb - 1), nb, aa, c, x1, x2);
-        else
-          gv[col] = 0.0;   // (unreachable: the host fuses no other face kind)
-      }
-      sb[2 * HV + (nb - 1) * FS + hi] = gv[0];
-      sb[2 * HV + (nb - 1) * FS + FH + hi] = gv[1];
-      u[2 * HV + (nb - 1) * FS + hi] = gv[0];
-      continue;
-    }
+    if (BCK && T.kind(nb - 1) != NB_LOCAL) continue;   // (the loop below)
     const double across = sb[sr_int<NC>(d, low ? 1 : NC, a, c)];
     const bool ea = a == 1 || a == NC;
     // along the face normal, then the two tangential axes (t1 < t2)
@@ -354,6 +349,29 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     s.zm = d == 2 ? dm : cm;
     s.zp = d == 2 ? dp : cp;
     sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, grhs[g]);
+  }
+  // physical / refinement-boundary faces: both colours of their ghosts from
+  // our final cells (the coarse operands of refinement-boundary cells were
+  // loaded with the neighbour operands above)
+  if (BCK && T.nonlocal()) {
+#pragma unroll
+    for (int r = 0; r < NPF; r++) {
+      const int p = tid + BS * r;
+      if (p >= NF) continue;
+      const int f = p / (NC * NC), cell = p % (NC * NC), nb = f + 1, kind = T.kind(f);
+      if (kind == NB_LOCAL) continue;
+      const int a = cell % NC + 1, c = cell / NC + 1, d = f >> 1;
+      const bool low = nb & 1;
+      const double x1 = sb[sr_int<NC>(d, low ? 1 : NC, a, c)], x2 = sb[sr_int<NC>(d, low ? 2 : NC - 1, a, c)];
+      const int gi = TL::ogh(nb, a, c);
+      double gv = 0.0;   // (other kinds: unreachable, the host fuses none)
+      if (kind == NB_PHYS)
+        gv = phys_ghost(F, bc, b, (long long)b * 6 + f, nb, T.phys_code(f), a, c, gi, x1, x2);
+      else if constexpr (BCK == 2)
+        if (kind == NB_RB) gv = rb_ghost_from(rt[r], a, c, x1, x2);
+      sb[gi] = gv;
+      if (gi < 2 * HV + f * FS + FH) u[gi] = gv;   // the colour-0 half to HBM
+    }
   }
   __syncthreads();
   // our new colour-0 boundary cells to the neighbours' colour-0 ghost halves
@@ -525,7 +543,11 @@ constexpr int prolong_smooth_lds() {
   return 2 * Tl<NC>::HV + (prolong_cb<NC>() > 6 * Tl<NC>::FH ? prolong_cb<NC>() : 6 * Tl<NC>::FH);
 }
 
-template <int NC, int OP, int BS>
+// RB (round 4): the level has refinement-boundary faces (one GPU): their
+// colour-0 ghosts are formed like the physical ones, from the corrected
+// boundary cells and the coarse face (sides_rb; Cv is final by now), and the
+// substep's epilogue fills them (gsrb_box's RB form)
+template <int NC, int OP, int BS, bool RB = false>
 __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const LevelView& F, double lambda,
                                                    const int* parent_local, const int* dixp, const GcBC& bc,
                                                    int one_child, const uint8_t* push0, int b, double* lds) {
@@ -540,11 +562,12 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   const int dix[3] = {dp & 1023, (dp >> 10) & 1023, dp >> 20};
   // The substep overwrites colour 1 without reading it (gs_value has no
   // centre term), so colour 1's corrected values are dead, except where a
-  // physical face's colour-0 ghost takes its boundary cell x1 (bc_to_gc).
-  // Boxes without a physical face prolong colour 0 only.
+  // physical (refinement-boundary) face's colour-0 ghost takes its boundary
+  // cell x1 (bc_to_gc, sides_rb).  Boxes without such a face prolong colour 0
+  // only.
   bool phys = false;
 #pragma unroll
-  for (int nb = 0; nb < 6; nb++) phys |= T.kind(nb) == NB_PHYS;
+  for (int nb = 0; nb < 6; nb++) phys |= T.kind(nb) == NB_PHYS || (RB && T.kind(nb) == NB_RB);
   const int npair = phys ? HV : HV / 2;
   // all loads that do not depend on LDS first (colour 0; a physical-face box
   // reads its colour 1 when it corrects it)
@@ -704,7 +727,7 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     const int nb = q / FH + 1, rr = q % FH;
     const long long fidx = (long long)b * 6 + nb - 1;
     const int kind = T.kind(nb - 1);
-    if (kind == NB_PHYS) {
+    if (kind == NB_PHYS || (RB && kind == NB_RB)) {
       const bool low = nb & 1;
       const int d = (nb + 1) >> 1, gpos = low ? 0 : NC + 1;
       const int c = rr / HN + 1, ah = rr % HN;
@@ -715,36 +738,56 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
       else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
       else { i1 = a; j1 = c; k1 = x1; }
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
-      gv[g] = phys_ghost(F, bc, b, fidx, nb, T.phys_code(nb - 1), a, c, TL::ogh(nb, a, c), sb[TL::oint(i1, j1, k1)],
-                         sb[TL::oint(i2, j2, k2)]);
+      const double v1 = sb[TL::oint(i1, j1, k1)], v2 = sb[TL::oint(i2, j2, k2)];
+      if (kind == NB_PHYS)
+        gv[g] = phys_ghost(F, bc, b, fidx, nb, T.phys_code(nb - 1), a, c, TL::ogh(nb, a, c), v1, v2);
+      else
+        gv[g] = rb_ghost(F, RbSide{Cv, nullptr}, T.arg(nb - 1), nb, a, c, v1, v2);
     }
     sg[(nb - 1) * FH + rr] = gv[g];
   }
   __syncthreads();
   // ---- substep 1: colour 1 from colour 0, then its ghost fill (push colour 1)
+  const RbSide rbs{Cv, nullptr};
 #if OMG_PS_PRE
-  gsrb_box<NC, OP, BS, 2, true>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, &pre);
+  gsrb_box<NC, OP, BS, 2, true, RB>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, &pre, RB ? &rbs : nullptr);
 #else
-  gsrb_box<NC, OP, BS, 2, true>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds);
+  gsrb_box<NC, OP, BS, 2, true, RB>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, nullptr, RB ? &rbs : nullptr);
 #endif
 }
 
-template <int NC, int OP, int BS>
-// 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64
-__global__ void __launch_bounds__(BS, OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
+template <int NC, int OP, int BS, bool RB = false>
+// 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64;
+// the refinement-boundary form holds the coarse operands of its epilogue in
+// registers too (4 waves per SIMD)
+__global__ void __launch_bounds__(BS, RB ? 4 : OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
                                                        int one_child, const int* list, const uint8_t* push0) {
   __shared__ double lds[prolong_smooth_lds<NC>()];
   const int t = xcd_box(blockIdx.x, gridDim.x, F.rev);
-  prolong_smooth_box<NC, OP, BS>(Cv, F, lambda, parent_local, dixp, bc, one_child, push0, list ? list[t] : t, lds);
+  prolong_smooth_box<NC, OP, BS, RB>(Cv, F, lambda, parent_local, dixp, bc, one_child, push0, list ? list[t] : t,
+                                     lds);
 }
 
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
                            const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
-                           const uint8_t* push0, hipStream_t st) {
+                           const uint8_t* push0, hipStream_t st, bool rb) {
   const int n = list ? n_list : F.n;
   if (n == 0) return;
   const dim3 g(n);
+  if (rb) {
+    if (F.nc != 16 && F.nc != 8) throw std::runtime_error("launch_prolong_smooth: refinement boundaries need 16^3 / 8^3");
+#define OMG_PSR(NC, BS)                                                                                         \
+  if (op == OP_HELM)                                                                                            \
+    k_prolong_smooth<NC, OP_HELM, BS, true><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child, \
+                                                              list, push0);                                     \
+  else                                                                                                          \
+    k_prolong_smooth<NC, OP_LPL, BS, true><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
+                                                             list, push0);
+    if (F.nc == 16) OMG_PSR(16, OMG_PS_BS16) else OMG_PSR(8, 256)
+#undef OMG_PSR
+    return;
+  }
 #define OMG_PS(NC, BS)                                                                                \
   if (op == OP_HELM)                                                                                  \
     k_prolong_smooth<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child, \
@@ -2108,18 +2151,38 @@ template <int OP, bool LEX>
 __global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ dA, unsigned long long seq) {
   extern __shared__ double lds[];
   const MidArgs& A = *dA;
-  // the participants: the P workgroups the dispatcher dealt to XCD A.xcd.
-  // Workgroups go round-robin over the 8 XCDs from wherever the previous
-  // dispatch stopped, so those are blockIdx = x0 + 8w, w = 0..P-1; each
-  // registers its slot (a slot taken twice: not that placement, error 2; a
-  // slot missing: the first barrier times out, error 1)
-  if (xcc_id() != A.xcd) return;
-  const int w = blockIdx.x >> 3, P = A.P;
-  unsigned long long* reg = A.sync + 16 * (kMidMaxBoxes + 1) + (seq & 1);
+  const int P = A.P;
+  // The participants: the first P workgroups to arrive on one XCD, whichever
+  // fills first (the 8P workgroups are usually dealt round-robin, but kernels
+  // of other streams dispatched meanwhile shift that).  Each workgroup takes a
+  // ticket on its XCD's counter; the one completing a group of P names that
+  // XCD; ticket holders below P wait for the name and stay if it is theirs.
+  // The counters of this launch (parity seq & 1) were zeroed by the launch
+  // before it.
+  __shared__ int sh_w;
+  unsigned long long* place = A.sync + 16 * (kMidMaxBoxes + 1 + 2 * (seq & 1));
   if (threadIdx.x == 0) {
-    const unsigned long long bit = 1ull << w;
-    if (atomicOr(reg, bit) & bit) atomicOr(A.err, 2);
+    const int x = xcc_id();
+    const unsigned long long t = atomicAdd(place + x, 1ull);
+    int wv = -1;
+    if (t < (unsigned long long)P) {
+      if (t == (unsigned long long)P - 1) atomicCAS(place + 8, 0ull, (unsigned long long)(x + 1));
+      long long it = 0;
+      unsigned long long win;
+      while ((win = __hip_atomic_load(place + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+        if (++it > kMidSpin) {
+          atomicOr(A.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (win == (unsigned long long)(x + 1)) wv = (int)t;
+    }
+    sh_w = wv;
   }
+  __syncthreads();
+  const int w = sh_w;
+  if (w < 0) return;
   for (int s = 0; s < A.n_steps; s++) {
     const MidStep S = A.st[s];
     const MidLevel& M = A.lv[S.li];
@@ -2132,10 +2195,11 @@ __global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ d
       __syncthreads();
     }
     if (!mid_barrier(A, w, (seq << 8) | (unsigned long long)(s + 1))) return;
-    // every participant has registered: clear this launch's word for the
-    // launch after next (stream order keeps the launches apart)
-    if (s == 0 && w == 0 && threadIdx.x == 0) atomicExch(reg, 0ull);
   }
+  // the next launch's placement counters (nothing of this launch reads them;
+  // the next launch starts after this one has ended)
+  unsigned long long* next = A.sync + 16 * (kMidMaxBoxes + 1 + 2 * ((seq + 1) & 1));
+  if (w == 0 && threadIdx.x < 9) __hip_atomic_store(next + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static_assert(sizeof(MidArgs) + 16 <= 4096, "MidArgs must fit the 4 KiB kernel-argument limit");
@@ -2169,9 +2233,5 @@ void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long se
 #undef OMG_MID
 }
 
-__global__ void k_xcc_probe(int* out) {
-  if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
-}
-void launch_xcc_probe(int* out, int n, hipStream_t st) { k_xcc_probe<<<n, 64, 0, st>>>(out); }
 
 }  // namespace omg
