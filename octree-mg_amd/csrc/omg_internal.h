@@ -310,9 +310,11 @@ struct omg_ctx {
   unsigned long long mid_seq = 0;                // launches so far (the barrier words carry it)
   bool no_mid = false;                           // OMG_NO_MID: the mid levels launch by launch
   // levels of at most this many boxes run in the mid kernel (OMG_MID_MAX_BOXES,
-  // 1..kMidMaxBoxes, A/B runs); its barrier costs 1.4-1.8 us at 8-64
-  // workgroups on the XCD (tools/xcd_probe.hip v4)
-  int mid_max_boxes = 64;
+  // 1..kMidMaxBoxes, A/B runs).  Its barrier costs 1.0-1.8 us at 8-64
+  // workgroups (tools/xcd_probe.hip v4), but one XCD's share of the memory
+  // bandwidth makes a step of a 64-box level slower than a whole-chip launch
+  // (C4 0.43 -> 0.60 ms per cycle with 64, profiles/r04)
+  int mid_max_boxes = 8;
   bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
   long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch

@@ -132,8 +132,10 @@ class MG(MGTree):
         for iv in ivs:
             for nb in range(1, 7):
                 cb = self.bc[nb][iv].refinement_bnd
+                had = self._rb_keep.get((iv, nb)) is not None
                 fp = self._rb_keep[(iv, nb)] = self._rb_trampoline(iv, nb, cb) if cb else None
-                c.call("set_refinement_bnd", iv, nb, C.cast(fp, C.c_void_p) if fp else None, None)
+                if fp or had:   # (nothing to clear otherwise: older libraries lack the entry)
+                    c.call("set_refinement_bnd", iv, nb, C.cast(fp, C.c_void_p) if fp else None, None)
             cbs = [self.bc[nb][iv].boundary_cond for nb in range(1, 7)]
             for nb in range(1, 7):
                 b = self.bc[nb][iv]
