@@ -740,15 +740,18 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
                           bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_bnd, L->n_bnd);
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
-      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm, lvl);
-      launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream_comm);
-      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
+      // the interior boxes are queued before the exchange is issued: the
+      // exchange may wait on the host (the loopback transport waits for its
+      // peer's message), and the interior substep needs nothing from it
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_int * L->nc * L->nc * L->nc, lvl);
         launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
                           bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int);
       }
+      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
+      exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm, lvl);
+      launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream_comm);
+      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
       finish_rb(c, L, 1);
       if (!L->phi_gc_ok) fill_gc_lvl(c, lvl, 1);
@@ -910,16 +913,16 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
                           bc_for(c, lvl, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd);
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
-      exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm, lvl);
-      launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm, 1);
-      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
-      {
+      {   // (queued before the exchange is issued, as in smooth_boxes)
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
         if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
                                  F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb, F->has_phys))
           throw OmgError("smooth_resid: not available for this level");
       }
+      HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
+      exchange(c, F->halo, F->d_sendbuf, F->d_recvbuf, c->stream_comm, lvl);
+      launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm, 1);
+      HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
       {
         Prof p(c, "resid_restrict", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl);
@@ -2640,7 +2643,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
-    c->no_mid = env_flag("OMG_NO_MID");
+    c->no_mid = !env_flag("OMG_MID");   // opt-in: measured slower
     if (const char* v = getenv("OMG_MID_MAX_BOXES")) c->mid_max_boxes = std::min(std::max(std::atoi(v), 1), kMidMaxBoxes);
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

@@ -308,7 +308,7 @@ struct omg_ctx {
   unsigned long long* d_mid_sync = nullptr;      // barrier words
   int* d_mid_err = nullptr;                      // sticky failure flag of k_mid
   unsigned long long mid_seq = 0;                // launches so far (the barrier words carry it)
-  bool no_mid = false;                           // OMG_NO_MID: the mid levels launch by launch
+  bool no_mid = true;                            // unless OMG_MID: the mid levels launch by launch
   // levels of at most this many boxes run in the mid kernel (OMG_MID_MAX_BOXES,
   // 1..kMidMaxBoxes, A/B runs).  Its barrier costs 1.0-1.8 us at 8-64
   // workgroups (tools/xcd_probe.hip v4), but one XCD's share of the memory

@@ -279,6 +279,7 @@ def _mid_launches(dev):
 @pytest.mark.parametrize("cap", ["8", "64"])
 @pytest.mark.parametrize("args", MID_CASES)
 def test_mid_levels_match_oracle(args, cap, monkeypatch):
+    monkeypatch.setenv("OMG_MID", "1")   # opt-in: slower than launch by launch
     monkeypatch.setenv("OMG_MID_MAX_BOXES", cap)
     cfg = parse(args)
     dev, orc = DeviceBackend(cfg), OracleBackend(cfg)

@@ -18,7 +18,7 @@ def main():
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].split("<")[0]
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("omg::", "")
             key = (k, int(r["Grid_Size"]) // int(r["Workgroup_Size"]), int(r["Workgroup_Size"]))
             per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     rows = []
@@ -30,7 +30,7 @@ def main():
         tot += g * n
         rows.append((key, n, a))
     rows.sort(key=lambda x: -x[2].get("GRBM_GUI_ACTIVE", 0.0) * x[1])
-    print(f"{'kernel':32s} {'WGs':>6s} {'thr':>4s} {'calls':>5s} {'waves':>7s} {'GUI_ACT/XCD':>11s} "
+    print(f"{'kernel':44s} {'WGs':>6s} {'thr':>4s} {'calls':>5s} {'waves':>7s} {'GUI_ACT/XCD':>11s} "
           f"{'SQ_BUSY':>9s} {'mean waves/XCD':>14s} {'wait %':>6s} {'HBM KB':>8s} {'% busy':>6s}")
     for (k, wg, th), n, a in rows:
         g = a.get("GRBM_GUI_ACTIVE", 0.0)
@@ -38,7 +38,7 @@ def main():
         occ = 4 * wc / g if g else 0.0   # g sums 8 XCDs, so this is per XCD
         wait = 100 * a.get("SQ_WAIT_ANY", 0.0) / wc if wc else 0.0
         hbm = (2 * a.get("FETCH_SIZE", 0.0) + a.get("WRITE_SIZE", 0.0))
-        print(f"{k[:32]:32s} {wg:6d} {th:4d} {n:5d} {a.get('SQ_WAVES', 0):7.0f} {g / 8:11.0f} "
+        print(f"{k[:44]:44s} {wg:6d} {th:4d} {n:5d} {a.get('SQ_WAVES', 0):7.0f} {g / 8:11.0f} "
               f"{a.get('SQ_BUSY_CYCLES', 0):9.0f} {occ:14.1f} {wait:6.1f} {hbm:8.0f} {100 * g * n / tot:6.1f}")
 
 
