@@ -950,8 +950,22 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     restrict_lvl(c, 1, lvl);
     restrict_lvl(c, 4, lvl);
   }
-  fill_gc_lvl(c, lvl - 1, 1);
   Level* C = level_ptr(c, lvl - 1);
+  // the fill of lvl-1 and its parents' coarse rhs in one pass when its faces
+  // are same-GPU or physical (k_fill_crhs: a parent box reads its
+  // neighbours' boundary cells itself instead of waiting for their pushes)
+  if (C && C->n && !C->parents.empty() && !C->has_rb && !C->has_remote && !c->no_fill_tile && !c->no_fill_crhs &&
+      (C->nc == 16 || C->nc == 8 || C->nc == 4)) {
+    C->phi_gc_ok = true;
+    rb_stale_above(c, lvl - 1);
+    {
+      Prof p(c, "fill_crhs", (double)C->n * C->nc * C->nc * C->nc, lvl - 1);
+      launch_fill_crhs(C->sweep_view(), c->op, c->lambda, bc_for(c, lvl - 1, 1), C->d_parmask, c->stream);
+    }
+    finish_halo(c, C, 1);
+    return;
+  }
+  fill_gc_lvl(c, lvl - 1, 1);
   if (C && !C->parents.empty()) {
     Prof p(c, "coarse_rhs", (double)C->parents.size() * C->nc * C->nc * C->nc, lvl - 1);
     if (!launch_coarse_rhs_tile(C->sweep_view(), c->op, c->lambda, C->d_parents, (int)C->parents.size(), c->stream))
@@ -2235,7 +2249,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_data); L.d_phi = nullptr; dfree(L.d_nbk); dfree(L.d_nba); dfree(L.d_sendpos); dfree(L.d_rb);
     dfree(L.d_topo);
     rbh_free(L);
-    dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix);
+    dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix); dfree(L.d_parmask);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
@@ -2465,6 +2479,11 @@ void build_plan(omg_ctx* c) {
       if (owns(id)) L.leaves.push_back(c->local_index[id]);
     L.d_parents = to_device(L.parents);
     L.d_leaves = to_device(L.leaves);
+    {
+      std::vector<uint8_t> pm(L.n, 0);
+      for (int b : L.parents) pm[b] = 1;
+      L.d_parmask = to_device(pm);
+    }
     dmalloc(&L.d_scratch, sizeof(double) * L.leaves.size());
     dmalloc(&L.d_scratch_rhs, sizeof(double) * L.leaves.size());
     L.all_parents = L.n > 0 && (int)L.parents.size() == L.n;
@@ -2635,6 +2654,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_skip1 = env_flag("OMG_NO_SKIP1");
     c->tail_timing = env_flag("OMG_TAIL_TIMING");
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
+    c->no_fill_crhs = env_flag("OMG_NO_FILL_CRHS");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");

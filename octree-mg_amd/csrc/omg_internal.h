@@ -143,6 +143,7 @@ struct Level {
   std::vector<int> parents, leaves;
   int* d_parents = nullptr;
   int* d_leaves = nullptr;
+  uint8_t* d_parmask = nullptr;     // per box: 1 = a parent (k_fill_crhs)
   // restriction onto this level from lvl+1 happens per fine box: for each of my
   // boxes at this level, the parent (local idx at lvl-1, or -1 if remote) and
   // its child offset inside the parent.
@@ -287,6 +288,7 @@ struct omg_ctx {
   bool no_skip1 = false;               // OMG_NO_SKIP1: correct colour 1 before the up-smoothing too
   bool no_fuse_down = false;           // OMG_NO_FUSE_DOWN: last down-substep and residual + restriction apart
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
+  bool no_fill_crhs = false;           // OMG_NO_FILL_CRHS: update_coarse's fill and coarse rhs as two passes
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
   bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring

@@ -223,6 +223,10 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
                            const uint8_t* push0, hipStream_t st, bool rb = false);
 // update_coarse's parent loop, LDS-tiled; false when the box size / operator
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
+// update_coarse's fill of the coarse level + its parents' coarse rhs in one
+// pass (levels whose faces are same-GPU or physical, 16^3 / 8^3 / 4^3 boxes)
+void launch_fill_crhs(const LevelView& C, int op, double lambda, const GcBC& bc, const uint8_t* parmask,
+                      hipStream_t st);
 bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int* parents, int n_par,
                             hipStream_t st);
 void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st);

@@ -1182,6 +1182,113 @@ __device__ __forceinline__ void coarse_rhs_box(const LevelView& Cv, double lambd
   }
 }
 
+// update_coarse's fill of the coarse level (mg_fill_ghost_cells_lvl,
+// m_ghost_cells.f90:131-175) and its parents' rhs = L(phi) + res, old = phi
+// (m_multigrid.f90:364-383) in one pass, for a level whose faces are same-GPU
+// or physical.  Every box pushes its boundary cells and forms its physical
+// ghosts as k_fill_tile does; a parent box also needs its own ghost faces
+// for the operator, and rather than wait for its neighbours' pushes it reads
+// their boundary cells itself (the same values the pushes carry: phi of this
+// level is final once the restriction above has run) and forms its physical
+// ghosts in LDS from its own cells (bc_to_gc, as the push side does).  Then
+// the tile holds exactly what k_coarse_rhs_tile would load after the fill.
+template <int NC, int OP, int BS>
+__global__ void __launch_bounds__(BS) k_fill_crhs(LevelView C, double lambda, GcBC bc,
+                                                  const uint8_t* __restrict__ parmask) {
+  using TL = Tl<NC>;
+  constexpr int HV = TL::HV, NST = TL::NST, FH = TL::FH, NR = (HV + BS - 1) / BS, H = NC / 2;
+  __shared__ double sb[NST];
+  const int tid = threadIdx.x, b = xcd_box(blockIdx.x, gridDim.x, C.rev);
+  const FaceTopo T = load_topo(C, b);
+  const long long boff = (long long)b * C.stride;
+  const double* __restrict__ u = C.phi + boff;
+  const bool par = parmask[b] != 0;
+  for (int q = tid; q < HV; q += BS) reinterpret_cast<v2d*>(sb)[q] = reinterpret_cast<const v2d*>(u)[q];
+  v2d rr[NR];
+  if (par) {
+    // the neighbours' boundary cells into our ghost faces (both colours)
+    for (int p = tid; p < 6 * NC * NC; p += BS) {
+      const int f = p / (NC * NC), cell = p % (NC * NC);
+      if (T.kind(f) != NB_LOCAL) continue;
+      const int nb = f + 1, a = cell % NC + 1, c = cell / NC + 1, d = f >> 1;
+      const bool low = nb & 1;
+      sb[TL::ogh(nb, a, c)] = C.phi[(long long)T.arg(f) * C.stride + sr_int<NC>(d, low ? NC : 1, a, c)];
+    }
+    const double* __restrict__ res = C.data + 3 * C.vstride + boff;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int q2 = tid + BS * r;
+      if (q2 < HV) rr[r] = ld_nt(res + 2 * q2);
+    }
+  }
+  __syncthreads();
+  tile_face_fill<NC>(C, b, T, sb, 3, bc, nullptr);
+  if (!par) return;
+  if (T.nonlocal()) {   // physical ghosts in the tile too
+    for (int p = tid; p < 6 * NC * NC; p += BS) {
+      const int f = p / (NC * NC), cell = p % (NC * NC);
+      if (T.kind(f) != NB_PHYS) continue;
+      const int nb = f + 1, a = cell % NC + 1, c = cell / NC + 1, d = f >> 1;
+      const bool low = nb & 1;
+      const int gi = TL::ogh(nb, a, c);
+      sb[gi] = phys_ghost(C, bc, b, (long long)b * 6 + f, nb, T.phys_code(f), a, c, gi,
+                          sb[sr_int<NC>(d, low ? 1 : NC, a, c)], sb[sr_int<NC>(d, low ? 2 : NC - 1, a, c)]);
+    }
+  }
+  __syncthreads();
+  // old = phi over the stored box, then rhs = L(phi) + res (coarse_rhs_box)
+  double* __restrict__ old = C.data + 2 * C.vstride + boff;
+  double* __restrict__ rhs = C.data + C.vstride + boff;
+  for (int q = tid; q < NST / 2; q += BS) {
+    const v2d x = reinterpret_cast<const v2d*>(sb)[q];
+    st_nt(old + 2 * q, x.x, x.y);
+  }
+  const OpCoef<OP> K(C, lambda);
+  constexpr int FS = TL::FS;
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q2 = tid + BS * r;
+    if (q2 >= HV) continue;
+    const int e = q2 >= HV / 2, o = 1 - e;
+    Nbr7 s0, s1;
+    if constexpr (H % 2 == 0) {
+      pair_stencil<NC>(sb + o * HV, sb + 2 * HV + o * FH, FS, e, 2 * q2 - e * HV, s0, s1);
+    } else {
+      int i, j, k;
+      TL::decode(2 * q2, i, j, k);
+      s0.xm = sb[TL::ocell(i - 1, j, k)]; s0.xp = sb[TL::ocell(i + 1, j, k)];
+      s0.ym = sb[TL::ocell(i, j - 1, k)]; s0.yp = sb[TL::ocell(i, j + 1, k)];
+      s0.zm = sb[TL::ocell(i, j, k - 1)]; s0.zp = sb[TL::ocell(i, j, k + 1)];
+      TL::decode(2 * q2 + 1, i, j, k);
+      s1.xm = sb[TL::ocell(i - 1, j, k)]; s1.xp = sb[TL::ocell(i + 1, j, k)];
+      s1.ym = sb[TL::ocell(i, j - 1, k)]; s1.yp = sb[TL::ocell(i, j + 1, k)];
+      s1.zm = sb[TL::ocell(i, j, k - 1)]; s1.zp = sb[TL::ocell(i, j, k + 1)];
+    }
+    const double2 cc = reinterpret_cast<const double2*>(sb)[q2];
+    s0.c = cc.x;
+    s1.c = cc.y;
+    double l0, l1;
+    op_pair<NC, OP>(K, C, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
+    st_nt(rhs + 2 * q2, l0 + rr[r].x, l1 + rr[r].y);
+  }
+}
+
+void launch_fill_crhs(const LevelView& C, int op, double lambda, const GcBC& bc, const uint8_t* parmask,
+                      hipStream_t st) {
+  if (C.n == 0) return;
+  const dim3 g(C.n);
+#define OMG_FC_OP(NC, BS, OPV) k_fill_crhs<NC, OPV, BS><<<g, BS, 0, st>>>(C, lambda, bc, parmask);
+#define OMG_FC(NC, BS) OMG_FOR_OP(op, OMG_FC_OP, NC, BS)
+  switch (C.nc) {
+    case 16: OMG_FC(16, 512) break;
+    case 8: OMG_FC(8, 256) break;
+    case 4: OMG_FC(4, 64) break;
+    default: throw std::runtime_error("launch_fill_crhs: box sizes 16, 8, 4");
+  }
+#undef OMG_FC
+#undef OMG_FC_OP
+}
+
 template <int NC, int OP, int BS>
 __global__ void __launch_bounds__(BS) k_coarse_rhs_tile(LevelView Cv, double lambda, const int* parents) {
   __shared__ double sb[Tl<NC>::NST];
