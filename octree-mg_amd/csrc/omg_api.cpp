@@ -484,8 +484,10 @@ GcBC bc_for(omg_ctx* c, int lvl, int iv) {
 // lvl (its interior and tangential ghosts, box_gc_for_fine_neighbor,
 // m_ghost_cells.f90:500-577): every write of phi on lvl makes them stale.
 void rb_stale_above(omg_ctx* c, int lvl) {
-  if (Level* U = level_ptr(c, lvl + 1))
+  if (Level* U = level_ptr(c, lvl + 1)) {
     if (U->any_rb) U->phi_gc_ok = false;
+    U->rbgv_ok = false;   // (its refinement-boundary coarse parts read lvl)
+  }
 }
 // phi was written on a level: its ghost faces may no longer match a fill
 void phi_dirty(omg_ctx* c, int lvl) {
@@ -493,7 +495,7 @@ void phi_dirty(omg_ctx* c, int lvl) {
   rb_stale_above(c, lvl);
 }
 void phi_dirty_all(omg_ctx* c) {
-  for (auto& kv : c->levels) kv.second.phi_gc_ok = false;
+  for (auto& kv : c->levels) kv.second.phi_gc_ok = kv.second.rbgv_ok = false;
 }
 
 // Refinement-boundary faces whose ghosts a host callback sets instead of
@@ -760,8 +762,12 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     }
     if (L->n) {
       Prof p(c, "smoother_gsrb", 0.5 * L->n * L->nc * L->nc * L->nc, lvl);
+      // refinement-boundary coarse parts: the first substep after the level
+      // below changed computes and stores them, the others read them
+      const int gvm = L->d_rbgv ? (L->rbgv_ok ? 2 : 1) : 0;
+      if (gvm) L->rbgv_ok = true;
       launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, odd ? 0 : 1 << e, view_of(c, lvl - 1), L->d_rb,
-                        L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream);
+                        L->has_rb, bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, nullptr, 0, L->d_rbgv, gvm);
     }
     const bool full_fill = odd || !L->phi_gc_ok;
     finish_halo(c, L, 1, !full_fill);
@@ -2250,6 +2256,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_topo);
     rbh_free(L);
     dfree(L.d_parents); dfree(L.d_leaves); dfree(L.d_parent_local); dfree(L.d_dix); dfree(L.d_parmask);
+    dfree(L.d_rbgv);
     dfree(L.d_pairs); dfree(L.d_sendbuf); dfree(L.d_recvbuf); dfree(L.d_scratch); dfree(L.d_scratch_rhs);
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
@@ -2426,6 +2433,10 @@ void build_plan(omg_ctx* c) {
     L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
+    // (one GPU, tiled box sizes: the red-black smoother's coarse-part buffer)
+    if (!L.h_rb.empty() && c->n_ranks == 1 && !c->host_only && (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2))
+      dmalloc(&L.d_rbgv, sizeof(double) * L.n * 6 * L.nc * L.nc);
+    L.rbgv_ok = false;
     {
       std::vector<int> pb;
       for (int b = 0; b < L.n; b++)

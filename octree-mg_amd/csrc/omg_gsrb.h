@@ -43,9 +43,15 @@ __device__ __forceinline__ void gsrb_load_rhs(const LevelView& L, int e, int b, 
 
 // The coarse side of refinement-boundary faces (fine side of sides_rb):
 // the level below and the per-face records; rb == nullptr: none on this level.
+// gv / gv_mode: the coarse part of every refinement-boundary ghost of the
+// level ([box][face][cell], rb_gv below), which stays fixed while the coarse
+// level does: 1 = the smoother computes it and stores it there, 2 = it reads
+// it instead of the five coarse operands (0: neither)
 struct RbSide {
   LevelView C;
   const RBRec* rb;
+  double* gv;
+  int gv_mode;
 };
 
 // Refinement-boundary ghost (box_gc_for_fine_neighbor + sides_rb,
@@ -67,12 +73,19 @@ __device__ __forceinline__ RbCoarse rb_coarse_load(const LevelView& L, const RbS
   auto T = [&](int p, int q) { return cu[off_face_cell(R.C, nb, clayer, rec.dix[t1] + p, rec.dix[t2] + q)]; };
   return RbCoarse{T(i, j), T(i - 1, j), T(i + 1, j), T(i, j - 1), T(i, j + 1)};
 }
-__device__ __forceinline__ double rb_ghost_from(const RbCoarse& t, int a, int c, double v1, double v2) {
+// the coarse part of the ghost (the interpolated coarse value), then the
+// ghost from it and the fine box's two boundary cells
+__device__ __forceinline__ double rb_gv(const RbCoarse& t, int a, int c) {
   const double g1 = 0.125 * (t.p1 - t.m1);
   const double g2 = 0.125 * (t.p2 - t.m2);
   double gv = ((a - 1) & 1) ? t.tc + g1 : t.tc - g1;
-  gv = ((c - 1) & 1) ? gv + g2 : gv - g2;
+  return ((c - 1) & 1) ? gv + g2 : gv - g2;
+}
+__device__ __forceinline__ double rb_ghost_gv(double gv, double v1, double v2) {
   return 0.5 * gv + 0.75 * v1 - 0.25 * v2;
+}
+__device__ __forceinline__ double rb_ghost_from(const RbCoarse& t, int a, int c, double v1, double v2) {
+  return rb_ghost_gv(rb_gv(t, a, c), v1, v2);
 }
 // the RBRec of an NB_RB face from its FaceTopo argument (coarse index in bits
 // 0-24, child offset halves in bits 25-27; pack_topo)
@@ -234,7 +247,10 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       if (p >= NF) continue;
       const int f = p / (NC * NC), cell = p % (NC * NC);
       if (T.kind(f) != NB_RB) continue;
-      rt[r] = rb_coarse_load(L, *rbs, rb_unpack(L, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
+      if (rbs->gv_mode == 2)   // the stored coarse part (in tc)
+        rt[r].tc = rbs->gv[((long long)b * 6 + f) * (NC * NC) + cell];
+      else
+        rt[r] = rb_coarse_load(L, *rbs, rb_unpack(L, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
     }
   }
   __syncthreads();
@@ -345,7 +361,13 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     } else if (RB && kind == NB_RB) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const double v2 = cellv(i2, j2, k2);
-      u[off_gh(L, nb, a, c)] = RBP ? rb_ghost_from(*rc, a, c, v1, v2) : rb_ghost(L, *rbs, arg, nb, a, c, v1, v2);
+      if constexpr (RBP) {
+        const double gv = rbs->gv_mode == 2 ? rc->tc : rb_gv(*rc, a, c);
+        if (rbs->gv_mode == 1) rbs->gv[fidx * (NC * NC) + cell] = gv;
+        u[off_gh(L, nb, a, c)] = rb_ghost_gv(gv, v1, v2);
+      } else {
+        u[off_gh(L, nb, a, c)] = rb_ghost(L, *rbs, arg, nb, a, c, v1, v2);
+      }
     }   // NB_RBREM: the caller's refinement-boundary exchange (finish_rb)
   };
   if constexpr (RBP) {

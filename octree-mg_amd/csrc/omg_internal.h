@@ -144,6 +144,10 @@ struct Level {
   int* d_parents = nullptr;
   int* d_leaves = nullptr;
   uint8_t* d_parmask = nullptr;     // per box: 1 = a parent (k_fill_crhs)
+  // refinement-boundary levels (one GPU): the coarse part of every rb ghost,
+  // [box][face][nc*nc] (RbSide::gv), valid while the level below is unchanged
+  double* d_rbgv = nullptr;
+  bool rbgv_ok = false;
   // restriction onto this level from lvl+1 happens per fine box: for each of my
   // boxes at this level, the parent (local idx at lvl-1, or -1 if remote) and
   // its child offset inside the parent.

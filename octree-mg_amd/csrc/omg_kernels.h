@@ -20,9 +20,12 @@ struct GcBC {
 // shift (device scalar or null): subtract it from every value the substep
 // loads (a pending subtract_mean of phi, bit-identical to applying it first)
 // boxes/n_boxes: only these boxes (local indices), else the whole level
+// rbgv / rbgv_mode: the level's buffer of refinement-boundary coarse parts
+// (RbSide::gv: 1 = compute and store, 2 = read; tiled kernel only)
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
-                       hipStream_t st, const int* boxes = nullptr, int n_boxes = 0);
+                       hipStream_t st, const int* boxes = nullptr, int n_boxes = 0, double* rbgv = nullptr,
+                       int rbgv_mode = 0);
 // whether launch_gs_substep takes the LDS-tiled kernel (which alone takes a shift)
 // M(NC, BS, OPV) for the operator op (OPV a compile-time Op)
 #define OMG_FOR_OP(op, M, NC, BS)         \

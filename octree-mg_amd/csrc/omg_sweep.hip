@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(BS) k_gsrb_tile(LevelView L, double lambda, in
 
 void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                        const RBRec* rb, bool has_rb, const GcBC& bc, double* sendbuf, const double* shift,
-                       hipStream_t st, const int* boxes, int n_boxes) {
+                       hipStream_t st, const int* boxes, int n_boxes, double* rbgv, int rbgv_mode) {
   if (L.n == 0) return;
   if (boxes && !gs_tiled(L.nc, op, has_rb)) return;   // subsets only exist for the tiled kernel
   if (!gs_tiled(L.nc, op, has_rb)) {
@@ -59,7 +59,7 @@ void launch_gs_substep(const LevelView& L, int op, double lambda, int e, int col
   const bool cached = (op == OP_LPL || op == OP_HELM) && 2ll * 8 * L.stride * L.n <= nt_bytes;
   const dim3 g(boxes ? n_boxes : L.n);
   if (g.x == 0) return;
-  const RbSide rbs{C, has_rb ? rb : nullptr};
+  const RbSide rbs{C, has_rb ? rb : nullptr, rbgv, rbgv ? rbgv_mode : 0};
 #ifndef OMG_GS_NT
 #define OMG_GS_NT 2
 #endif
