@@ -938,7 +938,8 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                               F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb, F->has_phys))
+                               F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb, F->has_phys,
+                               F->rbgv_ok ? F->d_rbgv : nullptr))
         throw OmgError("smooth_resid: not available for this level");
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
@@ -1013,7 +1014,8 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
     Prof p(c, "prolong_smooth", (double)n * F->nc * F->nc * F->nc, lvl + 1);
     launch_prolong_smooth(C->view(), F->sweep_view(), c->op, c->lambda, F->d_parent_local, F->d_dix,
                           bc_for(c, lvl + 1, 1), C->nc * 2 == F->nc, split ? F->d_int : nullptr, n,
-                          split ? F->d_push0 : nullptr, c->stream, F->has_rb);
+                          split ? F->d_push0 : nullptr, c->stream, F->has_rb, F->has_rb ? F->d_rbgv : nullptr);
+    if (F->has_rb && F->d_rbgv) F->rbgv_ok = true;   // (its substep stored the coarse parts)
   }
   if (split) {
     // multi-GPU: boxes with a face on another GPU take the unfused pair,

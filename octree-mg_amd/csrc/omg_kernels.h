@@ -200,7 +200,7 @@ void launch_fill_tile_xl(const LevelView& L, const GcBC& bc, double* sendbuf, co
 // pass (k_smooth_resid); false: not available for this op / box size
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
                          const int* parent_local, const int* dixp, hipStream_t st, const int* list,
-                         int n_list, const GcBC& bc, bool has_rb, bool has_phys);
+                         int n_list, const GcBC& bc, bool has_rb, bool has_phys, const double* rbgv = nullptr);
 void launch_resid_restrict(const LevelView& F, const LevelView& C, int op, double lambda,
                            unsigned long long* maxbits, int restrict_on, const int* parent_local,
                            const int* dixp, hipStream_t st, const int* list = nullptr, int n_list = 0);
@@ -223,7 +223,7 @@ void launch_copy_ghosts(const LevelView& L, hipStream_t st);
 // level has refinement-boundary faces (one GPU, 16^3 / 8^3 boxes)
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
                            const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
-                           const uint8_t* push0, hipStream_t st, bool rb = false);
+                           const uint8_t* push0, hipStream_t st, bool rb = false, double* rbgv = nullptr);
 // update_coarse's parent loop, LDS-tiled; false when the box size / operator
 // has no tiled kernel (caller falls back to launch_coarse_rhs)
 // update_coarse's fill of the coarse level + its parents' coarse rhs in one

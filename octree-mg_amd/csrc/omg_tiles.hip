@@ -233,7 +233,7 @@ __device__ __forceinline__ v2d sr_ld(const double* p) {
 template <int NC, int OP, int BS, int BCK = 0>
 __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, double lambda, int restrict_on,
                                                      const int* parent_local, const int* dixp,
-                                                     const int* list, GcBC bc) {
+                                                     const int* list, GcBC bc, const double* __restrict__ rbgv) {
   using TL = Tl<NC>;
   constexpr int H = NC / 2, HV = TL::HV, FH = TL::FH, FS = TL::FS, NR = (HV + BS - 1) / BS;
   constexpr int NG = (6 * FH + BS - 1) / BS;   // colour-0 ghost cells per thread
@@ -300,7 +300,10 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
         if (p >= NF) continue;
         const int f = p / (NC * NC), cell = p % (NC * NC);
         if (T.kind(f) != NB_RB) continue;
-        rt[r] = rb_coarse_load(F, RbSide{Cv, nullptr}, rb_unpack(F, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
+        if (rbgv)   // the coarse parts the level's substeps stored (RbSide::gv)
+          rt[r].tc = rbgv[((long long)b * 6 + f) * (NC * NC) + cell];
+        else
+          rt[r] = rb_coarse_load(F, RbSide{Cv, nullptr}, rb_unpack(F, T.arg(f)), f + 1, cell % NC + 1, cell / NC + 1);
       }
     }
   }
@@ -368,7 +371,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
       if (kind == NB_PHYS)
         gv = phys_ghost(F, bc, b, (long long)b * 6 + f, nb, T.phys_code(f), a, c, gi, x1, x2);
       else if constexpr (BCK == 2)
-        if (kind == NB_RB) gv = rb_ghost_from(rt[r], a, c, x1, x2);
+        if (kind == NB_RB) gv = rb_ghost_gv(rbgv ? rt[r].tc : rb_gv(rt[r], a, c), x1, x2);
       sb[gi] = gv;
       if (gi < 2 * HV + f * FS + FH) u[gi] = gv;   // the colour-0 half to HBM
     }
@@ -550,7 +553,8 @@ constexpr int prolong_smooth_lds() {
 template <int NC, int OP, int BS, bool RB = false>
 __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const LevelView& F, double lambda,
                                                    const int* parent_local, const int* dixp, const GcBC& bc,
-                                                   int one_child, const uint8_t* push0, int b, double* lds) {
+                                                   int one_child, const uint8_t* push0, int b, double* lds,
+                                                   double* rbgv = nullptr) {
   using TL = Tl<NC>;
   constexpr int HV = TL::HV, FH = TL::FH, NR = (HV + BS - 1) / BS, HN = NC / 2, CB = HN + 2;
   double* sb = lds;                     // both colours of the corrected interior (so | se of gsrb_box)
@@ -748,7 +752,9 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   }
   __syncthreads();
   // ---- substep 1: colour 1 from colour 0, then its ghost fill (push colour 1)
-  const RbSide rbs{Cv, nullptr};
+  // (the substep's epilogue stores the level's refinement-boundary coarse
+  // parts for the substeps after it, RbSide::gv)
+  const RbSide rbs{Cv, nullptr, rbgv, rbgv ? 1 : 0};
 #if OMG_PS_PRE
   gsrb_box<NC, OP, BS, 2, true, RB>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, &pre, RB ? &rbs : nullptr);
 #else
@@ -762,16 +768,17 @@ template <int NC, int OP, int BS, bool RB = false>
 // registers too (4 waves per SIMD)
 __global__ void __launch_bounds__(BS, RB ? 4 : OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
-                                                       int one_child, const int* list, const uint8_t* push0) {
+                                                       int one_child, const int* list, const uint8_t* push0,
+                                                       double* rbgv) {
   __shared__ double lds[prolong_smooth_lds<NC>()];
   const int t = xcd_box(blockIdx.x, gridDim.x, F.rev);
   prolong_smooth_box<NC, OP, BS, RB>(Cv, F, lambda, parent_local, dixp, bc, one_child, push0, list ? list[t] : t,
-                                     lds);
+                                     lds, rbgv);
 }
 
 void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, double lambda, const int* parent_local,
                            const int* dixp, const GcBC& bc, int one_child, const int* list, int n_list,
-                           const uint8_t* push0, hipStream_t st, bool rb) {
+                           const uint8_t* push0, hipStream_t st, bool rb, double* rbgv) {
   const int n = list ? n_list : F.n;
   if (n == 0) return;
   const dim3 g(n);
@@ -780,10 +787,10 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
 #define OMG_PSR(NC, BS)                                                                                         \
   if (op == OP_HELM)                                                                                            \
     k_prolong_smooth<NC, OP_HELM, BS, true><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child, \
-                                                              list, push0);                                     \
+                                                              list, push0, rbgv);                               \
   else                                                                                                          \
     k_prolong_smooth<NC, OP_LPL, BS, true><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
-                                                             list, push0);
+                                                             list, push0, rbgv);
     if (F.nc == 16) OMG_PSR(16, OMG_PS_BS16) else OMG_PSR(8, 256)
 #undef OMG_PSR
     return;
@@ -791,10 +798,10 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
 #define OMG_PS(NC, BS)                                                                                \
   if (op == OP_HELM)                                                                                  \
     k_prolong_smooth<NC, OP_HELM, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child, \
-                                                        list, push0);                                 \
+                                                        list, push0, nullptr);                        \
   else                                                                                                \
     k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
-                                                       list, push0);
+                                                       list, push0, nullptr);
   switch (F.nc) {
     case 16: OMG_PS(16, OMG_PS_BS16) break;
     case 8: OMG_PS(8, 256) break;
@@ -1043,16 +1050,19 @@ bool launch_fill_tile(const LevelView& L, const GcBC& bc, double* sendbuf, hipSt
 
 bool launch_smooth_resid(const LevelView& F, const LevelView& C, int op, double lambda, int restrict_on,
                          const int* parent_local, const int* dixp, hipStream_t st, const int* list,
-                         int n_list, const GcBC& bc, bool has_rb, bool has_phys) {
+                         int n_list, const GcBC& bc, bool has_rb, bool has_phys, const double* rbgv) {
   if (op != OP_LPL && op != OP_HELM) return false;
+  if (!has_rb) rbgv = nullptr;
   const int n = list ? n_list : F.n;
   if (n == 0) return true;
   const dim3 g(n);
 #define OMG_SR_RB(NC, BS, RB)                                                                                    \
   if (op == OP_LPL)                                                                                              \
-    k_smooth_resid<NC, OP_LPL, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc);  \
+    k_smooth_resid<NC, OP_LPL, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc,   \
+                                                         rbgv);                                                   \
   else                                                                                                           \
-    k_smooth_resid<NC, OP_HELM, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc);
+    k_smooth_resid<NC, OP_HELM, BS, RB><<<g, BS, 0, st>>>(F, C, lambda, restrict_on, parent_local, dixp, list, bc,  \
+                                                          rbgv);
 #define OMG_SR(NC, BS)           \
   if (has_rb) {                  \
     OMG_SR_RB(NC, BS, 2)         \
