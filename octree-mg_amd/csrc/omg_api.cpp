@@ -2436,7 +2436,8 @@ void build_plan(omg_ctx* c) {
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
     // (one GPU, tiled box sizes: the red-black smoother's coarse-part buffer)
-    if (!L.h_rb.empty() && c->n_ranks == 1 && !c->host_only && (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2))
+    if (!L.h_rb.empty() && c->n_ranks == 1 && !c->host_only && !c->no_rbgv &&
+        (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2))
       dmalloc(&L.d_rbgv, sizeof(double) * L.n * 6 * L.nc * L.nc);
     L.rbgv_ok = false;
     {
@@ -2668,6 +2669,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->tail_timing = env_flag("OMG_TAIL_TIMING");
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
     c->no_fill_crhs = env_flag("OMG_NO_FILL_CRHS");
+    c->no_rbgv = env_flag("OMG_NO_RBGV");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");

@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_fill_crhs: parity (one-rank goldens, per-operation and fused tests,
-# multi-rank goldens), then A/B against OMG_NO_FILL_CRHS
+# multi-rank goldens), then A/B against OMG_NO_FILL_CRHS and OMG_NO_RBGV
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r04
@@ -11,4 +11,5 @@ tail -1 $O/s12_tests.log
 for round in 1 2; do
   timeout -k 10 300 python -u tools/configs_bench.py --no-cpu --only C4 C2 C3 C1-gsrb C2-gs > $O/s12_A$round.txt 2>&1 || exit 1
   OMG_NO_FILL_CRHS=1 timeout -k 10 300 python -u tools/configs_bench.py --no-cpu --only C4 C2 C3 C1-gsrb C2-gs > $O/s12_B$round.txt 2>&1 || exit 1
+  OMG_NO_RBGV=1 timeout -k 10 300 python -u tools/configs_bench.py --no-cpu --only C4 > $O/s12_C$round.txt 2>&1 || exit 1
 done
