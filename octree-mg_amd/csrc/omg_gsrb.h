@@ -37,6 +37,7 @@ __device__ __forceinline__ void gsrb_load_rhs(const LevelView& L, int e, int b, 
       } else {
         fr.v[r] = *fp;
       }
+      if (L.rk) fr.v[r] = make_double2(rhs_true(L, fr.v[r].x), rhs_true(L, fr.v[r].y));
     }
   }
 }

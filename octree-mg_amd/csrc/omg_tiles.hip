@@ -79,7 +79,10 @@ __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const Lev
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
+    if (q2 < HV) {
+      fr[r] = ld_nt(f + 2 * q2);
+      if (F.rk) fr[r] = v2d{rhs_true(F, fr[r].x), rhs_true(F, fr[r].y)};
+    }
   }
   __syncthreads();
   resid_restrict_core<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp, b, sb, fr);
@@ -255,7 +258,10 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
 #pragma unroll
     for (int r = 0; r < NR; r++) {
       const int q2 = tid + BS * r;
-      if (q2 < HV) fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
+      if (q2 < HV) {
+        fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
+        if (F.rk) fr[r] = v2d{rhs_true(F, fr[r].x), rhs_true(F, fr[r].y)};
+      }
     }
   };
   if (!OMG_SR_EARLY) bulk_loads();
@@ -862,6 +868,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
     dst[r] = bb * P + seg * SEG + 2 * off;
   }
   const double m = SUB ? *mean : 0.0;
+  const bool chain = iv == 2 && L.rk;   // the true rhs (pending means applied)
   double2 v[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r]);
@@ -872,6 +879,7 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
     const int rc = H * (((c % (NC / R)) * R) + NC * (c / (NC / R)));   // chunk offset
 #pragma unroll
     for (int r = 0; r < PER; r++) {
+      if (chain) v[r] = make_double2(rhs_true(L, v[r].x), rhs_true(L, v[r].y));
       if (SUB) {
         v[r].x = v[r].x - m;
         v[r].y = v[r].y - m;
