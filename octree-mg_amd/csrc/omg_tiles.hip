@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const long long noff = (long long)T.arg(nb - 1) * F.stride;
     const double* un = F.phi + noff;
     gdeep[g] = un[sr_int<NC>(d, low ? NC - 1 : 2, a, c)];
-    grhs[g] = F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)];
+    grhs[g] = rhs_true(F, F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)]);
     // a tangential neighbour outside N's face (edges; two at corners)
     gedge[g][0] = gedge[g][1] = 0.0;
     const bool ea = a == 1 || a == NC, ec = c == 1 || c == NC;
