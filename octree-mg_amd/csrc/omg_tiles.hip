@@ -81,7 +81,6 @@ __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const Lev
     const int q2 = tid + BS * r;
     if (q2 < HV) {
       fr[r] = ld_nt(f + 2 * q2);
-      if (F.rk) fr[r] = v2d{rhs_true(F, fr[r].x), rhs_true(F, fr[r].y)};
     }
   }
   __syncthreads();
@@ -129,7 +128,7 @@ __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const Le
     s1.c = cc.y;
     double l0, l1;
     op_pair<NC, OP>(K, F, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
-    const double r0 = fr[r].x - l0, r1 = fr[r].y - l1;
+    const double r0 = rhs_true(F, fr[r].x) - l0, r1 = rhs_true(F, fr[r].y) - l1;
     mx = amax(mx, amax(fabs(r0), fabs(r1)));
     rv[r] = make_double2(r0, r1);
     st_nt(res + 2 * q2, r0, r1);
@@ -260,7 +259,6 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
       const int q2 = tid + BS * r;
       if (q2 < HV) {
         fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
-        if (F.rk) fr[r] = v2d{rhs_true(F, fr[r].x), rhs_true(F, fr[r].y)};
       }
     }
   };
@@ -284,7 +282,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     const long long noff = (long long)T.arg(nb - 1) * F.stride;
     const double* un = F.phi + noff;
     gdeep[g] = un[sr_int<NC>(d, low ? NC - 1 : 2, a, c)];
-    grhs[g] = rhs_true(F, F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)]);
+    grhs[g] = F.data[F.vstride + noff + sr_int<NC>(d, nl, a, c)];
     // a tangential neighbour outside N's face (edges; two at corners)
     gedge[g][0] = gedge[g][1] = 0.0;
     const bool ea = a == 1 || a == NC, ec = c == 1 || c == NC;
@@ -324,7 +322,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     if (q2 >= HV / 2) continue;
     Nbr7 s0, s1;
     pair_stencil<NC>(sb + HV, sb + 2 * HV + FH, FS, 0, 2 * q2, s0, s1);
-    const double v0 = gs_value<OP>(K, s0, fr[r].x), v1 = gs_value<OP>(K, s1, fr[r].y);
+    const double v0 = gs_value<OP>(K, s0, rhs_true(F, fr[r].x)), v1 = gs_value<OP>(K, s1, rhs_true(F, fr[r].y));
     reinterpret_cast<double2*>(sb)[q2] = make_double2(v0, v1);
     st_nt(u + 2 * q2, v0, v1);
   }
@@ -357,7 +355,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     s.yp = d == 1 ? dp : (d == 0 ? ap : cp);
     s.zm = d == 2 ? dm : cm;
     s.zp = d == 2 ? dp : cp;
-    sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, grhs[g]);
+    sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, rhs_true(F, grhs[g]));
   }
   // physical / refinement-boundary faces: both colours of their ghosts from
   // our final cells (the coarse operands of refinement-boundary cells were
