@@ -1124,10 +1124,6 @@ enum { kChPhi = 0, kChRhs = 1 };
 double* red_acc(omg_ctx* c, int ch) { return c->d_red + ch; }
 double* red_mean(omg_ctx* c, int ch) { return c->d_red + 2 + ch; }
 double* red_all(omg_ctx* c, int ch) { return c->d_red + 8 + (size_t)ch * c->n_ranks; }
-// the pending subtract_mean(rhs) means (LevelView::rchain) and a zero
-constexpr int kRhsChainMax = 8;
-double* red_chain(omg_ctx* c) { return c->d_red + 8 + 2 * (size_t)c->n_ranks; }
-double* red_zero(omg_ctx* c) { return red_chain(c) + kRhsChainMax; }
 
 // get_sum's loop (m_multigrid.f90:278-294) for this rank, in two parts: the
 // per-leaf sums of every level (into the channel's scratch), then acc = 0 and
@@ -1266,59 +1262,10 @@ void drop_rhs_cache(omg_ctx* c) {
   c->rhs_cache_valid = false;
   drop_rhs_lex(c);
 }
-
-// The pending-means chain of a periodic standalone cycle (round 4).  The
-// reference subtracts mean(rhs) from rhs at the start of every cycle
-// (m_multigrid.f90:170-174, 245-276): a read and a write of every leaf cell
-// (440 us of the 4.9-ms C3 cycle, with the box sums of the new values).  The
-// means are kept instead in a chain on the device and every kernel that
-// reads the level's rhs applies them on load, in order, each subtraction
-// rounded as the reference's (rhs_true, omg_device.h): the red-black
-// substeps, the fused down-step, residual + restriction, the box sums.  Each
-// cycle then only reads rhs for the sums of the new true values; every
-// kRhsChainMax cycles (and before anything else reads rhs) the chain is
-// written into rhs.  Where it applies: a red-black Laplacian / Helmholtz
-// stand-alone cycle whose leaves are exactly the boxes of the highest level,
-// which is LDS-tiled and more than one box (no coarse tail, no generic
-// kernel reads it).
-Level* rhs_chain_level(omg_ctx* c) {
-  if (c->no_rhs_chain || c->capturing || c->smoother != OMG_SMOOTHER_GSRB || (c->op != OP_LPL && c->op != OP_HELM))
-    return nullptr;
-  Level* H = level_ptr(c, c->highest);
-  if (!H || (int)H->leaves.size() != H->n || (int)c->ids[c->highest].size() < 2 || !tiled_nc(H->nc) ||
-      !subtract_sums_nc(H->nc))
-    return nullptr;
-  for (auto& kv : c->levels)
-    if (kv.first != c->highest && !kv.second.leaves.empty()) return nullptr;
-  return H;
-}
-void set_rhs_chain(omg_ctx* c, int k) {
-  c->rk = k;
-  for (auto& kv : c->levels) {
-    kv.second.rk = kv.first == c->highest ? k : 0;
-    kv.second.rchain = red_chain(c);
-  }
-}
-// write the chain into rhs (rhs = rhs_true; the same kernel as subtract_mean's
-// with a zero mean: x - 0.0 is x for every double)
-void materialize_rhs(omg_ctx* c) {
-  if (!c->rk) return;
-  side_done(c);   // (the box-sum scratch may feed a chain on the side stream)
-  for (auto& kv : c->levels) {
-    Level& L = kv.second;
-    if (!L.rk || !L.n) continue;
-    Prof p(c, "subtract_rhs", (double)L.n * L.nc * L.nc * L.nc, L.lvl);
-    launch_subtract_sums(L.sweep_view(), 2, L.d_leaves, L.n, red_zero(c), L.d_scratch_rhs, c->stream);
-  }
-  set_rhs_chain(c, 0);
-  c->rhs_cache_valid = false;
-}
-
 // entry points other than the cycles: apply pending phi work first; `writes`
 // = the call may change rhs (the cached rhs sum is dropped)
 void enter(omg_ctx* c, bool writes = true) {
   materialize_phi(c);
-  materialize_rhs(c);
   if (writes) drop_rhs_cache(c);
 }
 
@@ -1338,35 +1285,8 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
     for (auto& kv : c->levels)
       if (!ghosts || kv.second.any_phys || kv.second.any_rb) kv.second.phi_gc_ok = false;
   }
-  Level* CH = iv == 2 && !ghosts && mode == kInCycle ? rhs_chain_level(c) : nullptr;
-  if (iv == 2 && !CH) materialize_rhs(c);
-  if (CH && c->rk < kRhsChainMax) {
-    // append this cycle's mean to the chain; the box sums of the new true
-    // rhs for the next cycle's get_sum, their sequential chain on the side
-    if (c->rhs_cache_valid) {
-      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_side, 0));
-    } else {
-      leaf_sum_device(c, 2, kChRhs);
-    }
-    drop_rhs_lex(c);
-    mean_device(c, kChRhs);
-    HIPCHK(hipMemcpyAsync(red_chain(c) + c->rk, red_mean(c, kChRhs), sizeof(double), hipMemcpyDeviceToDevice,
-                          c->stream));
-    set_rhs_chain(c, c->rk + 1);
-    {
-      Prof p(c, "box_sums", (double)CH->n * CH->nc * CH->nc * CH->nc, CH->lvl);
-      launch_box_sums(CH->sweep_view(), 2, CH->d_leaves, CH->n, CH->d_scratch_rhs, c->stream);
-    }
-    HIPCHK(hipEventRecord(c->ev_main, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_main, 0));
-    leaf_chain(c, kChRhs, c->stream2);
-    HIPCHK(hipEventRecord(c->ev_side, c->stream2));
-    c->rhs_cache_valid = true;
-    return;
-  }
   if (iv == 2 && !ghosts) {
     // rhs: the sums may already be running on the side stream (see below)
-    // (a full chain: the subtraction below writes it into rhs first)
     if (c->rhs_cache_valid) {
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_side, 0));
     } else {
@@ -1384,12 +1304,10 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       if (l >= 1 && (int)L->leaves.size() == L->n && subtract_sums_nc(L->nc))
         launch_subtract_sums(L->sweep_view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
       else {
-        if (L->rk) throw OmgError("internal: rhs chain on a level without the fused subtraction");
         launch_subtract(L->view(), 2, red_mean(c, kChRhs), 0, c->stream);
         if (l >= 1 && !L->leaves.empty()) all_fused = false;
       }
     }
-    set_rhs_chain(c, 0);   // (a full chain went into rhs with this mean)
     if (all_fused) {
       // the next get_sum(rhs): its leaf sums were produced by the fused
       // kernels; its sequential chain runs now on the side stream
@@ -1675,7 +1593,6 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   const bool has_highest = highest_lvl >= c->lowest;
   const int min_lvl = c->lowest, max_lvl = has_highest ? highest_lvl : c->highest;
   const bool full = standalone && !has_highest;   // a stand-alone cycle over the whole tree
-  if (!full) materialize_rhs(c);   // (the pending rhs means live only across stand-alone cycles)
   // a pending phi shift (previous stand-alone cycle) is absorbed by the first
   // substep on max_lvl or dropped where restriction overwrites a level
   if (c->phi_shift_pending) {
@@ -1771,7 +1688,6 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
 
 // mg_fas_fmg (m_multigrid.f90:84-147)
 double fas_fmg(omg_ctx* c, bool have_guess, bool want_max_res) {
-  materialize_rhs(c);
   if (have_guess) {
     materialize_phi(c);
   } else {
@@ -2754,7 +2670,6 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
     c->no_fill_crhs = env_flag("OMG_NO_FILL_CRHS");
     c->no_rbgv = env_flag("OMG_NO_RBGV");
-    c->no_rhs_chain = env_flag("OMG_NO_RHS_CHAIN");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
@@ -2772,8 +2687,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_scalar, sizeof(double) * (64 + 2 * (size_t)n_ranks)));
-    HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks + kRhsChainMax + 1)));
-    HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks + kRhsChainMax + 1)));
+    HIPCHK(hipMalloc(&c->d_red, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
+    HIPCHK(hipMemset(c->d_red, 0, sizeof(double) * (8 + 2 * (size_t)n_ranks)));
     HIPCHK(hipMalloc(&c->d_maxslots, sizeof(unsigned long long) * omg::kMaxSlots * omg::kMaxSlotStride));
     // (allocated here: no allocation may happen while a cycle is captured)
     HIPCHK(hipMalloc(&c->d_tail, sizeof(TailArgs)));
@@ -2922,7 +2837,6 @@ int omg_tree_setup(omg_ctx* c, int n_boxes, const int* lvl, const int* parent, c
     c->phi_shift_pending = false;
     c->phi_mean_on_side = false;
     build_plan(c);
-    if (!c->host_only) set_rhs_chain(c, 0);
     if (!c->host_only) HIPCHK(hipDeviceSynchronize());
   });
 }
@@ -2950,10 +2864,7 @@ int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* pee
 }
 
 int omg_set_operator(omg_ctx* c, int op, double lambda) {
-  return guarded([&] {
-    materialize_rhs(c);   // (the pending means are applied by the red-black Laplacian / Helmholtz kernels)
-    set_operator(c, op, lambda);
-  });
+  return guarded([&] { set_operator(c, op, lambda); });
 }
 
 int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up, int max_coarse_cycles,
@@ -2961,7 +2872,6 @@ int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up,
   return guarded([&] {
     if (smoother != OMG_SMOOTHER_GS && smoother != OMG_SMOOTHER_GSRB)
       throw OmgError("unsupported smoother type");
-    materialize_rhs(c);
     c->smoother = smoother;
     c->n_substeps = smoother == OMG_SMOOTHER_GSRB ? 2 : 1;
     ensure_rhs_lex(c);
@@ -2974,10 +2884,7 @@ int omg_set_smoother(omg_ctx* c, int smoother, int n_cycle_down, int n_cycle_up,
 }
 
 int omg_set_subtract_mean(omg_ctx* c, int on) {
-  return guarded([&] {
-    materialize_rhs(c);
-    c->subtract_mean = on;
-  });
+  return guarded([&] { c->subtract_mean = on; });
 }
 
 int omg_set_bc(omg_ctx* c, int iv, int nb, int bc_type, double bc_value) {

@@ -108,14 +108,6 @@ struct Tl {
   }
 };
 
-// the level's true rhs from the stored value: the pending subtract_mean(rhs)
-// means, in order, each subtraction rounded as the reference's was
-// (LevelView::rchain; rk = 0 everywhere but a periodic cycle's leaf level)
-__device__ __forceinline__ double rhs_true(const LevelView& L, double x) {
-  for (int j = 0; j < L.rk; j++) x = x - L.rchain[j];
-  return x;
-}
-
 // max of two |res| values (non-negative, or NaN) on their IEEE bit patterns:
 // the same result as fmax for numbers, but NaN and Inf propagate (fmax drops
 // a NaN operand), so a diverged field reaches the max residual

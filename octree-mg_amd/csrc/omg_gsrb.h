@@ -294,11 +294,9 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
       if constexpr (is_varop(OP)) {
         AEps E0, E1;
         pair_eps<NC, OP>(L, b, e, q, E0, E1);
-        nv = make_double2(ags_value<OP>(K, s0, E0, rhs_true(L, fr[r].x)), ags_value<OP>(K, s1, E1, rhs_true(L, fr[r].y)));
+        nv = make_double2(ags_value<OP>(K, s0, E0, fr[r].x), ags_value<OP>(K, s1, E1, fr[r].y));
       } else {
-        // (the pending rhs means applied where rhs is used: at the load they
-        // would make the stream-in wait for each value)
-        nv = make_double2(gs_value<OP>(K, s0, rhs_true(L, fr[r].x)), gs_value<OP>(K, s1, rhs_true(L, fr[r].y)));
+        nv = make_double2(gs_value<OP>(K, s0, fr[r].x), gs_value<OP>(K, s1, fr[r].y));
       }
     } else {   // NC == 2: one cell per row
       double v[2];
@@ -316,9 +314,9 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
         st.zm = k > 1 ? so[tj + H * (row - NC)] : sg[4 * FH + tj + H * (j - 1)];
         st.zp = k < NC ? so[tj + H * (row + NC)] : sg[5 * FH + tj + H * (j - 1)];
         if constexpr (is_varop(OP))
-          v[s] = ags_value<OP>(K, st, load_eps<OP>(L, b, i, j, k), rhs_true(L, s ? fr[r].y : fr[r].x));
+          v[s] = ags_value<OP>(K, st, load_eps<OP>(L, b, i, j, k), s ? fr[r].y : fr[r].x);
         else
-          v[s] = gs_value<OP>(K, st, rhs_true(L, s ? fr[r].y : fr[r].x));
+          v[s] = gs_value<OP>(K, st, s ? fr[r].y : fr[r].x);
       }
       nv = make_double2(v[0], v[1]);
     }

@@ -56,11 +56,6 @@ struct LevelView {
   const int* sendpos;    // [n*6] halo send slot of remote faces (or -1)
   const int* topo;       // [n*8] packed face kinds + arguments (FaceTopo, omg_face.h; pack_topo)
   int rev;               // walk each XCD's run of boxes backwards (xcd_box)
-  // pending subtract_mean(rhs) values: the level's true rhs is the stored one
-  // minus rchain[0], then minus rchain[1], ... (rk values, each rounded), which
-  // every kernel that reads this level's rhs applies on load (rhs_true)
-  const double* rchain;
-  int rk;
 };
 
 // doubles of one stored ghost face (both colour halves)
@@ -149,8 +144,6 @@ struct Level {
   int* d_parents = nullptr;
   int* d_leaves = nullptr;
   uint8_t* d_parmask = nullptr;     // per box: 1 = a parent (k_fill_crhs)
-  const double* rchain = nullptr;   // pending rhs means (LevelView::rchain, omg_api.cpp rhs_chain_level)
-  int rk = 0;
   // refinement-boundary levels (one GPU): the coarse part of every rb ghost,
   // [box][face][nc*nc] (RbSide::gv), valid while the level below is unchanged
   double* d_rbgv = nullptr;
@@ -216,8 +209,6 @@ struct Level {
     v.sendpos = d_sendpos;
     v.topo = d_topo;
     v.rev = 0;
-    v.rchain = rchain;
-    v.rk = rk;
     return v;
   }
   // the view for a level-wide pass: successive passes walk the boxes in
@@ -303,8 +294,6 @@ struct omg_ctx {
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
   bool no_fill_crhs = false;           // OMG_NO_FILL_CRHS: update_coarse's fill and coarse rhs as two passes
   bool no_rbgv = false;                // OMG_NO_RBGV: no stored refinement-boundary coarse parts
-  bool no_rhs_chain = false;           // OMG_NO_RHS_CHAIN: subtract_mean(rhs) writes rhs every cycle
-  int rk = 0;                          // pending rhs means (d_red's chain slots, rhs_chain_level)
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
   bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring

@@ -79,9 +79,7 @@ __device__ __forceinline__ void resid_restrict_box(const LevelView& F, const Lev
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int q2 = tid + BS * r;
-    if (q2 < HV) {
-      fr[r] = ld_nt(f + 2 * q2);
-    }
+    if (q2 < HV) fr[r] = ld_nt(f + 2 * q2);
   }
   __syncthreads();
   resid_restrict_core<NC, OP, BS>(F, Cv, lambda, maxbits, restrict_on, parent_local, dixp, b, sb, fr);
@@ -128,7 +126,7 @@ __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const Le
     s1.c = cc.y;
     double l0, l1;
     op_pair<NC, OP>(K, F, b, e, 2 * q2 - e * HV, s0, s1, l0, l1);
-    const double r0 = rhs_true(F, fr[r].x) - l0, r1 = rhs_true(F, fr[r].y) - l1;
+    const double r0 = fr[r].x - l0, r1 = fr[r].y - l1;
     mx = amax(mx, amax(fabs(r0), fabs(r1)));
     rv[r] = make_double2(r0, r1);
     st_nt(res + 2 * q2, r0, r1);
@@ -257,9 +255,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
 #pragma unroll
     for (int r = 0; r < NR; r++) {
       const int q2 = tid + BS * r;
-      if (q2 < HV) {
-        fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
-      }
+      if (q2 < HV) fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
     }
   };
   if (!OMG_SR_EARLY) bulk_loads();
@@ -322,7 +318,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     if (q2 >= HV / 2) continue;
     Nbr7 s0, s1;
     pair_stencil<NC>(sb + HV, sb + 2 * HV + FH, FS, 0, 2 * q2, s0, s1);
-    const double v0 = gs_value<OP>(K, s0, rhs_true(F, fr[r].x)), v1 = gs_value<OP>(K, s1, rhs_true(F, fr[r].y));
+    const double v0 = gs_value<OP>(K, s0, fr[r].x), v1 = gs_value<OP>(K, s1, fr[r].y);
     reinterpret_cast<double2*>(sb)[q2] = make_double2(v0, v1);
     st_nt(u + 2 * q2, v0, v1);
   }
@@ -355,7 +351,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
     s.yp = d == 1 ? dp : (d == 0 ? ap : cp);
     s.zm = d == 2 ? dm : cm;
     s.zp = d == 2 ? dp : cp;
-    sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, rhs_true(F, grhs[g]));
+    sb[2 * HV + (nb - 1) * FS + hi] = gs_value<OP>(K, s, grhs[g]);
   }
   // physical / refinement-boundary faces: both colours of their ghosts from
   // our final cells (the coarse operands of refinement-boundary cells were
@@ -866,7 +862,6 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
     dst[r] = bb * P + seg * SEG + 2 * off;
   }
   const double m = SUB ? *mean : 0.0;
-  const bool chain = iv == 2 && L.rk;   // the true rhs (pending means applied)
   double2 v[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r]);
@@ -877,7 +872,6 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
     const int rc = H * (((c % (NC / R)) * R) + NC * (c / (NC / R)));   // chunk offset
 #pragma unroll
     for (int r = 0; r < PER; r++) {
-      if (chain) v[r] = make_double2(rhs_true(L, v[r].x), rhs_true(L, v[r].y));
       if (SUB) {
         v[r].x = v[r].x - m;
         v[r].y = v[r].y - m;
