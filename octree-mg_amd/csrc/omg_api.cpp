@@ -894,7 +894,9 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
 
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down
 // substep is still to do (smooth_resid_ok), k_smooth_resid runs it
-void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
+// with tail_crhs the coarse tail forms lvl-1's ghosts and coarse rhs itself
+// (its top level, TailArgs::top_crhs): only the residual and the restriction here
+void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = false) {
   Level* F = level_ptr(c, lvl);
   if (Level* Cl = level_ptr(c, lvl - 1)) {
     Cl->rhs_lex_ok = false;   // its rhs is rewritten below
@@ -957,6 +959,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false) {
     restrict_lvl(c, 1, lvl);
     restrict_lvl(c, 4, lvl);
   }
+  if (tail_crhs) return;
   Level* C = level_ptr(c, lvl - 1);
   // the fill of lvl-1 and its parents' coarse rhs in one pass when its faces
   // are same-GPU or physical (k_fill_crhs: a parent box reads its
@@ -1505,7 +1508,37 @@ void check_mid_err(omg_ctx* c) {
 
 // Levels lowest..top of the V-cycle (down-smoothing of top .. up-smoothing of
 // top) in one launch, bit-identical to the level-by-level path.
-void run_tail(omg_ctx* c, int top) {
+// the LDS-resident part of the tail (omg_tiles.hip): one box per level whose
+// faces are physical or the box itself, the lowest levels up to 8^3 cells
+// (at most three: 2^3, 4^3, 8^3, 5,120 doubles for their four variables),
+// and a 16^3 top level right above them
+void tail_lds_plan(omg_ctx* c, int top, int* lds_levels, int* lds_top) {
+  const int n_lvls = top - c->lowest + 1;
+  auto lds_box_ok = [&](int l, int max_nc) {
+    Level* L = level_ptr(c, l);
+    if (!L || L->n != 1 || L->nc > max_nc) return false;
+    for (int nb = 0; nb < 6; nb++) {
+      const int k = L->h_nbk[nb];
+      if (!(k == NB_PHYS || (k == NB_LOCAL && L->h_nba[nb] == 0))) return false;
+    }
+    return true;
+  };
+  int n = 0;
+  while (n < std::min(n_lvls, kTailLdsMaxLevels) && lds_box_ok(c->lowest + n, 8)) n++;
+  *lds_levels = n;
+  *lds_top = n > 0 && n == n_lvls - 1 && level_ptr(c, top)->nc == 16 && lds_box_ok(top, 16);
+}
+
+// whether the tail can take over update_coarse's fill and coarse rhs of its
+// top level: a single parent box on this GPU whose faces are physical or same-
+// GPU (kTailMaxBoxes), after a level-by-level down-step of top+1
+bool tail_crhs_ok(omg_ctx* c, int top) {
+  const Level* T = level_ptr(c, top);
+  return !c->no_tail_crhs && T && T->n == 1 && !T->parents.empty() && !T->has_rb && !T->has_remote &&
+         level_ptr(c, top + 1) != nullptr;
+}
+
+void run_tail(omg_ctx* c, int top, bool top_crhs) {
   TailArgs A;
   std::memset(&A, 0, sizeof(A));   // padding too: compared bytewise below
   A.n_lvls = top - c->lowest + 1;
@@ -1533,28 +1566,13 @@ void run_tail(omg_ctx* c, int top) {
   A.maxbits = (unsigned long long*)c->d_scalar;
   A.coarse_its = (int*)(c->d_scalar + 1);
   A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
-  // the LDS-resident part of the tail (omg_tiles.hip): one box per level whose
-  // faces are physical or the box itself, the lowest levels up to 8^3 cells
-  // (at most three: 2^3, 4^3, 8^3, 5,120 doubles for their four variables),
-  // and a 16^3 top level right above them
-  auto lds_box_ok = [&](int l, int max_nc) {
-    Level* L = level_ptr(c, l);
-    if (!L || L->n != 1 || L->nc > max_nc) return false;
-    for (int nb = 0; nb < 6; nb++) {
-      const int k = L->h_nbk[nb];
-      if (!(k == NB_PHYS || (k == NB_LOCAL && L->h_nba[nb] == 0))) return false;
-    }
-    return true;
-  };
-  A.lds_levels = 0;
-  while (A.lds_levels < std::min(A.n_lvls, kTailLdsMaxLevels) && lds_box_ok(c->lowest + A.lds_levels, 8))
-    A.lds_levels++;
-  A.lds_top = A.lds_levels > 0 && A.lds_levels == A.n_lvls - 1 && level_ptr(c, top)->nc == 16 &&
-              lds_box_ok(top, 16);
+  A.top_crhs = top_crhs;
+  tail_lds_plan(c, top, &A.lds_levels, &A.lds_top);
   const bool tail_timing = c->tail_timing;
   if (tail_timing) {
     if (!c->d_tail_stamps) HIPCHK(hipMalloc(&c->d_tail_stamps, 8 * 64));   // (never captured: graph_ok)
     A.stamps = c->d_tail_stamps;
+    HIPCHK(hipMemsetAsync(c->d_tail_stamps, 0, 8 * 64, c->stream));   // (unwritten stamps stay 0)
   }
   if (std::memcmp(&A, c->h_tail, sizeof(TailArgs)) != 0) {
     *c->h_tail = A;   // what d_tail holds once the stream gets here
@@ -1568,9 +1586,8 @@ void run_tail(omg_ctx* c, int top) {
     long long h[64];
     HIPCHK(hipMemcpyAsync(h, c->d_tail_stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     host_sync(c, c->stream);
-    const int n = 4 * (A.n_lvls - 1) + 2 + 2 * (A.n_lvls - 1);
     std::fprintf(stderr, "tail us:");
-    for (int i = 1; i < n; i++) std::fprintf(stderr, " %.1f", (h[i] - h[i - 1]) * 0.01);
+    for (int i = 1; i < 64 && h[i]; i++) std::fprintf(stderr, " %.1f", (h[i] - h[i - 1]) * 0.01);
     std::fprintf(stderr, "\n");
   }
   for (int l = c->lowest; l <= top; l++) level_ptr(c, l)->phi_gc_ok = true;
@@ -1631,6 +1648,7 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   const int top = tail_top(c, max_lvl);
   const bool tail = top >= min_lvl && !c->no_tail;
   const int mtop = tail ? mid_top(c, top, max_lvl) : INT_MIN;
+  const bool tail_crhs = tail && mtop == INT_MIN && max_lvl > top && tail_crhs_ok(c, top);
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
     if (mtop != INT_MIN && l == mtop) {   // mtop .. top+1 in one launch
@@ -1639,10 +1657,10 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
     const bool fused = smooth_resid_ok(c, l);
     smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
-    update_coarse(c, l, fused);
+    update_coarse(c, l, fused, tail_crhs && l == top + 1);
   }
   if (tail) {
-    run_tail(c, top);
+    run_tail(c, top, tail_crhs);
   } else {
     // coarse grid: all its boxes live on one rank (error stop otherwise, :197-200)
     const auto& ids = c->ids[min_lvl];
@@ -2669,6 +2687,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->tail_timing = env_flag("OMG_TAIL_TIMING");
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
     c->no_fill_crhs = env_flag("OMG_NO_FILL_CRHS");
+    c->no_tail_crhs = env_flag("OMG_NO_TAIL_CRHS");
     c->no_rbgv = env_flag("OMG_NO_RBGV");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");

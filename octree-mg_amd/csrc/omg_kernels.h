@@ -144,6 +144,9 @@ struct TailArgs {
   // cells, a single box whose local faces are itself), and lds_top: the 16^3
   // top level above them too (tail_lds_plan in omg_api.cpp)
   int lds_levels, lds_top;
+  // the tail forms the top level's ghosts and its coarse rhs = L(phi) + res,
+  // old = phi itself (update_coarse of top+1 stopped after the restriction)
+  int top_crhs, pad_;
 };
 // how many of the tail's lowest levels qualify for the LDS-resident program
 constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3

@@ -1593,7 +1593,7 @@ __device__ __forceinline__ int stored_dense(int q) {
   return i + S * (j + S * k);
 }
 
-template <int NC, int NV, bool LOAD>
+template <int NC, int NV, bool LOAD, int V0 = 1>
 __device__ void tail_io_stored(const LevelView& L, double* dst) {
   constexpr int S = NC + 2, S3 = S * S * S, NP = Tl<NC>::NST / 2, N = NV * NP;
   constexpr int R = (N + kTailBS - 1) / kTailBS;
@@ -1620,7 +1620,7 @@ __device__ void tail_io_stored(const LevelView& L, double* dst) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int t = tid + kTailBS * r;
-      if (t < N) v[r] = reinterpret_cast<const v2d*>(boxp(L, t / NP + 1, 0))[t % NP];
+      if (t < N) v[r] = reinterpret_cast<const v2d*>(boxp(L, t / NP + V0, 0))[t % NP];
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -1639,10 +1639,53 @@ __device__ void tail_io_stored(const LevelView& L, double* dst) {
       v2d x;
       x.x = dst[var * S3 + stored_dense<NC>(2 * p)];
       x.y = dst[var * S3 + stored_dense<NC>(2 * p + 1)];
-      reinterpret_cast<v2d*>(boxp(L, var + 1, 0))[p] = x;
+      reinterpret_cast<v2d*>(boxp(L, var + V0, 0))[p] = x;
     }
   }
 }
+
+// the same load in two halves, so that the loads of several boxes are all in
+// flight before the first one is scattered (one memory latency for the tail's
+// whole entry instead of one per box)
+template <int NC, int NV>
+struct TailIoRegs {
+  static constexpr int NP = Tl<NC>::NST / 2, N = NV * NP, R = (N + kTailBS - 1) / kTailBS;
+  v2d v[R];
+  __device__ __forceinline__ void issue(const LevelView& L) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int t = threadIdx.x + kTailBS * r;
+      if (t < N) v[r] = reinterpret_cast<const v2d*>(boxp(L, t / NP + 1, 0))[t % NP];
+    }
+  }
+  __device__ __forceinline__ void commit(double* dst) const {
+    constexpr int S = NC + 2, S3 = S * S * S, NE = 12 * NC + 8;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < NV * NE; t += kTailBS) {   // edges and corners: zero
+      const int var = t / NE, e = t % NE;
+      int x, y, z;
+      if (e < 12 * NC) {
+        const int ax = e / (4 * NC), w = e % (4 * NC), m = w / NC, a = w % NC + 1;
+        const int u = (m & 1) ? S - 1 : 0, q = (m & 2) ? S - 1 : 0;
+        if (ax == 0) { x = a; y = u; z = q; }
+        else if (ax == 1) { x = u; y = a; z = q; }
+        else { x = u; y = q; z = a; }
+      } else {
+        const int m = e - 12 * NC;
+        x = (m & 1) ? S - 1 : 0; y = (m & 2) ? S - 1 : 0; z = (m & 4) ? S - 1 : 0;
+      }
+      dst[var * S3 + x + S * (y + S * z)] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int t = tid + kTailBS * r;
+      if (t >= N) continue;
+      const int var = t / NP, p = t % NP;
+      dst[var * S3 + stored_dense<NC>(2 * p)] = v[r].x;
+      dst[var * S3 + stored_dense<NC>(2 * p + 1)] = v[r].y;
+    }
+  }
+};
 
 template <bool LOAD>
 __device__ void tail_io_box(const LevelView& L, double* dst) {   // the LDS levels: all four variables
@@ -1670,44 +1713,78 @@ __device__ void tail_boxes_io(const TailArgs& A, int ls, double* tl) {
 // physical face cell (bc_to_gc's argument: the stored value in the rhs ghost
 // when mg_phi_bc_store ran, else the tabulated or constant one); after the
 // rhs ghosts are in LDS
-__device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailLdsLevel& D) {
-  const TailLevel& T = A.lv[l];
-  const LevelView& L = T.L;
-  const GcBC& bc = T.bc;
+__device__ __forceinline__ void tail_setup_coef(const TailArgs& A, int l, TailLdsLevel& D, int nb) {
+  const LevelView& L = A.lv[l].L;
+  const GcBC& bc = A.lv[l].bc;
+  const bool low = nb & 1;
+  int type;
+  if (bc.phi_stored) type = L.nba[nb - 1];
+  else if (bc.face_off && bc.face_off[nb - 1] >= 0) type = bc.face_type[nb - 1];
+  else type = bc.type[nb - 1];
+  double c0, c1, c2;
+  if (type == -10) {
+    c0 = 2; c1 = -1; c2 = 0;
+  } else if (type == -11) {
+    c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
+  } else {
+    c0 = 0; c1 = 2; c2 = -1;
+  }
+  D.local[nb - 1] = L.nbk[nb - 1] == NB_LOCAL;
+  D.c0[nb - 1] = c0;
+  D.c1[nb - 1] = c1;
+  D.c2[nb - 1] = c2;
+}
+
+// face cell p (6 nc^2 of them) of level l: whether its face is physical, and
+// its bc value into bv
+__device__ __forceinline__ bool tail_bc_value(const TailArgs& A, int l, const TailBox& X, int p, double& bv) {
+  const LevelView& L = A.lv[l].L;
+  const GcBC& bc = A.lv[l].bc;
   const int nc = X.nc, nc2 = nc * nc;
-  if (threadIdx.x < 6) {
-    const int nb = threadIdx.x + 1;
-    const bool low = nb & 1;
-    int type;
-    if (bc.phi_stored) type = L.nba[nb - 1];
-    else if (bc.face_off && bc.face_off[nb - 1] >= 0) type = bc.face_type[nb - 1];
-    else type = bc.type[nb - 1];
-    double c0, c1, c2;
-    if (type == -10) {
-      c0 = 2; c1 = -1; c2 = 0;
-    } else if (type == -11) {
-      c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
-    } else {
-      c0 = 0; c1 = 2; c2 = -1;
-    }
-    D.local[nb - 1] = L.nbk[nb - 1] == NB_LOCAL;
-    D.c0[nb - 1] = c0;
-    D.c1[nb - 1] = c1;
-    D.c2[nb - 1] = c2;
-  }
-  for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
-    const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
-    if (L.nbk[nb - 1] != NB_PHYS) continue;
-    const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
+  const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
+  if (L.nbk[nb - 1] != NB_PHYS) return false;
+  const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
+  if (bc.phi_stored)
+    bv = X.F[d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g)];
+  else if (bc.face_off && bc.face_off[nb - 1] >= 0)
+    bv = bc.face_data[bc.face_off[nb - 1] + (a - 1) + (long long)nc * (c - 1)];
+  else
+    bv = bc.value[nb - 1];
+  return true;
+}
+
+__device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailLdsLevel& D) {
+  if (threadIdx.x < 6) tail_setup_coef(A, l, D, threadIdx.x + 1);
+  for (int p = threadIdx.x; p < 6 * X.nc * X.nc; p += blockDim.x) {
     double bv;
-    if (bc.phi_stored)
-      bv = X.F[d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g)];
-    else if (bc.face_off && bc.face_off[nb - 1] >= 0)
-      bv = bc.face_data[bc.face_off[nb - 1] + (a - 1) + (long long)nc * (c - 1)];
-    else
-      bv = bc.value[nb - 1];
-    X.B[p] = bv;
+    if (tail_bc_value(A, l, X, p, bv)) X.B[p] = bv;
   }
+}
+
+// tail_lds_setup of the usual chain (16^3 top over 8^3, 4^3, 2^3) at once:
+// every bc value of the four levels read before the first is stored
+__device__ void tail_setup_chain(const TailArgs& A, int top, const TailBox& XB, double* lds, TailLdsLevel* tll) {
+  constexpr int O8 = 6 * 256, O4 = O8 + 6 * 64, O2 = O4 + 6 * 16, NT = O2 + 6 * 4;
+  constexpr int R = (NT + kTailBS - 1) / kTailBS;
+  if (threadIdx.x < 24) {
+    const int k = threadIdx.x / 6, l = k == 0 ? top : 3 - k;
+    tail_setup_coef(A, l, tll[l], threadIdx.x % 6 + 1);
+  }
+  double bv[R];
+  double* dst[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    dst[r] = nullptr;
+    const int t = threadIdx.x + kTailBS * r;
+    if (t >= NT) continue;
+    const int l = t < O8 ? top : t < O4 ? 2 : t < O2 ? 1 : 0;
+    const int p = t - (t < O8 ? 0 : t < O4 ? O8 : t < O2 ? O4 : O2);
+    const TailBox X = l == top ? XB : tail_box(A, l, lds);
+    if (tail_bc_value(A, l, X, p, bv[r])) dst[r] = X.B + p;
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (dst[r]) *dst[r] = bv[r];
 }
 
 // phi and rhs of the 16^3 top level (interior and face ghosts) HBM <-> LDS;
@@ -1800,6 +1877,38 @@ __device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
   __syncthreads();
 }
 
+
+// update_coarse's parent part for the 16^3 top level (A.top_crhs): the ghost
+// fill of phi in LDS, old = phi over the stored box and rhs = L(phi) + res on
+// the interior, both to HBM (the level's rhs and old after the cycle, and the
+// old its correction of top+1 reads), rhs into LDS for the smoothing; the
+// arithmetic of k_fill_crhs / coarse_rhs_box on the same operands
+template <int OP>
+__device__ void tail_big_crhs(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X) {
+  const LevelView& L = A.lv[li].L;
+  const OpCoef<OP> K(L, A.lambda);
+  constexpr int N3 = 16 * 16 * 16, R = N3 / kTailBS;
+  static_assert(N3 % kTailBS == 0, "whole rounds of interior cells");
+  const double* res = boxp(L, 4, 0);
+  double* rhs = boxp(L, 2, 0);
+  double rv[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {   // the residual loads overlap the fill
+    const int q = threadIdx.x + kTailBS * r;
+    rv[r] = res[off_int(L, (q & 15) + 1, ((q >> 4) & 15) + 1, (q >> 8) + 1)];
+  }
+  tail_lds_fill(D, X);
+  tail_io_stored<16, 1, false, 3>(L, X.P);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int q = threadIdx.x + kTailBS * r;
+    const int i = (q & 15) + 1, j = ((q >> 4) & 15) + 1, k = (q >> 8) + 1, c = X.at(i, j, k);
+    const double v = op_value<OP>(K, tail_nbr(X, X.P, c)) + rv[r];
+    X.F[c] = v;
+    rhs[off_int(L, i, j, k)] = v;
+  }
+  __syncthreads();
+}
 
 // one red-black substep (colour e) of an NC^3 box in LDS: the cells of colour
 // e only, i = 2*ih + 1 + p with (i+j+k) & 1 == e; colour e reads colour 1-e
@@ -2014,13 +2123,50 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
     __syncthreads();
   };
   stamp();
-  if (ls == top) enter_lds();
+  if (ls == top) {
+    enter_lds();
+    if (A.top_crhs) {
+      const TailBox X = tail_box(A, top, lds);
+      tail_lds_fill(tll[top], X);
+      tail_lds_coarse_rhs<OP>(A, top, X);
+    }
+  } else if (A.top_crhs && !big) {
+    tail_fill(A, top);
+    tail_coarse_rhs<OP>(A, top, lds);
+  }
   if (big) {
-    tail_big_io<true>(A.lv[top].L, XB);
-    tail_boxes_io<true>(A, ls, lds);
-    for (int l = 0; l <= ls; l++) tail_lds_setup(A, l, tail_box(A, l, lds), tll[l]);
-    tail_lds_setup(A, top, XB, tll[top]);
+    if (ls == 2 && A.lv[0].L.nc == 2 && A.lv[1].L.nc == 4 && A.lv[2].L.nc == 8) {
+      // the usual chain (16^3 over 8^3, 4^3, 2^3): every load in flight at once
+      TailIoRegs<16, 2> r16;
+      TailIoRegs<8, 4> r8;
+      TailIoRegs<4, 4> r4;
+      TailIoRegs<2, 4> r2;
+      r16.issue(A.lv[top].L);
+      r8.issue(A.lv[2].L);
+      r4.issue(A.lv[1].L);
+      r2.issue(A.lv[0].L);
+      r16.commit(XB.P);
+      r8.commit(tail_box(A, 2, lds).P);
+      r4.commit(tail_box(A, 1, lds).P);
+      r2.commit(tail_box(A, 0, lds).P);
+      __syncthreads();
+      stamp();
+    } else {
+      tail_big_io<true>(A.lv[top].L, XB);
+      tail_boxes_io<true>(A, ls, lds);
+      stamp();
+    }
+    stamp();
+    if (ls == 2 && A.lv[0].L.nc == 2 && A.lv[1].L.nc == 4 && A.lv[2].L.nc == 8) {
+      tail_setup_chain(A, top, XB, lds, tll);
+    } else {
+      for (int l = 0; l <= ls; l++) tail_lds_setup(A, l, tail_box(A, l, lds), tll[l]);
+      tail_lds_setup(A, top, XB, tll[top]);
+    }
     __syncthreads();
+    stamp();
+    if (A.top_crhs) tail_big_crhs<OP>(A, top, tll[top], XB);
+    stamp();
     const TailBox Xc = tail_box(A, ls, lds);
     tail_lds_smooth<OP, LEX>(A, top, tll[top], XB, A.n_down);
     stamp();
