@@ -1556,6 +1556,16 @@ void run_tail(omg_ctx* c, int top, bool top_crhs) {
     T.n_par = (int)L->parents.size();
     T.parent_local = L->d_parent_local;
     T.dixp = L->d_dix;
+    // the first box's bc table entries inline (the LDS setup reads them
+    // without a dependent load)
+    auto fo = c->h_face_off_lvl[0].find(l);
+    auto ft = c->h_face_type_lvl[0].find(l);
+    for (int nb = 0; nb < 6; nb++) {
+      const bool tab = fo != c->h_face_off_lvl[0].end() && fo->second.size() >= 6;
+      const long long o = tab ? fo->second[nb] : -1;
+      T.foff[nb] = o > INT_MAX ? -2 : (int)o;
+      T.ftype[nb] = (signed char)(tab && ft != c->h_face_type_lvl[0].end() && ft->second.size() >= 6 ? ft->second[nb] : 0);
+    }
   }
   A.lambda = c->lambda;
   A.n_down = c->n_cycle_down;
@@ -2135,6 +2145,8 @@ void free_store_bc(omg_ctx* c, omg_free_state* S, const double* box_r_min) {
   for (auto& kv : c->d_face_type_lvl[k]) dfree(kv.second);
   c->d_face_off_lvl[k].clear();
   c->d_face_type_lvl[k].clear();
+  c->h_face_off_lvl[k].clear();
+  c->h_face_type_lvl[k].clear();
   dfree(c->d_face_data[k]);
   std::vector<FreeFace> faces;
   long long n_data = 0;
@@ -2164,6 +2176,8 @@ void free_store_bc(omg_ctx* c, omg_free_state* S, const double* box_r_min) {
       }
     c->d_face_off_lvl[k][kv.first] = to_device(off);
     c->d_face_type_lvl[k][kv.first] = to_device(typ);
+    c->h_face_off_lvl[k][kv.first] = off;
+    c->h_face_type_lvl[k][kv.first] = typ;
   }
   for (int nb = 0; nb < 6; nb++) {
     c->bc[k].type[nb] = OMG_BC_DIRICHLET;
@@ -2294,6 +2308,8 @@ void free_levels(omg_ctx* c) {
     for (auto& kv : c->d_face_type_lvl[iv]) dfree(kv.second);
     c->d_face_off_lvl[iv].clear();
     c->d_face_type_lvl[iv].clear();
+    c->h_face_off_lvl[iv].clear();
+    c->h_face_type_lvl[iv].clear();
     dfree(c->d_face_data[iv]);
   }
 }
@@ -2925,6 +2941,8 @@ int omg_set_bc_faces(omg_ctx* c, int iv, const long long* face_off, const int* f
     for (auto& kv : c->d_face_type_lvl[k]) dfree(kv.second);
     c->d_face_off_lvl[k].clear();
     c->d_face_type_lvl[k].clear();
+    c->h_face_off_lvl[k].clear();
+    c->h_face_type_lvl[k].clear();
     dfree(c->d_face_data[k]);
     if (!face_off) return;
     // only the faces of my boxes travel to the device, re-packed
@@ -2960,6 +2978,8 @@ int omg_set_bc_faces(omg_ctx* c, int iv, const long long* face_off, const int* f
         }
       c->d_face_off_lvl[k][kv.first] = to_device(off);
       c->d_face_type_lvl[k][kv.first] = to_device(typ);
+      c->h_face_off_lvl[k][kv.first] = off;
+      c->h_face_type_lvl[k][kv.first] = typ;
     }
     c->d_face_data[k] = to_device(packed);
   });

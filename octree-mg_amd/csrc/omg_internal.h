@@ -279,6 +279,10 @@ struct omg_ctx {
   double* d_face_data[omg::kMaxVars] = {};
   std::map<int, long long*> d_face_off_lvl[omg::kMaxVars];
   std::map<int, int*> d_face_type_lvl[omg::kMaxVars];
+  // host copies of the first box's entries (the coarse tail's one-box levels
+  // carry them inline, TailLevel::foff)
+  std::map<int, std::vector<long long>> h_face_off_lvl[omg::kMaxVars];
+  std::map<int, std::vector<int>> h_face_type_lvl[omg::kMaxVars];
   // scalars
   double* d_red = nullptr;             // device reductions (get_sum / subtract_mean)
   hipStream_t stream2 = nullptr;       // side stream (rhs sum chain)

@@ -129,6 +129,9 @@ struct TailLevel {
   int n_par;
   const int* parent_local; // per box: parent's local index at lvl-1
   const int* dixp;         // per box: packed child offset
+  int foff[6];             // bc.face_off / face_type of the level's first box
+  signed char ftype[6];    // (-1: not tabulated, -2: beyond int, read bc.face_off),
+                           // resolved on the host
 };
 struct TailArgs {
   int n_lvls;              // lv[0] = lowest .. lv[n_lvls-1] = top

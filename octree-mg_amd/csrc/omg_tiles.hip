@@ -1713,13 +1713,19 @@ __device__ void tail_boxes_io(const TailArgs& A, int ls, double* tl) {
 // physical face cell (bc_to_gc's argument: the stored value in the rhs ghost
 // when mg_phi_bc_store ran, else the tabulated or constant one); after the
 // rhs ghosts are in LDS
+__device__ __forceinline__ long long tail_foff(const TailArgs& A, int l, int nb) {
+  const int o = A.lv[l].foff[nb - 1];
+  return o == -2 ? A.lv[l].bc.face_off[nb - 1] : (long long)o;
+}
+
 __device__ __forceinline__ void tail_setup_coef(const TailArgs& A, int l, TailLdsLevel& D, int nb) {
   const LevelView& L = A.lv[l].L;
   const GcBC& bc = A.lv[l].bc;
   const bool low = nb & 1;
   int type;
   if (bc.phi_stored) type = L.nba[nb - 1];
-  else if (bc.face_off && bc.face_off[nb - 1] >= 0) type = bc.face_type[nb - 1];
+  else if (A.lv[l].foff[nb - 1] == -2) type = bc.face_type[nb - 1];
+  else if (A.lv[l].foff[nb - 1] >= 0) type = A.lv[l].ftype[nb - 1];
   else type = bc.type[nb - 1];
   double c0, c1, c2;
   if (type == -10) {
@@ -1746,14 +1752,14 @@ __device__ __forceinline__ bool tail_bc_value(const TailArgs& A, int l, const Ta
   const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
   if (bc.phi_stored)
     bv = X.F[d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g)];
-  else if (bc.face_off && bc.face_off[nb - 1] >= 0)
-    bv = bc.face_data[bc.face_off[nb - 1] + (a - 1) + (long long)nc * (c - 1)];
+  else if (A.lv[l].foff[nb - 1] != -1)
+    bv = bc.face_data[tail_foff(A, l, nb) + (a - 1) + (long long)nc * (c - 1)];
   else
     bv = bc.value[nb - 1];
   return true;
 }
 
-__device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailLdsLevel& D) {
+__device__ __forceinline__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailLdsLevel& D) {
   if (threadIdx.x < 6) tail_setup_coef(A, l, D, threadIdx.x + 1);
   for (int p = threadIdx.x; p < 6 * X.nc * X.nc; p += blockDim.x) {
     double bv;
@@ -1761,36 +1767,58 @@ __device__ void tail_lds_setup(const TailArgs& A, int l, const TailBox& X, TailL
   }
 }
 
-// tail_lds_setup of the usual chain (16^3 top over 8^3, 4^3, 2^3) at once:
-// every bc value of the four levels read before the first is stored
-__device__ void tail_setup_chain(const TailArgs& A, int top, const TailBox& XB, double* lds, TailLdsLevel* tll) {
-  constexpr int O8 = 6 * 256, O4 = O8 + 6 * 64, O2 = O4 + 6 * 16, NT = O2 + 6 * 4;
-  constexpr int R = (NT + kTailBS - 1) / kTailBS;
-  if (threadIdx.x < 24) {
-    const int k = threadIdx.x / 6, l = k == 0 ? top : 3 - k;
-    tail_setup_coef(A, l, tll[l], threadIdx.x % 6 + 1);
-  }
+// tail_lds_setup of the usual chain (16^3 top over 8^3, 4^3, 2^3) in two
+// halves around the boxes' load: issue() reads every bc value held in HBM
+// (tabulated faces) while the boxes' loads are in flight, commit() (after
+// they are in LDS) takes the stored ones from the rhs ghosts and writes all
+struct TailChainBc {
+  static constexpr int O8 = 6 * 256, O4 = O8 + 6 * 64, O2 = O4 + 6 * 16, NT = O2 + 6 * 4;
+  static constexpr int R = (NT + kTailBS - 1) / kTailBS;
   double bv[R];
-  double* dst[R];
+  int dst[R], src[R];   // offsets into the LDS array: the bc slot (-1: not a
+                        // physical face), the rhs ghost it is stored in (-1: bv)
+  __device__ __forceinline__ void issue(const TailArgs& A, int top, const TailBox& XB, double* lds,
+                                        TailLdsLevel* tll) {
+    if (threadIdx.x < 24) {
+      const int k = threadIdx.x / 6, l = k == 0 ? top : 3 - k;
+      tail_setup_coef(A, l, tll[l], threadIdx.x % 6 + 1);
+    }
 #pragma unroll
-  for (int r = 0; r < R; r++) {
-    dst[r] = nullptr;
-    const int t = threadIdx.x + kTailBS * r;
-    if (t >= NT) continue;
-    const int l = t < O8 ? top : t < O4 ? 2 : t < O2 ? 1 : 0;
-    const int p = t - (t < O8 ? 0 : t < O4 ? O8 : t < O2 ? O4 : O2);
-    const TailBox X = l == top ? XB : tail_box(A, l, lds);
-    if (tail_bc_value(A, l, X, p, bv[r])) dst[r] = X.B + p;
+    for (int r = 0; r < R; r++) {
+      dst[r] = -1;
+      src[r] = -1;
+      bv[r] = 0.0;
+      const int t = threadIdx.x + kTailBS * r;
+      if (t >= NT) continue;
+      const int l = t < O8 ? top : t < O4 ? 2 : t < O2 ? 1 : 0;
+      const int p = t - (t < O8 ? 0 : t < O4 ? O8 : t < O2 ? O4 : O2);
+      const TailBox X = l == top ? XB : tail_box(A, l, lds);
+      const LevelView& L = A.lv[l].L;
+      const GcBC& bc = A.lv[l].bc;
+      const int nc = X.nc, nc2 = nc * nc;
+      const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
+      if (L.nbk[nb - 1] != NB_PHYS) continue;
+      dst[r] = (int)(X.B - lds) + p;
+      const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
+      if (bc.phi_stored)
+        src[r] = (int)(X.F - lds) + (d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g));
+      else if (A.lv[l].foff[nb - 1] != -1)
+        bv[r] = bc.face_data[tail_foff(A, l, nb) + (a - 1) + (long long)nc * (c - 1)];
+      else
+        bv[r] = bc.value[nb - 1];
+    }
   }
+  __device__ __forceinline__ void commit(double* lds) const {
 #pragma unroll
-  for (int r = 0; r < R; r++)
-    if (dst[r]) *dst[r] = bv[r];
-}
+    for (int r = 0; r < R; r++)
+      if (dst[r] >= 0) lds[dst[r]] = src[r] >= 0 ? lds[src[r]] : bv[r];
+  }
+};
 
 // phi and rhs of the 16^3 top level (interior and face ghosts) HBM <-> LDS;
 // only phi goes back
 template <bool LOAD>
-__device__ void tail_big_io(const LevelView& L, const TailBox& X) {
+__device__ __forceinline__ void tail_big_io(const LevelView& L, const TailBox& X) {
   if (LOAD)
     tail_io_stored<16, 2, true>(L, X.P);
   else
@@ -1803,7 +1831,7 @@ __device__ void tail_big_io(const LevelView& L, const TailBox& X) {
 // HBM as residual_box leaves them) summed as restrict_onto sums them, next to
 // the sum of their phi
 template <int OP>
-__device__ void tail_big_resid_restrict(const TailArgs& A, int li, const TailBox& X, const TailBox& Xc) {
+__device__ __forceinline__ void tail_big_resid_restrict(const TailArgs& A, int li, const TailBox& X, const TailBox& Xc) {
   const LevelView& L = A.lv[li].L;
   const OpCoef<OP> K(L, A.lambda);
   const int dp = A.lv[li].dixp[0];
@@ -1857,7 +1885,7 @@ __device__ __forceinline__ void tail_lds_fill_nc(const TailLdsLevel& D, const Ta
   __syncthreads();
 }
 
-__device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
+__device__ __forceinline__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
   // ghosts are written only from interior cells, so the reads may precede the writes
   if (X.nc == 16) return tail_lds_fill_nc<16>(D, X);
   const int nc = X.nc, nc2 = nc * nc, ln = X.ln;
@@ -1883,27 +1911,36 @@ __device__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
 // the interior, both to HBM (the level's rhs and old after the cycle, and the
 // old its correction of top+1 reads), rhs into LDS for the smoothing; the
 // arithmetic of k_fill_crhs / coarse_rhs_box on the same operands
+// the top level's residuals, read before the fill (their loads in flight
+// with the entry's)
+struct TailCrhsRegs {
+  static constexpr int N3 = 16 * 16 * 16, R = N3 / kTailBS;
+  static_assert(N3 % kTailBS == 0, "whole rounds of interior cells");
+  double rv[R];
+  __device__ __forceinline__ void issue(const LevelView& L) {
+    const double* res = boxp(L, 4, 0);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int q = threadIdx.x + kTailBS * r;
+      rv[r] = res[off_int(L, (q & 15) + 1, ((q >> 4) & 15) + 1, (q >> 8) + 1)];
+    }
+  }
+};
+
 template <int OP>
-__device__ void tail_big_crhs(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X) {
+__device__ __forceinline__ void tail_big_crhs(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
+                                              const TailCrhsRegs& rr) {
   const LevelView& L = A.lv[li].L;
   const OpCoef<OP> K(L, A.lambda);
-  constexpr int N3 = 16 * 16 * 16, R = N3 / kTailBS;
-  static_assert(N3 % kTailBS == 0, "whole rounds of interior cells");
-  const double* res = boxp(L, 4, 0);
+  constexpr int R = TailCrhsRegs::R;
   double* rhs = boxp(L, 2, 0);
-  double rv[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {   // the residual loads overlap the fill
-    const int q = threadIdx.x + kTailBS * r;
-    rv[r] = res[off_int(L, (q & 15) + 1, ((q >> 4) & 15) + 1, (q >> 8) + 1)];
-  }
   tail_lds_fill(D, X);
   tail_io_stored<16, 1, false, 3>(L, X.P);
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const int q = threadIdx.x + kTailBS * r;
     const int i = (q & 15) + 1, j = ((q >> 4) & 15) + 1, k = (q >> 8) + 1, c = X.at(i, j, k);
-    const double v = op_value<OP>(K, tail_nbr(X, X.P, c)) + rv[r];
+    const double v = op_value<OP>(K, tail_nbr(X, X.P, c)) + rr.rv[r];
     X.F[c] = v;
     rhs[off_int(L, i, j, k)] = v;
   }
@@ -1937,7 +1974,7 @@ __device__ __forceinline__ void tail_rb_substep(const OpCoef<OP>& K, const TailB
 // or lexicographic sweeps (hyperplanes i+j+k = d, as gs_lex_box), each
 // followed by the ghost fill
 template <int OP, bool LEX>
-__device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X, int n_cycle) {
+__device__ __forceinline__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X, int n_cycle) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, n3 = nc * nc * nc;
   if constexpr (LEX) {
@@ -1980,7 +2017,7 @@ __device__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D
 // restrict_onto of phi and res into the parent box Xc (sequential 8-cell sum
 // from +0.0, i fastest, times 0.125)
 template <int OP>
-__device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X, const TailBox* Xc,
+__device__ __forceinline__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X, const TailBox* Xc,
                                     double* red) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, n3 = nc * nc * nc;
@@ -2023,7 +2060,7 @@ __device__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X,
 // update_coarse's parent part: rhs = L(phi) + res on the interior, old = phi
 // on the whole stored box
 template <int OP>
-__device__ void tail_lds_coarse_rhs(const TailArgs& A, int li, const TailBox& X) {
+__device__ __forceinline__ void tail_lds_coarse_rhs(const TailArgs& A, int li, const TailBox& X) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, s3 = X.S * X.S * X.S;
   for (int q = threadIdx.x; q < s3; q += blockDim.x) {
@@ -2070,7 +2107,7 @@ __device__ __forceinline__ void tail_correct_nc(const TailArgs& A, int li, const
   __syncthreads();
 }
 
-__device__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
+__device__ __forceinline__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
                                  const TailBox& Xc) {
   if (X.nc == 16 && Xc.S == 10) {   // the 16^3 level, a one-box parent of half the size
     tail_correct_nc<16>(A, li, X, Xc);
@@ -2135,8 +2172,11 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
     tail_coarse_rhs<OP>(A, top, lds);
   }
   if (big) {
+    TailCrhsRegs rr;
+    if (A.top_crhs) rr.issue(A.lv[top].L);
     if (ls == 2 && A.lv[0].L.nc == 2 && A.lv[1].L.nc == 4 && A.lv[2].L.nc == 8) {
-      // the usual chain (16^3 over 8^3, 4^3, 2^3): every load in flight at once
+      // the usual chain (16^3 over 8^3, 4^3, 2^3): every load of the entry
+      // in flight at once
       TailIoRegs<16, 2> r16;
       TailIoRegs<8, 4> r8;
       TailIoRegs<4, 4> r4;
@@ -2145,27 +2185,26 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
       r8.issue(A.lv[2].L);
       r4.issue(A.lv[1].L);
       r2.issue(A.lv[0].L);
+      TailChainBc cb;
+      cb.issue(A, top, XB, lds, tll);
+      stamp();
       r16.commit(XB.P);
       r8.commit(tail_box(A, 2, lds).P);
       r4.commit(tail_box(A, 1, lds).P);
       r2.commit(tail_box(A, 0, lds).P);
       __syncthreads();
       stamp();
+      cb.commit(lds);
     } else {
       tail_big_io<true>(A.lv[top].L, XB);
       tail_boxes_io<true>(A, ls, lds);
       stamp();
-    }
-    stamp();
-    if (ls == 2 && A.lv[0].L.nc == 2 && A.lv[1].L.nc == 4 && A.lv[2].L.nc == 8) {
-      tail_setup_chain(A, top, XB, lds, tll);
-    } else {
       for (int l = 0; l <= ls; l++) tail_lds_setup(A, l, tail_box(A, l, lds), tll[l]);
       tail_lds_setup(A, top, XB, tll[top]);
     }
     __syncthreads();
     stamp();
-    if (A.top_crhs) tail_big_crhs<OP>(A, top, tll[top], XB);
+    if (A.top_crhs) tail_big_crhs<OP>(A, top, tll[top], XB, rr);
     stamp();
     const TailBox Xc = tail_box(A, ls, lds);
     tail_lds_smooth<OP, LEX>(A, top, tll[top], XB, A.n_down);
