@@ -296,3 +296,47 @@ def test_mid_levels_match_oracle(args, cap, monkeypatch):
         _assert_same(dev, orc, ivs=(1, 2, 3, 4))
     c.call("set_profiling", 0)
     assert _mid_launches(dev) > 0, "the mid kernel did not run"
+
+
+# the coarse tail forming its top level's fill and coarse rhs itself (the
+# default) against update_coarse doing it in its own launch
+# (OMG_NO_TAIL_CRHS=1): every stored cell of phi, rhs, old and res after each
+# cycle equals the oracle's either way; the 16^3 top over the 8/4/2 chain
+# (tabulated faces, lexicographic GS with Helmholtz), an LDS-resident top
+# (box 8, periodic) and FMG
+TAIL_CRHS_CASES = ["16 128 128 128 2 v gsrb lpl 0 sol sol 2 lb 0",
+                   "16 64 64 64 2 v gs helm 2 d0 sol 1 lb 0",
+                   "8 64 64 64 2 v gsrb lpl 0 per sol 1 lb 0",
+                   "8 32 32 32 2 f gs lpl 0 n0 sol 1 lb 1"]
+
+
+def _coarse_fill_launches(dev):
+    n = 0
+    for lvl in dev.levels():
+        for fam in ("fill_crhs", "fill_gc", "coarse_rhs"):
+            n += dev.mg.ctx.kernel_stats(f"{fam}@{lvl}")[0]
+    return n
+
+
+@pytest.mark.parametrize("args", TAIL_CRHS_CASES)
+def test_tail_top_coarse_rhs_matches_oracle(args, monkeypatch):
+    launches = {}
+    for switch in ("0", "1"):
+        if switch == "1":
+            monkeypatch.setenv("OMG_NO_TAIL_CRHS", "1")
+        cfg = parse(args)
+        dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+        for be in (dev, orc):
+            setup_problem(be)
+        c = dev.mg.ctx
+        c.call("reset_stats")
+        c.call("set_profiling", 1)
+        for _ in range(2):
+            if cfg["cycle"] == "f":
+                assert dev.fmg(True, True) == orc.fmg(True, True)
+            else:
+                assert dev.vcycle(True) == orc.vcycle(True)
+            _assert_same(dev, orc, ivs=(1, 2, 3, 4))
+        c.call("set_profiling", 0)
+        launches[switch] = _coarse_fill_launches(dev)
+    assert launches["0"] < launches["1"], launches
