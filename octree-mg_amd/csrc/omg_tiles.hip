@@ -1722,20 +1722,20 @@ __device__ __forceinline__ void tail_setup_coef(const TailArgs& A, int l, TailLd
   const LevelView& L = A.lv[l].L;
   const GcBC& bc = A.lv[l].bc;
   const bool low = nb & 1;
-  int type;
-  if (bc.phi_stored) type = L.nba[nb - 1];
-  else if (A.lv[l].foff[nb - 1] == -2) type = bc.face_type[nb - 1];
-  else if (A.lv[l].foff[nb - 1] >= 0) type = A.lv[l].ftype[nb - 1];
-  else type = bc.type[nb - 1];
+  // every read first, then the selection (one round trip, not one per test)
+  const int ps = bc.phi_stored, fo = A.lv[l].foff[nb - 1];
+  const int nba = L.nba[nb - 1], fty = A.lv[l].ftype[nb - 1], typ = bc.type[nb - 1], kind = L.nbk[nb - 1];
+  const double drv = L.dr[(nb - 1) >> 1];
+  const int type = ps ? nba : fo == -2 ? bc.face_type[nb - 1] : fo >= 0 ? fty : typ;
   double c0, c1, c2;
   if (type == -10) {
     c0 = 2; c1 = -1; c2 = 0;
   } else if (type == -11) {
-    c0 = L.dr[(nb - 1) >> 1] * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
+    c0 = drv * (low ? -1.0 : 1.0); c1 = 1; c2 = 0;
   } else {
     c0 = 0; c1 = 2; c2 = -1;
   }
-  D.local[nb - 1] = L.nbk[nb - 1] == NB_LOCAL;
+  D.local[nb - 1] = kind == NB_LOCAL;
   D.c0[nb - 1] = c0;
   D.c1[nb - 1] = c1;
   D.c2[nb - 1] = c2;
@@ -1777,12 +1777,18 @@ struct TailChainBc {
   double bv[R];
   int dst[R], src[R];   // offsets into the LDS array: the bc slot (-1: not a
                         // physical face), the rhs ghost it is stored in (-1: bv)
+  // Every read of the argument block a face cell needs is issued before any
+  // of them is tested (each test would wait for its own round trip), and the
+  // LDS places of the chain's boxes are compile-time (tail_box's layout).
   __device__ __forceinline__ void issue(const TailArgs& A, int top, const TailBox& XB, double* lds,
                                         TailLdsLevel* tll) {
     if (threadIdx.x < 24) {
       const int k = threadIdx.x / 6, l = k == 0 ? top : 3 - k;
       tail_setup_coef(A, l, tll[l], threadIdx.x % 6 + 1);
     }
+    constexpr int P0 = 0, P1 = P0 + 4 * 4 * 4 * 4, P2 = P1 + 4 * 6 * 6 * 6;   // phi of 2^3, 4^3, 8^3
+    constexpr int B0 = kTailLdsDoubles, B1 = B0 + 6 * 4, B2 = B1 + 6 * 16;    // their bc slots
+    const int bt = (int)(XB.B - lds), ft = (int)(XB.F - lds);
 #pragma unroll
     for (int r = 0; r < R; r++) {
       dst[r] = -1;
@@ -1790,22 +1796,29 @@ struct TailChainBc {
       bv[r] = 0.0;
       const int t = threadIdx.x + kTailBS * r;
       if (t >= NT) continue;
-      const int l = t < O8 ? top : t < O4 ? 2 : t < O2 ? 1 : 0;
-      const int p = t - (t < O8 ? 0 : t < O4 ? O8 : t < O2 ? O4 : O2);
-      const TailBox X = l == top ? XB : tail_box(A, l, lds);
-      const LevelView& L = A.lv[l].L;
-      const GcBC& bc = A.lv[l].bc;
-      const int nc = X.nc, nc2 = nc * nc;
-      const int nb = p / nc2 + 1, cell = p % nc2, a = cell % nc + 1, c = cell / nc + 1;
-      if (L.nbk[nb - 1] != NB_PHYS) continue;
-      dst[r] = (int)(X.B - lds) + p;
+      const int q = t < O8 ? 0 : t < O4 ? 1 : t < O2 ? 2 : 3;   // top, 8^3, 4^3, 2^3
+      const int l = q == 0 ? top : 3 - q;
+      const int p = t - (q == 0 ? 0 : q == 1 ? O8 : q == 2 ? O4 : O2);
+      const int ln = 4 - q, nc = 1 << ln, S = nc + 2;
+      const int bofs = q == 0 ? bt : q == 1 ? B2 : q == 2 ? B1 : B0;
+      const int fofs = q == 0 ? ft : (q == 1 ? P2 : q == 2 ? P1 : P0) + S * S * S;
+      const int nb = (p >> (2 * ln)) + 1, cell = p & (nc * nc - 1), a = (cell & (nc - 1)) + 1, c = (cell >> ln) + 1;
+      const TailLevel& T = A.lv[l];
+      const int kind = T.L.nbk[nb - 1];
+      const int ps = T.bc.phi_stored;
+      const int fo = T.foff[nb - 1];
+      const double val = T.bc.value[nb - 1];
+      const double* fd = T.bc.face_data;
+      if (kind != NB_PHYS) continue;
+      dst[r] = bofs + p;
       const int d = (nb + 1) >> 1, g = (nb & 1) ? 0 : nc + 1;
-      if (bc.phi_stored)
-        src[r] = (int)(X.F - lds) + (d == 1 ? X.at(g, a, c) : d == 2 ? X.at(a, g, c) : X.at(a, c, g));
-      else if (A.lv[l].foff[nb - 1] != -1)
-        bv[r] = bc.face_data[tail_foff(A, l, nb) + (a - 1) + (long long)nc * (c - 1)];
-      else
-        bv[r] = bc.value[nb - 1];
+      if (ps) {
+        src[r] = fofs + (d == 1 ? g + S * (a + S * c) : d == 2 ? a + S * (g + S * c) : a + S * (c + S * g));
+      } else if (fo != -1) {
+        bv[r] = fd[(fo == -2 ? T.bc.face_off[nb - 1] : (long long)fo) + (a - 1) + (long long)nc * (c - 1)];
+      } else {
+        bv[r] = val;
+      }
     }
   }
   __device__ __forceinline__ void commit(double* lds) const {
