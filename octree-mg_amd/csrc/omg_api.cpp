@@ -1577,7 +1577,6 @@ void run_tail(omg_ctx* c, int top, bool top_crhs) {
   A.coarse_its = (int*)(c->d_scalar + 1);
   A.gs_lex = c->smoother != OMG_SMOOTHER_GSRB;
   A.top_crhs = top_crhs;
-  A.wave_lds = !c->no_tail_wave;
   tail_lds_plan(c, top, &A.lds_levels, &A.lds_top);
   const bool tail_timing = c->tail_timing;
   if (tail_timing) {
@@ -2705,7 +2704,6 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_tile = env_flag("OMG_NO_FILL_TILE");
     c->no_fill_crhs = env_flag("OMG_NO_FILL_CRHS");
     c->no_tail_crhs = env_flag("OMG_NO_TAIL_CRHS");
-    c->no_tail_wave = !env_flag("OMG_TAIL_WAVE");
     c->no_rbgv = env_flag("OMG_NO_RBGV");
     c->no_graph = !env_flag("OMG_GRAPH");
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");

@@ -298,7 +298,6 @@ struct omg_ctx {
   bool no_fill_tile = false;           // OMG_NO_FILL_TILE: the per-cell ghost fill kernel everywhere
   bool no_fill_crhs = false;           // OMG_NO_FILL_CRHS: update_coarse's fill and coarse rhs as two passes
   bool no_tail_crhs = false;           // OMG_NO_TAIL_CRHS: the tail top's fill + coarse rhs by update_coarse
-  bool no_tail_wave = true;            // !OMG_TAIL_WAVE: the tail's smallest LDS levels on the whole workgroup
   bool no_rbgv = false;                // OMG_NO_RBGV: no stored refinement-boundary coarse parts
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel

@@ -149,9 +149,7 @@ struct TailArgs {
   int lds_levels, lds_top;
   // the tail forms the top level's ghosts and its coarse rhs = L(phi) + res,
   // old = phi itself (update_coarse of top+1 stopped after the restriction)
-  int top_crhs;
-  // the LDS levels below a 16^3 top on one wave (k_coarse_tail, team_sync)
-  int wave_lds;
+  int top_crhs, pad_;
 };
 // how many of the tail's lowest levels qualify for the LDS-resident program
 constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3

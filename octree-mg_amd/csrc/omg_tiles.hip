@@ -1868,26 +1868,6 @@ __device__ __forceinline__ void tail_big_resid_restrict(const TailArgs& A, int l
   __syncthreads();
 }
 
-// The LDS-resident levels below a 16^3 top (at most 8^3 cells) can run on
-// one wave (TailArgs::wave_lds): W = true iterates with stride 64 and orders
-// the phases with a wave-scope barrier instead of a workgroup barrier (LDS
-// accesses of one wave complete in order); the other waves wait at the next
-// workgroup barrier.
-template <bool W>
-__device__ __forceinline__ int team_n() {
-  return W ? 64 : (int)blockDim.x;
-}
-template <bool W>
-__device__ __forceinline__ void team_sync() {
-  if constexpr (W) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  } else {
-    __syncthreads();
-  }
-}
-
 // mg_fill_ghost_cells_lvl of phi for the box in LDS: a periodic face copies
 // the opposite boundary layer (what the owner pushes), a physical face is
 // bc_to_gc's c0*bc + c1*x1 + c2*x2
@@ -1918,13 +1898,11 @@ __device__ __forceinline__ void tail_lds_fill_nc(const TailLdsLevel& D, const Ta
   __syncthreads();
 }
 
-template <bool W = false>
 __device__ __forceinline__ void tail_lds_fill(const TailLdsLevel& D, const TailBox& X) {
   // ghosts are written only from interior cells, so the reads may precede the writes
-  if constexpr (!W)
-    if (X.nc == 16) return tail_lds_fill_nc<16>(D, X);
+  if (X.nc == 16) return tail_lds_fill_nc<16>(D, X);
   const int nc = X.nc, nc2 = nc * nc, ln = X.ln;
-  for (int p = threadIdx.x; p < 6 * nc2; p += team_n<W>()) {
+  for (int p = threadIdx.x; p < 6 * nc2; p += blockDim.x) {
     const int nb = (p >> (2 * ln)) + 1, cell = p & (nc2 - 1), a = (cell & (nc - 1)) + 1, c = (cell >> ln) + 1;
     const bool low = nb & 1;
     const int d = (nb + 1) >> 1, g = low ? 0 : nc + 1, x1 = low ? 1 : nc, x2 = low ? 2 : nc - 1;
@@ -1937,7 +1915,7 @@ __device__ __forceinline__ void tail_lds_fill(const TailLdsLevel& D, const TailB
     }
     X.P[cell_at(g)] = D.c0[nb - 1] * X.B[p] + D.c1[nb - 1] * X.P[cell_at(x1)] + D.c2[nb - 1] * X.P[cell_at(x2)];
   }
-  team_sync<W>();
+  __syncthreads();
 }
 
 
@@ -2008,29 +1986,29 @@ __device__ __forceinline__ void tail_rb_substep(const OpCoef<OP>& K, const TailB
 // smooth_boxes: red-black substeps (colour e = n & 1 for n = 1 .. 2 n_cycle)
 // or lexicographic sweeps (hyperplanes i+j+k = d, as gs_lex_box), each
 // followed by the ghost fill
-template <int OP, bool LEX, bool W = false>
+template <int OP, bool LEX>
 __device__ __forceinline__ void tail_lds_smooth(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X, int n_cycle) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, n3 = nc * nc * nc;
   if constexpr (LEX) {
     for (int n = 1; n <= n_cycle; n++) {
       for (int d = 3; d <= 3 * nc; d++) {
-        for (int p = threadIdx.x; p < nc * nc; p += team_n<W>()) {
+        for (int p = threadIdx.x; p < nc * nc; p += blockDim.x) {
           const int j = (p & (nc - 1)) + 1, k = (p >> X.ln) + 1, i = d - j - k;
           if (i < 1 || i > nc) continue;
           const int c = X.at(i, j, k);
           X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
         }
-        team_sync<W>();
+        __syncthreads();
       }
-      tail_lds_fill<W>(D, X);
+      tail_lds_fill(D, X);
     }
     return;
   }
   const int h = nc / 2;
   for (int n = 1; n <= 2 * n_cycle; n++) {
     const int e = n & 1;
-    if (!W && nc == 16) {   // the box size known at compile time: every read of a
+    if (nc == 16) {   // the box size known at compile time: every read of a
                       // thread's cells issued before its first update
       tail_rb_substep<16, OP>(K, X, e);
       __syncthreads();
@@ -2038,27 +2016,27 @@ __device__ __forceinline__ void tail_lds_smooth(const TailArgs& A, int li, const
       continue;
     }
     // the cells of colour e only: i = 2*ih + 1 + p with (i+j+k) & 1 == e
-    for (int q = threadIdx.x; q < n3 / 2; q += team_n<W>()) {
+    for (int q = threadIdx.x; q < n3 / 2; q += blockDim.x) {
       const int ih = q & (h - 1), row = q >> (X.ln - 1), j = (row & (nc - 1)) + 1, k = (row >> X.ln) + 1;
       const int c = X.at(2 * ih + 1 + ((1 + j + k + e) & 1), j, k);
       X.P[c] = gs_value<OP>(K, tail_nbr(X, X.P, c), X.F[c]);
     }
-    team_sync<W>();
-    tail_lds_fill<W>(D, X);
+    __syncthreads();
+    tail_lds_fill(D, X);
   }
 }
 
 // residual_box (res = rhs - L phi) over the box, max |res| when asked, then
 // restrict_onto of phi and res into the parent box Xc (sequential 8-cell sum
 // from +0.0, i fastest, times 0.125)
-template <int OP, bool W = false>
+template <int OP>
 __device__ __forceinline__ double tail_lds_residual(const TailArgs& A, int li, const TailBox& X, const TailBox* Xc,
                                     double* red) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, n3 = nc * nc * nc;
   double mx = 0.0;
   const int ln = X.ln;
-  for (int q = threadIdx.x; q < n3; q += team_n<W>()) {
+  for (int q = threadIdx.x; q < n3; q += blockDim.x) {
     const int c = X.at((q & (nc - 1)) + 1, ((q >> ln) & (nc - 1)) + 1, (q >> (2 * ln)) + 1);
     const double r = X.F[c] - op_value<OP>(K, tail_nbr(X, X.P, c));
     X.R[c] = r;
@@ -2066,22 +2044,18 @@ __device__ __forceinline__ double tail_lds_residual(const TailArgs& A, int li, c
   }
   if (red) {
     for (int off = 32; off > 0; off >>= 1) mx = amax(mx, __shfl_down(mx, off, 64));
-    if constexpr (W) {
-      mx = __shfl(mx, 0, 64);   // the wave holds every cell
-    } else {
-      __syncthreads();   // every thread has read the previous maximum
-      if (threadIdx.x == 0) *red = 0.0;
-      __syncthreads();
-      if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned long long*>(red),
-                                             (unsigned long long)__double_as_longlong(mx));
-    }
+    __syncthreads();   // every thread has read the previous maximum
+    if (threadIdx.x == 0) *red = 0.0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned long long*>(red),
+                                           (unsigned long long)__double_as_longlong(mx));
   }
-  team_sync<W>();
+  __syncthreads();
   if (Xc) {
     const int dp = A.lv[li].dixp[0];
     const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, hn = nc / 2;
     const int lh = ln - 1;   // log2(hn)
-    for (int t = threadIdx.x; t < 2 * hn * hn * hn; t += team_n<W>()) {
+    for (int t = threadIdx.x; t < 2 * hn * hn * hn; t += blockDim.x) {
       const int pass = t >> (3 * lh), q = t & (hn * hn * hn - 1);
       const int i = (q & (hn - 1)) + 1, j = ((q >> lh) & (hn - 1)) + 1, k = (q >> (2 * lh)) + 1;
       const double* src = pass ? X.R : X.P;
@@ -2091,25 +2065,24 @@ __device__ __forceinline__ double tail_lds_residual(const TailArgs& A, int li, c
           for (int ii = 0; ii < 2; ii++) acc += src[X.at(2 * i - 1 + ii, 2 * j - 1 + jj, 2 * k - 1 + kk)];
       (pass ? Xc->R : Xc->P)[Xc->at(dx + i, dy + j, dz + k)] = 0.125 * acc;
     }
-    team_sync<W>();
+    __syncthreads();
   }
-  if constexpr (W) return red ? mx : 0.0;
   return red ? *red : 0.0;
 }
 
 // update_coarse's parent part: rhs = L(phi) + res on the interior, old = phi
 // on the whole stored box
-template <int OP, bool W = false>
+template <int OP>
 __device__ __forceinline__ void tail_lds_coarse_rhs(const TailArgs& A, int li, const TailBox& X) {
   const OpCoef<OP> K(A.lv[li].L, A.lambda);
   const int nc = X.nc, s3 = X.S * X.S * X.S;
-  for (int q = threadIdx.x; q < s3; q += team_n<W>()) {
+  for (int q = threadIdx.x; q < s3; q += blockDim.x) {
     const int i = q % X.S, j = (q / X.S) % X.S, k = q / (X.S * X.S);
     X.O[q] = X.P[q];
     if (i < 1 || i > nc || j < 1 || j > nc || k < 1 || k > nc) continue;
     X.F[q] = op_value<OP>(K, tail_nbr(X, X.P, q)) + X.R[q];
   }
-  team_sync<W>();
+  __syncthreads();
 }
 
 // correct_children of the parent Xc (res = phi - old over its stored cells)
@@ -2147,21 +2120,20 @@ __device__ __forceinline__ void tail_correct_nc(const TailArgs& A, int li, const
   __syncthreads();
 }
 
-template <bool W = false>
 __device__ __forceinline__ void tail_lds_correct(const TailArgs& A, int li, const TailLdsLevel& D, const TailBox& X,
                                  const TailBox& Xc) {
-  if (!W && X.nc == 16 && Xc.S == 10) {   // the 16^3 level, a one-box parent of half the size
+  if (X.nc == 16 && Xc.S == 10) {   // the 16^3 level, a one-box parent of half the size
     tail_correct_nc<16>(A, li, X, Xc);
-    tail_lds_fill<W>(D, X);
+    tail_lds_fill(D, X);
     return;
   }
   const int sc3 = Xc.S * Xc.S * Xc.S;
-  for (int q = threadIdx.x; q < sc3; q += team_n<W>()) Xc.R[q] = Xc.P[q] - Xc.O[q];
-  team_sync<W>();
+  for (int q = threadIdx.x; q < sc3; q += blockDim.x) Xc.R[q] = Xc.P[q] - Xc.O[q];
+  __syncthreads();
   const int dp = A.lv[li].dixp[0];
   const int dx = dp & 1023, dy = (dp >> 10) & 1023, dz = dp >> 20, nc = X.nc, n3 = nc * nc * nc;
   const int ln = X.ln;
-  for (int q = threadIdx.x; q < n3; q += team_n<W>()) {
+  for (int q = threadIdx.x; q < n3; q += blockDim.x) {
     const int i = (q & (nc - 1)) + 1, j = ((q >> ln) & (nc - 1)) + 1, k = (q >> (2 * ln)) + 1;
     const int c0 = Xc.at(((i + 1) >> 1) + dx, ((j + 1) >> 1) + dy, ((k + 1) >> 1) + dz);
     const double f0 = 0.25 * Xc.R[c0];
@@ -2171,8 +2143,8 @@ __device__ __forceinline__ void tail_lds_correct(const TailArgs& A, int li, cons
     const int c = X.at(i, j, k);
     X.P[c] = X.P[c] + (f0 + fx + fy + fz);
   }
-  team_sync<W>();
-  tail_lds_fill<W>(D, X);
+  __syncthreads();
+  tail_lds_fill(D, X);
 }
 
 template <int OP, bool LEX>
@@ -2257,13 +2229,8 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
     tail_lds_coarse_rhs<OP>(A, ls, Xc);
     stamp();
   }
-  int its = 0;
-  if (big && A.wave_lds) {
-    // the levels 0..wl (4^3 cells and less) on wave 0 (see team_sync); 8^3
-    // measured slower on one wave than on the workgroup
-    int wl = -1;
-    while (wl + 1 < top && A.lv[wl + 1].L.nc <= 4) wl++;
-    for (int li = top - 1; li > wl; li--) {
+  for (int li = big ? top - 1 : top; li >= 1; li--) {
+    if (li <= ls) {
       const TailBox X = tail_box(A, li, lds), Xc = tail_box(A, li - 1, lds);
       tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_down);
       stamp();
@@ -2273,121 +2240,61 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
       stamp();
       tail_lds_coarse_rhs<OP>(A, li - 1, Xc);
       stamp();
+      continue;
     }
-    if (wl < 0) {   // no level small enough: the coarse solve on the workgroup
-      const TailBox X0 = tail_box(A, 0, lds);
-      const double init_res = tail_lds_residual<OP>(A, 0, X0, nullptr, &red);
-      for (int i = 1; i <= A.max_coarse; i++) {
-        tail_lds_smooth<OP, LEX>(A, 0, tll[0], X0, A.n_up + A.n_down);
-        its = i;
-        const double res = tail_lds_residual<OP>(A, 0, X0, nullptr, &red);
-        if (res < A.res_rel * init_res || res < A.res_abs) break;
-      }
+    tail_smooth<OP, LEX>(A, li, A.n_down, lds);
+    stamp();
+    tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
+    stamp();
+    if (li - 1 == ls) {   // the level below goes to LDS now
+      enter_lds();
+      const TailBox Xc = tail_box(A, ls, lds);
+      tail_lds_fill(tll[ls], Xc);
       stamp();
-    } else if (threadIdx.x < 64) {
-      for (int li = wl; li >= 1; li--) {
-        const TailBox X = tail_box(A, li, lds), Xc = tail_box(A, li - 1, lds);
-        tail_lds_smooth<OP, LEX, true>(A, li, tll[li], X, A.n_down);
-        stamp();
-        tail_lds_residual<OP, true>(A, li, X, &Xc, nullptr);
-        stamp();
-        tail_lds_fill<true>(tll[li - 1], Xc);
-        stamp();
-        tail_lds_coarse_rhs<OP, true>(A, li - 1, Xc);
-        stamp();
-      }
-      const TailBox X0 = tail_box(A, 0, lds);
-      const double init_res = tail_lds_residual<OP, true>(A, 0, X0, nullptr, &red);
-      for (int i = 1; i <= A.max_coarse; i++) {
-        tail_lds_smooth<OP, LEX, true>(A, 0, tll[0], X0, A.n_up + A.n_down);
-        its = i;
-        const double res = tail_lds_residual<OP, true>(A, 0, X0, nullptr, &red);
-        if (res < A.res_rel * init_res || res < A.res_abs) break;
-      }
+      tail_lds_coarse_rhs<OP>(A, ls, Xc);
       stamp();
-      for (int li = 1; li <= wl; li++) {
-        const TailBox X = tail_box(A, li, lds), Xc = tail_box(A, li - 1, lds);
-        tail_lds_correct<true>(A, li, tll[li], X, Xc);
-        stamp();
-        tail_lds_smooth<OP, LEX, true>(A, li, tll[li], X, A.n_up);
-        stamp();
-      }
+      continue;
     }
-    __syncthreads();
-    for (int li = wl + 1; li <= top; li++) {
-      const TailBox X = li < top ? tail_box(A, li, lds) : XB, Xc = tail_box(A, li - 1, lds);
+    tail_fill(A, li - 1);
+    stamp();
+    tail_coarse_rhs<OP>(A, li - 1, lds);
+    stamp();
+  }
+  // coarse solve (m_multigrid.f90:197-208)
+  int its = 0;
+  if (ls >= 0) {
+    const TailBox X = tail_box(A, 0, lds);
+    const double init_res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
+    for (int i = 1; i <= A.max_coarse; i++) {
+      tail_lds_smooth<OP, LEX>(A, 0, tll[0], X, A.n_up + A.n_down);
+      its = i;
+      const double res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
+      if (res < A.res_rel * init_res || res < A.res_abs) break;
+    }
+  } else {
+    const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
+    for (int i = 1; i <= A.max_coarse; i++) {
+      tail_smooth<OP, LEX>(A, 0, A.n_up + A.n_down, lds);
+      its = i;
+      const double res = tail_residual<OP>(A, 0, 0, true, lds);
+      if (res < A.res_rel * init_res || res < A.res_abs) break;
+    }
+  }
+  stamp();
+  for (int li = 1; li <= top; li++) {
+    if (li <= ls || big) {
+      const TailBox X = li <= ls ? tail_box(A, li, lds) : XB, Xc = tail_box(A, li - 1, lds);
       tail_lds_correct(A, li, tll[li], X, Xc);
       stamp();
       tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_up);
       stamp();
+      continue;
     }
-  } else {
-    for (int li = big ? top - 1 : top; li >= 1; li--) {
-      if (li <= ls) {
-        const TailBox X = tail_box(A, li, lds), Xc = tail_box(A, li - 1, lds);
-        tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_down);
-        stamp();
-        tail_lds_residual<OP>(A, li, X, &Xc, nullptr);
-        stamp();
-        tail_lds_fill(tll[li - 1], Xc);
-        stamp();
-        tail_lds_coarse_rhs<OP>(A, li - 1, Xc);
-        stamp();
-        continue;
-      }
-      tail_smooth<OP, LEX>(A, li, A.n_down, lds);
-      stamp();
-      tail_residual<OP>(A, li, 1, false, lds);   // update_coarse: residual + restriction of phi, res
-      stamp();
-      if (li - 1 == ls) {   // the level below goes to LDS now
-        enter_lds();
-        const TailBox Xc = tail_box(A, ls, lds);
-        tail_lds_fill(tll[ls], Xc);
-        stamp();
-        tail_lds_coarse_rhs<OP>(A, ls, Xc);
-        stamp();
-        continue;
-      }
-      tail_fill(A, li - 1);
-      stamp();
-      tail_coarse_rhs<OP>(A, li - 1, lds);
-      stamp();
-    }
-    // coarse solve (m_multigrid.f90:197-208)
-    if (ls >= 0) {
-      const TailBox X = tail_box(A, 0, lds);
-      const double init_res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
-      for (int i = 1; i <= A.max_coarse; i++) {
-        tail_lds_smooth<OP, LEX>(A, 0, tll[0], X, A.n_up + A.n_down);
-        its = i;
-        const double res = tail_lds_residual<OP>(A, 0, X, nullptr, &red);
-        if (res < A.res_rel * init_res || res < A.res_abs) break;
-      }
-    } else {
-      const double init_res = tail_residual<OP>(A, 0, 0, true, lds);
-      for (int i = 1; i <= A.max_coarse; i++) {
-        tail_smooth<OP, LEX>(A, 0, A.n_up + A.n_down, lds);
-        its = i;
-        const double res = tail_residual<OP>(A, 0, 0, true, lds);
-        if (res < A.res_rel * init_res || res < A.res_abs) break;
-      }
-    }
+    if (li == ls + 1 && ls >= 0) tail_boxes_io<false>(A, ls, lds);   // the LDS levels back to HBM first
+    tail_correct(A, li, lds);
     stamp();
-    for (int li = 1; li <= top; li++) {
-      if (li <= ls || big) {
-        const TailBox X = li <= ls ? tail_box(A, li, lds) : XB, Xc = tail_box(A, li - 1, lds);
-        tail_lds_correct(A, li, tll[li], X, Xc);
-        stamp();
-        tail_lds_smooth<OP, LEX>(A, li, tll[li], X, A.n_up);
-        stamp();
-        continue;
-      }
-      if (li == ls + 1 && ls >= 0) tail_boxes_io<false>(A, ls, lds);   // the LDS levels back to HBM first
-      tail_correct(A, li, lds);
-      stamp();
-      tail_smooth<OP, LEX>(A, li, A.n_up, lds);
-      stamp();
-    }
+    tail_smooth<OP, LEX>(A, li, A.n_up, lds);
+    stamp();
   }
   if (ls == top || big) tail_boxes_io<false>(A, ls, lds);
   if (big) tail_big_io<false>(A.lv[top].L, XB);
