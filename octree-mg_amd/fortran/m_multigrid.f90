@@ -35,10 +35,16 @@ module m_multigrid
   private
 
   type(c_ptr) :: ctx = c_null_ptr
-  integer     :: ctx_n_boxes = -1
-  integer     :: ctx_n_vars  = -1
-  integer     :: ctx_lowest  = huge(1)
-  integer     :: ctx_highest = -huge(1)
+
+  !> The identity of the tree the device context was built for (tree_key):
+  !> every array omg_tree_setup took, plus the scalars.  A tree rebuilt after
+  !> mg_deallocate_storage (AMRVAC's regrid,
+  !> coupling_amrvac/mod_multigrid_coupling.t:116-130,272-351) or re-balanced
+  !> can keep n_boxes and the level range while its neighbours, children,
+  !> ranks and ids order change; any difference rebuilds the context and
+  !> uploads the host data.
+  integer(c_int), allocatable :: ctx_key(:)
+  real(c_double), allocatable :: ctx_key_dr(:)
 
   !> Resident mode (opt-in, see mg_gpu_set_resident): the data stays on the
   !> GPU between calls instead of round-tripping through mg%boxes(:)%cc.
@@ -54,6 +60,8 @@ module m_multigrid
   integer :: timer_device_fmg    = -1
   integer :: timer_host_to_dev   = -1
   integer :: timer_dev_to_host   = -1
+
+  integer, parameter :: key_head = 9   !< scalars at the head of tree_key
 
   public :: mg_fas_vcycle
   public :: mg_fas_fmg
@@ -306,7 +314,9 @@ contains
 
   subroutine sync_in(mg)
     type(mg_t), intent(inout) :: mg
-    if (resident .and. device_current .and. ctx_n_boxes == mg%n_boxes) return
+    if (resident .and. device_current) then
+       if (same_tree(mg)) return
+    end if
     call to_device(mg)
     device_current = .true.
   end subroutine sync_in
@@ -319,14 +329,92 @@ contains
   ! ------------------------------------------------------------------------
   ! Host <-> device
 
+  !> The tree's identity, laid out as omg_tree_setup takes it: key holds
+  !> [n_boxes, n_vars, lowest_lvl, highest_lvl, first_normal_lvl, box_size,
+  !> n_cpu, my_rank, n_lists, then lvl(n), parent(n), children(8,n),
+  !> neighbors(6,n), ix(3,n), rank(n), box_size_lvl(nlev), list_off(4nlev+1),
+  !> lists], dr holds dr(3,nlev).
+  subroutine tree_key(mg, key, dr)
+    type(mg_t), intent(in)                     :: mg
+    integer(c_int), allocatable, intent(inout) :: key(:)
+    real(c_double), allocatable, intent(inout) :: dr(:)
+    integer                                    :: n, nlev, n_lists, lvl, t, p, o, id
+
+    n = mg%n_boxes
+    nlev = mg%highest_lvl - mg%lowest_lvl + 1
+    n_lists = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       n_lists = n_lists + size(mg%lvls(lvl)%ids) + size(mg%lvls(lvl)%leaves) + &
+            size(mg%lvls(lvl)%parents) + size(mg%lvls(lvl)%ref_bnds)
+    end do
+    if (allocated(key)) deallocate(key)
+    if (allocated(dr)) deallocate(dr)
+    allocate(key(key_head + 20*n + nlev + 4*nlev+1 + max(n_lists, 1)), dr(NDIM*nlev))
+    key(1:key_head) = [n, mg_num_vars + mg%n_extra_vars, mg%lowest_lvl, mg%highest_lvl, &
+         mg%first_normal_lvl, mg%box_size, mg%n_cpu, mg%my_rank, n_lists]
+    o = key_head
+    do id = 1, n
+       key(o + id)              = mg%boxes(id)%lvl
+       key(o + n + id)          = mg%boxes(id)%parent
+       key(o + 2*n + 8*(id-1) + 1 : o + 2*n + 8*id)   = mg%boxes(id)%children
+       key(o + 10*n + 6*(id-1) + 1 : o + 10*n + 6*id) = mg%boxes(id)%neighbors
+       key(o + 16*n + 3*(id-1) + 1 : o + 16*n + 3*id) = mg%boxes(id)%ix
+       key(o + 19*n + id)       = mg%boxes(id)%rank
+    end do
+    o = o + 20*n
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       t = lvl - mg%lowest_lvl
+       key(o + t + 1) = mg%box_size_lvl(lvl)
+       dr(NDIM*t+1 : NDIM*t+NDIM) = mg%dr(:, lvl)
+    end do
+    o = o + nlev
+    ! list_off (4*nlev+1 entries, starting at 0) and the lists after it
+    p = 0
+    key(o + 1) = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       t = lvl - mg%lowest_lvl
+       call put_list(mg%lvls(lvl)%ids, 4*t+2)
+       call put_list(mg%lvls(lvl)%leaves, 4*t+3)
+       call put_list(mg%lvls(lvl)%parents, 4*t+4)
+       call put_list(mg%lvls(lvl)%ref_bnds, 4*t+5)
+    end do
+    if (n_lists == 0) key(o + 4*nlev+1 + 1) = 0
+
+  contains
+
+    subroutine put_list(ids, slot)
+      integer, intent(in) :: ids(:)
+      integer, intent(in) :: slot
+      integer             :: m
+      m = size(ids)
+      if (m > 0) key(o + 4*nlev+1 + p + 1 : o + 4*nlev+1 + p + m) = ids
+      p = p + m
+      key(o + slot) = p
+    end subroutine put_list
+  end subroutine tree_key
+
+  !> Whether the device context was built for this tree (tree_key).
+  logical function same_tree(mg)
+    type(mg_t), intent(in)      :: mg
+    integer(c_int), allocatable :: key(:)
+    real(c_double), allocatable :: dr(:)
+    same_tree = .false.
+    if (.not. c_associated(ctx) .or. .not. allocated(ctx_key)) return
+    call tree_key(mg, key, dr)
+    if (size(key) /= size(ctx_key)) return
+    if (any(key /= ctx_key)) return
+    ! the level spacings, compared bit for bit
+    same_tree = all(transfer(dr, 0_c_int64_t, size(dr)) == &
+         transfer(ctx_key_dr, 0_c_int64_t, size(ctx_key_dr)))
+  end function same_tree
+
   !> Build (or rebuild) the device context for the current tree.
   subroutine attach(mg)
     type(mg_t), intent(inout)    :: mg
     integer(c_int8_t)            :: uid(omg_unique_id_bytes)
-    integer(c_int), allocatable  :: blvl(:), bpar(:), bch(:, :), bnb(:, :)
-    integer(c_int), allocatable  :: bix(:, :), brank(:), bsl(:), off(:), lists(:)
-    real(c_double), allocatable  :: dr(:, :)
-    integer                      :: n, id, lvl, nlev, t, pos, ierr, n_vars
+    integer(c_int), allocatable  :: key(:)
+    real(c_double), allocatable  :: dr(:)
+    integer                      :: n, nlev, o, ierr
 
 #if NDIM != 3
     error stop "octree-mg GPU backend: only NDIM == 3 is supported"
@@ -335,11 +423,10 @@ contains
     if (mg%geometry_type /= mg_cartesian) &
          error stop "octree-mg GPU backend: only Cartesian geometry is supported"
 
-    n_vars = mg_num_vars + mg%n_extra_vars
-    if (c_associated(ctx) .and. ctx_n_boxes == mg%n_boxes .and. &
-         ctx_n_vars == n_vars .and. ctx_lowest == mg%lowest_lvl .and. &
-         ctx_highest == mg%highest_lvl) return
+    if (same_tree(mg)) return
     if (c_associated(ctx)) call omg_ok(omg_ctx_destroy(ctx), "ctx_destroy")
+    ctx = c_null_ptr
+    if (allocated(ctx_key)) deallocate(ctx_key)
 
     uid = 0
     if (mg%n_cpu > 1) then
@@ -349,57 +436,17 @@ contains
     call omg_ok(omg_ctx_create(ctx, -1_c_int, int(mg%my_rank, c_int), &
          int(mg%n_cpu, c_int), uid), "ctx_create")
 
+    call tree_key(mg, key, dr)
     n = mg%n_boxes
-    allocate(blvl(n), bpar(n), bch(2**NDIM, n), bnb(2*NDIM, n), bix(NDIM, n), brank(n))
-    do id = 1, n
-       blvl(id)     = mg%boxes(id)%lvl
-       bpar(id)     = mg%boxes(id)%parent
-       bch(:, id)   = mg%boxes(id)%children
-       bnb(:, id)   = mg%boxes(id)%neighbors
-       bix(:, id)   = mg%boxes(id)%ix
-       brank(id)    = mg%boxes(id)%rank
-    end do
-
     nlev = mg%highest_lvl - mg%lowest_lvl + 1
-    allocate(bsl(nlev), dr(NDIM, nlev), off(4*nlev+1))
-    pos = 0
-    do lvl = mg%lowest_lvl, mg%highest_lvl
-       pos = pos + size(mg%lvls(lvl)%ids) + size(mg%lvls(lvl)%leaves) + &
-            size(mg%lvls(lvl)%parents) + size(mg%lvls(lvl)%ref_bnds)
-    end do
-    allocate(lists(max(pos, 1)))
-    pos = 0
-    off(1) = 0
-    do lvl = mg%lowest_lvl, mg%highest_lvl
-       t = lvl - mg%lowest_lvl
-       bsl(t+1)   = mg%box_size_lvl(lvl)
-       dr(:, t+1) = mg%dr(:, lvl)
-       call put_list(mg%lvls(lvl)%ids, 4*t+2)
-       call put_list(mg%lvls(lvl)%leaves, 4*t+3)
-       call put_list(mg%lvls(lvl)%parents, 4*t+4)
-       call put_list(mg%lvls(lvl)%ref_bnds, 4*t+5)
-    end do
-
-    call omg_ok(omg_tree_setup(ctx, int(n, c_int), blvl, bpar, bch, bnb, bix, brank, &
+    o = key_head
+    call omg_ok(omg_tree_setup(ctx, int(n, c_int), key(o+1:), key(o+n+1:), key(o+2*n+1:), &
+         key(o+10*n+1:), key(o+16*n+1:), key(o+19*n+1:), &
          int(mg%lowest_lvl, c_int), int(mg%highest_lvl, c_int), &
-         int(mg%first_normal_lvl, c_int), int(mg%box_size, c_int), bsl, dr, off, &
-         lists, int(n_vars, c_int)), "tree_setup")
-    ctx_n_boxes = mg%n_boxes
-    ctx_n_vars  = n_vars
-    ctx_lowest  = mg%lowest_lvl
-    ctx_highest = mg%highest_lvl
-
-  contains
-
-    subroutine put_list(ids, slot)
-      integer, intent(in) :: ids(:)
-      integer, intent(in) :: slot
-      integer             :: m
-      m = size(ids)
-      if (m > 0) lists(pos+1:pos+m) = ids
-      pos = pos + m
-      off(slot) = pos
-    end subroutine put_list
+         int(mg%first_normal_lvl, c_int), int(mg%box_size, c_int), key(o+20*n+1:), dr, &
+         key(o+20*n+nlev+1:), key(o+20*n+nlev+4*nlev+1+1:), key(2)), "tree_setup")
+    call move_alloc(key, ctx_key)
+    call move_alloc(dr, ctx_key_dr)
   end subroutine attach
 
   !> Methods, boundary conditions and all data of this rank onto the device.

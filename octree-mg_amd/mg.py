@@ -27,7 +27,7 @@ import numpy as np
 from . import device
 from .tree import (MG_AHELMHOLTZ, MG_VHELMHOLTZ, MG_VLAPLACIAN, MG_BC_DIRICHLET, MG_CARTESIAN, MG_HELMHOLTZ,
                    MG_IPHI, MG_LAPLACIAN, MG_NO_BOX, MG_NUM_VARS,
-                   MG_SMOOTHER_GS, MG_SMOOTHER_GSRB, MGTree)
+                   MG_SMOOTHER_GS, MG_SMOOTHER_GSRB, MGLevel, MGTree)
 
 
 class BC:
@@ -305,6 +305,10 @@ def mg_deallocate_storage(mg: MG):
         raise RuntimeError("deallocate_storage: tree is not allocated")
     mg.ctx.close()
     mg.ctx = None
+    # as src/m_allocate_storage.f90:14-47: the level lists go, the tree is empty
+    for lvl in range(mg.lowest_lvl, mg.highest_lvl + 1):
+        mg.lvls[lvl] = MGLevel()
+    mg.n_boxes = 0
     mg.is_allocated = False
 
 

@@ -31,7 +31,14 @@
 !     lb       lb (mg_load_balance) | lbp (+ mg_load_balance_parents);
 !              a trailing "rb" (lbrb, lbprb) installs a custom refinement_bnd
 !              callback for phi (custom_rb: sides_rb's form with other
-!              coefficients, m_ghost_cells.f90:769-861)
+!              coefficients, m_ghost_cells.f90:769-861); a trailing "mv"
+!              (lbmv, lbpmv) rebuilds the tree after the n_its iterations as
+!              AMRVAC's regrid does (coupling_amrvac/mod_multigrid_coupling.t:
+!              116-130,272-351): mg_deallocate_storage, the same AMR tree with
+!              its refined region moved (+1/4 of the domain in x, -1/4 in y:
+!              same box count, other neighbours, children, ranks and ids
+!              order), load balance, mg_allocate_storage, the problem set up
+!              again and n_its more iterations (a second IT 0.. block)
 !     maxres   0 | 1  (request max_res from mg_fas_vcycle/mg_fas_fmg)
 !     dump     x, or a file: final phi interior of every box (ids order per
 !              level, lowest..highest, i fastest), raw float64; with more
@@ -53,7 +60,8 @@ program omg_golden
   logical             :: periodic(NDIM) = .false.
   real(dp), parameter :: pi = acos(-1.0_dp)
   character(len=64)   :: a_cycle, a_smoother, a_op, a_bc, a_rhs, a_lb, a_dump, arg
-  integer             :: n, ierr, maxres_flag, i_sol, order
+  integer             :: n, ierr, maxres_flag, i_sol, order, n_tree, n_trees
+  real(dp)            :: shift(NDIM) = 0.0_dp
   real(dp)            :: max_res, t0, t1
   real(dp), parameter :: diff_coeff = 0.5_dp, diff_tol = 1.0e-8_dp
   type(mg_t)          :: mg
@@ -135,6 +143,18 @@ program omg_golden
   call mg_set_methods(mg)
   call mg_comm_init(mg)
 
+  n = len_trim(a_lb)
+  n_trees = 1
+  if (n > 2) then
+     if (a_lb(n-1:n) == "mv") n_trees = 2
+  end if
+
+  do n_tree = 1, n_trees
+  if (n_tree == 2) then
+     ! AMRVAC's regrid: free the storage, build the new tree, balance, allocate
+     call mg_deallocate_storage(mg)
+     shift = [0.25_dp, -0.25_dp, 0.0_dp]
+  end if
   if (n_levels <= 1) then
      call mg_build_rectangle(mg, domain_size, box_size, dr, r_min, periodic, 0)
   else
@@ -201,7 +221,8 @@ program omg_golden
      call print_state(mg, n, max_res)
   end do
   t1 = mpi_wtime()
-  if (mg%my_rank == 0) write(*, '(A,ES25.17,A,I0)') "TIME", (t1 - t0) / n_its, " NCPU ", mg%n_cpu
+  if (mg%my_rank == 0) write(*, '(A,ES25.17,A,I0)') "TIME", (t1 - t0) / max(n_its, 1), " NCPU ", mg%n_cpu
+  end do
 
   if (len_trim(a_dump) > 0) then
      if (mg%n_cpu == 1) then
@@ -453,8 +474,8 @@ contains
     do lvl = 1, n_amr_levels-1
        do i = 1, size(mg%lvls(lvl)%ids)
           id = mg%lvls(lvl)%ids(i)
-          r0 = 0.5_dp * domain_len - domain_len * 0.5**(lvl+1)
-          r1 = 0.5_dp * domain_len + domain_len * 0.5**(lvl+1)
+          r0 = (0.5_dp + shift) * domain_len - domain_len * 0.5**(lvl+1)
+          r1 = (0.5_dp + shift) * domain_len + domain_len * 0.5**(lvl+1)
           box_center = mg%boxes(id)%r_min + 0.5_dp * box_size * mg%boxes(id)%dr
           if (all(box_center >= r0 .and. box_center <= r1)) call mg_add_children(mg, id)
        end do

@@ -98,6 +98,15 @@ CONFIGS = {
     # coarse faces of some refinement boundaries arrive from another rank
     "c4_ref2_box16_gsrb_rb": ("16 128 128 128 4 v gsrb lpl 0 sol sol 2 lbrb 0", True, [1, 3]),
     "ref3_gs_rb": ("8 32 32 32 4 v gs lpl 0 sol sol 3 lbrb 0", True, [1, 3]),
+    # a rebuilt tree (lb suffix "mv", omg_golden.f90): n_its iterations, then
+    # mg_deallocate_storage, the AMR tree with its refined region moved (same
+    # box count, other neighbours / children / ranks / ids order),
+    # mg_load_balance (+ _parents), mg_allocate_storage, the problem set up
+    # again and n_its more iterations: AMRVAC's regrid
+    # (coupling_amrvac/mod_multigrid_coupling.t:116-130,272-351)
+    "regrid_ref2_gs": ("8 32 32 32 2 v gs lpl 0 sol sol 2 lbpmv 1", True, [1, 3]),
+    "regrid_ref3_gsrb_d0": ("8 32 32 32 2 v gsrb lpl 0 d0 sol 3 lbmv 1", True, [1, 3]),
+    "regrid_c4_box16_gsrb": ("16 128 128 128 2 v gsrb lpl 0 sol sol 2 lbpmv 0", True, [1, 3]),
     # §8(f) row 1: m_diffusion — one implicit time step per iteration from
     # phi = u (cycle d1 = backward Euler, d2 = Crank-Nicolson; the lambda
     # field is dt; helm: diffusion_solve with D = 0.5, vhelm: _vcoeff)

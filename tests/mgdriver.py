@@ -42,9 +42,19 @@ def parse(args: str) -> dict:
                 n_levels=int(f[11]), lb=f[12], maxres=int(f[13]))
 
 
-def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0):
+def regrids(cfg: dict) -> bool:
+    """omg_golden's lb suffix "mv": after n_its iterations the tree is rebuilt
+    with its refined region moved (AMRVAC's regrid) and n_its more run."""
+    return cfg["lb"].endswith("mv")
+
+
+REGRID_SHIFT = (0.25, -0.25, 0.0)   # omg_golden.f90: the second tree's shift
+
+
+def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0, shift=(0.0, 0.0, 0.0)):
     """The tree set-up of omg_golden (reference tests' mg_build_rectangle or
-    build_amr_tree, tests/test_refinement.f90:191-247, then load balance)."""
+    build_amr_tree, tests/test_refinement.f90:191-247, with the refined region
+    centred at 0.5 + shift, then load balance)."""
     tree.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
     tree.n_cpu, tree.my_rank = n_ranks, my_rank
     dom = np.array(cfg["domain"], dtype=np.int64)
@@ -57,11 +67,12 @@ def build_tree(cfg: dict, tree, n_ranks=1, my_rank=0):
         nl = cfg["n_levels"]
         n_finer = nl * int(np.prod(dom // box)) + 1000
         domain_len = dom * dr
+        ctr = 0.5 + np.asarray(shift, dtype=np.float64)
         tree.build_rectangle(dom, box, dr, [0.0, 0.0, 0.0], periodic, n_finer)
         for lvl in range(1, nl):
             for id_ in tree.lvls[lvl].ids:
-                r0 = 0.5 * domain_len - domain_len * 0.5 ** (lvl + 1)
-                r1 = 0.5 * domain_len + domain_len * 0.5 ** (lvl + 1)
+                r0 = ctr * domain_len - domain_len * 0.5 ** (lvl + 1)
+                r1 = ctr * domain_len + domain_len * 0.5 ** (lvl + 1)
                 center = tree.box_r_min[id_] + 0.5 * box * tree.box_dr[id_]
                 if np.all((center >= r0) & (center <= r1)):
                     tree.add_children(int(id_))
@@ -124,13 +135,14 @@ def diffusion_coeff(cfg):
 
 
 class OracleBackend:
-    def __init__(self, cfg, n_ranks=1):
+    def __init__(self, cfg, n_ranks=1, shift=(0.0, 0.0, 0.0)):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle  # checker only
         self.cfg = cfg
         if cfg["lb"].endswith("rb"):
             raise NotImplementedError("the oracle has no custom refinement_bnd (its goldens pin the drop-in)")
-        self.tree = build_tree(cfg, T.MGTree(), n_ranks)
+        self.n_ranks = n_ranks
+        self.tree = build_tree(cfg, T.MGTree(), n_ranks, shift=shift)
         self.o = pyoracle.Oracle(self.tree, n_vars(cfg), n_ranks)
         op = OPS[cfg["op"]]
         sm = pyoracle.GSRB if cfg["smoother"] == "gsrb" else pyoracle.GS
@@ -146,6 +158,10 @@ class OracleBackend:
 
     def my_ids(self, lvl):
         return self.tree.lvls[lvl].ids
+
+    def regrid(self, shift):
+        """A new oracle over the moved tree (the checker has no storage to free)."""
+        self.__init__(self.cfg, self.n_ranks, shift)
 
     def collective(self, lvl, iv=None):
         return False
@@ -192,7 +208,12 @@ class DeviceBackend:
         mg.smoother_type = T.MG_SMOOTHER_GSRB if cfg["smoother"] == "gsrb" else T.MG_SMOOTHER_GS
         omg.mg_set_methods(mg)
         omg.mg_comm_init(mg, comm)
-        build_tree(cfg, mg, mg.n_cpu, mg.my_rank)
+        self.mg = mg
+        self._build((0.0, 0.0, 0.0))
+
+    def _build(self, shift):
+        cfg, mg = self.cfg, self.mg
+        build_tree(cfg, mg, mg.n_cpu, mg.my_rank, shift)
         omg.mg_set_methods(mg)
 
         def set_bc(iv, nb, t, v):
@@ -210,9 +231,15 @@ class DeviceBackend:
         omg.mg_allocate_storage(mg)
         for iv, (off, typ, data) in faces.items():
             mg.ctx.call("set_bc_faces", iv, off, typ, data, len(data))
-        self.mg = mg
         self.tree = mg
         self.rep_lvl = mg.ctx.replicated_level()
+
+    def regrid(self, shift):
+        """omg_golden's "mv" step on the same mg: mg_deallocate_storage, the
+        moved tree, load balance, mg_allocate_storage."""
+        self.mg.ctx.call("synchronize")
+        omg.mg_deallocate_storage(self.mg)
+        self._build(shift)
 
     def levels(self):
         return range(self.mg.lowest_lvl, self.mg.highest_lvl + 1)
@@ -369,6 +396,17 @@ class StepError(RuntimeError):
 
 
 def _cycles(be, cfg, reduce=None):
+    """The iterations of omg_golden; with "mv" the second tree's set-up and
+    iterations follow (its IT 0.. block appended)."""
+    hist = _tree_cycles(be, cfg, reduce)
+    if regrids(cfg):
+        be.regrid(REGRID_SHIFT)
+        setup_problem(be)
+        hist += _tree_cycles(be, cfg, reduce)
+    return hist
+
+
+def _tree_cycles(be, cfg, reduce=None):
     hist = []
 
     def record(it, mres):

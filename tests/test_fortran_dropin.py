@@ -98,7 +98,7 @@ def test_reference_programs_unchanged(name):
 RESIDENT = os.path.join(BUILD, "omg_golden_gpu_resident")
 RESIDENT_CASES = ["c1_gsrb_f_maxres", "per32_gsrb_v", "helm32_gs_c0", "ref3_gsrb_v", "vlpl32_gsrb_v",
                   "u32_gs_d0_one", "diff_helm_d2_d0", "diff_helm_d1_ref2", "diff_vhelm_d1_per",
-                  "c4_ref2_box16_gsrb"]
+                  "c4_ref2_box16_gsrb", "regrid_ref2_gs", "regrid_c4_box16_gsrb"]
 
 
 @pytest.mark.gpu
