@@ -657,19 +657,19 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
                       !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
-    // the compacted-plane kernel reads rhs from its plane-order copy, rebuilt
+    // the register-ring kernel reads rhs from its ring-order copy, rebuilt
     // here when a write since the last build dropped it (update_coarse for
     // the levels below the top, every entry point that may change rhs)
-    const bool plane = n_sub >= 1 && L->d_rhs_lex && gs_lex_plane_ok(L->nc, c->op);
-    if (plane && !L->rhs_lex_ok) {
+    const bool ring = n_sub >= 1 && L->d_rhs_lex && gs_lex_ring_ok(L->nc, c->op);
+    if (ring && !L->rhs_lex_ok) {
       Prof p(c, "rhs_lex", (double)L->n * L->nc * L->nc * L->nc, lvl);
-      launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream, !c->gs_lex_plane);
+      launch_rhs_lex(L->view(), L->d_rhs_lex, c->stream);
       L->rhs_lex_ok = true;
     }
     // the register ring also writes the boxes' new x boundary layers, so the
     // fill after each sweep stages 12 KB per box instead of 32 (no
     // refinement boundaries on the level; OMG_NO_FILL_XL: the plain fill)
-    const bool xlf = plane && !c->gs_lex_plane && L->d_xlay && !L->has_rb && !c->no_fill_tile && !c->no_fill_xl;
+    const bool xlf = ring && L->d_xlay && !L->has_rb && !c->no_fill_tile && !c->no_fill_xl;
     // Round 4: an even number of ring sweeps on a level whose faces are
     // same-GPU or physical runs with no fill in between: sweep n reads the
     // ghost set sweep n-1 pushed into (the box storage's own faces for odd
@@ -679,6 +679,9 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // form (k_phys_gc).  The reference fills after every sweep
     // (m_multigrid.f90:412-423): the same values reach the same ghosts
     // before every read.  OMG_NO_GS_DBL: the fill after every sweep.
+    // (d_galt exists only where no fill of this level exchanges anything:
+    // no remote faces, no refinement-boundary faces, and no coarse faces
+    // this rank owes another rank's refinement boundaries, ensure_rhs_lex.)
     if (xlf && L->d_galt && n_sub % 2 == 0 && L->n && !c->no_gs_dbl) {
       const GcBC bc = bc_for(c, lvl, 1);
       double* prim = L->d_phi + 2 * (long long)L->view().hv;
@@ -691,7 +694,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
         gs.out_stride = odd ? 6 * (long long)stored_face(L->nc) : L->stride;
         gs.phys_load = n > 1;
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, L->d_rhs_lex, true, nullptr, &gs, &bc);
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, L->d_rhs_lex, nullptr, &gs, &bc);
       }
       if (L->n_physbox) {
         Prof p(c, "fill_gc", (double)L->n_physbox * 6 * L->nc * L->nc, lvl);
@@ -703,7 +706,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
         Prof p(c, "smoother_gs", (double)L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, plane ? L->d_rhs_lex : nullptr, !c->gs_lex_plane,
+        launch_gs_lex(L->view(), c->op, c->lambda, c->stream, ring ? L->d_rhs_lex : nullptr,
                       xlf ? L->d_xlay : nullptr);
       }
       if (xlf) {
@@ -736,10 +739,12 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       // stream while the interior boxes run (the substep reads only its own
       // box's ghost faces, and an interior box has no remote one; the unpack
       // writes remote faces only)
+      const int gvm = L->d_rbgv ? (L->rbgv_ok ? 2 : 1) : 0;
+      if (gvm) L->rbgv_ok = true;
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_bnd * L->nc * L->nc * L->nc, lvl);
         launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
-                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_bnd, L->n_bnd);
+                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_bnd, L->n_bnd, L->d_rbgv, gvm);
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
       // the interior boxes are queued before the exchange is issued: the
@@ -748,7 +753,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       {
         Prof p(c, "smoother_gsrb", 0.5 * L->n_int * L->nc * L->nc * L->nc, lvl);
         launch_gs_substep(L->sweep_view(), c->op, c->lambda, e, 1 << e, view_of(c, lvl - 1), L->d_rb, L->has_rb,
-                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int);
+                          bc_for(c, lvl, 1), L->d_sendbuf, shift, c->stream, L->d_int, L->n_int, L->d_rbgv, gvm);
       }
       HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
       exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, c->stream_comm, lvl);
@@ -790,7 +795,6 @@ void residual_lvl(omg_ctx* c, int lvl, unsigned long long* maxbits) {
     launch_residual(L->view(), c->op, c->lambda, maxbits, c->stream);
 }
 
-void check_mid_err(omg_ctx* c);
 // max over levels lo..hi of max_residual_lvl (m_multigrid.f90:296-311), this
 // rank only: the levels' maxima fold into one word on the device, read back
 // with one synchronisation
@@ -807,7 +811,6 @@ double max_residual_levels(omg_ctx* c, int lo, int hi) {
     return 0.0;
   }
   host_sync(c, c->stream);
-  check_mid_err(c);
   return c->h_scalar[0];
 }
 
@@ -882,14 +885,14 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
          c->n_cycle_down >= 1 &&
          (c->op == OP_LPL || c->op == OP_HELM) && (F->nc == 16 || F->nc == 8) &&
          !(c->no_fuse_down_bc && (F->has_rb || F->has_phys)) && (!F->has_remote || F->n_int) &&
-         // Physical / refinement-boundary faces fuse on one GPU only, decided
-         // alike on every rank.  On a split level the boxes with a remote face
-         // run the plain substep first, whose epilogue rewrites both colour
-         // halves of their physical ghosts, and the fused interior boxes' edge
-         // taps would then read colour-1 ghosts one substep too new; across
-         // ranks, refinement boundaries also exchange coarse faces after every
-         // substep.
-         !(c->n_ranks > 1 && (F->any_phys || F->any_rb));
+         // Refinement-boundary faces whose coarse box is on another rank
+         // exchange coarse faces after every substep (finish_rb); the fused
+         // kernel forms those ghosts from the coarse box itself.  Decided
+         // alike on every rank (any_rbx: the global tree).  Physical and
+         // same-GPU refinement-boundary faces fuse on split levels too
+         // (update_coarse: the boundary boxes' substep leaves the colour-1
+         // halves of those ghosts for the fused boxes' edge taps).
+         !F->any_rbx;
 }
 
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down
@@ -906,6 +909,12 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
     else materialize_level(c, Cl);
   }
   if (F && F->n && tiled_level(c, F)) {
+    // The stored refinement-boundary coarse parts of lvl (d_rbgv) were formed
+    // from lvl-1 as it stands until the restriction below writes it, which is
+    // what the fused down-substep's ghosts need; read the flag before
+    // phi_dirty drops it.  (The coarse boxes across those faces are leaves:
+    // the restriction never writes them.)
+    const bool rbgv = F->rbgv_ok;
     // residual + restriction of phi and res in one pass (omg_tiles.hip)
     phi_dirty(c, lvl - 1);
     if (fused && F->has_remote) {
@@ -915,16 +924,25 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
       // face edges, and some of those faces are remote: the unpack therefore
       // writes the colour-0 halves only (the colour this substep changed;
       // colour 1 is consistent since the previous substep's exchange).
+      // Physical and refinement-boundary ghosts: a fused box's edge tap reads
+      // its neighbour's colour-1 ghost on the neighbour's side face as it
+      // stood before this substep, so the boundary boxes' substep writes only
+      // the colour-0 halves of those ghosts (colours bit 2), and k_face_gc
+      // forms them whole once the fused launch is done, before the boundary
+      // boxes' residual reads them.
+      const bool faces = F->any_phys || F->any_rb;
       {
         Prof p(c, "smoother_gsrb", 0.5 * F->n_bnd * F->nc * F->nc * F->nc, lvl);
-        launch_gs_substep(F->view(), c->op, c->lambda, 0, 1, view_of(c, lvl - 1), F->d_rb, F->has_rb,
-                          bc_for(c, lvl, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd);
+        launch_gs_substep(F->view(), c->op, c->lambda, 0, faces ? 1 | 4 : 1, view_of(c, lvl - 1), F->d_rb,
+                          F->has_rb, bc_for(c, lvl, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd,
+                          rbgv ? F->d_rbgv : nullptr, rbgv ? 2 : 0);
       }
       HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
       {   // (queued before the exchange is issued, as in smooth_boxes)
         Prof p(c, "smooth_resid", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
         if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
-                                 F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb, F->has_phys))
+                                 F->d_dix, c->stream, F->d_int, F->n_int, bc_for(c, lvl, 1), F->has_rb, F->has_phys,
+                                 rbgv ? F->d_rbgv : nullptr))
           throw OmgError("smooth_resid: not available for this level");
       }
       HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
@@ -932,6 +950,10 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
       launch_unpack_faces(F->view(), 1, F->halo.d_recv_items, F->halo.n_recv, F->d_recvbuf, c->stream_comm, 1);
       HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+      if (faces && F->n_bndface) {
+        Prof p(c, "face_gc", (double)F->n_bndface * 6 * F->nc * F->nc, lvl);
+        launch_face_gc(F->view(), view_of(c, lvl - 1), bc_for(c, lvl, 1), F->d_bndface, F->n_bndface, c->stream);
+      }
       {
         Prof p(c, "resid_restrict", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl);
         launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
@@ -941,7 +963,7 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
                                F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb, F->has_phys,
-                               F->rbgv_ok ? F->d_rbgv : nullptr))
+                               rbgv ? F->d_rbgv : nullptr))
         throw OmgError("smooth_resid: not available for this level");
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
@@ -999,9 +1021,10 @@ void correct_children(omg_ctx* c, int lvl) {
 bool prolong_smooth(omg_ctx* c, int lvl) {
   Level* F = level_ptr(c, lvl + 1);
   Level* C = level_ptr(c, lvl);
-  // refinement-boundary faces: on one GPU, formed on the device (no host
-  // refinement_bnd for phi), 16^3 / 8^3 boxes
-  const bool rb_ok = F && !c->no_rb_fill_fuse && c->n_ranks == 1 && (F->nc == 16 || F->nc == 8) &&
+  // refinement-boundary faces: their coarse boxes on this GPU (decided alike
+  // on every rank: any_rbx), formed on the device (no host refinement_bnd
+  // for phi), 16^3 / 8^3 boxes
+  const bool rb_ok = F && !c->no_rb_fill_fuse && !F->any_rbx && (F->nc == 16 || F->nc == 8) &&
                      !(F->rbh.count(1) && F->rbh.at(1).n);
   if (c->no_fuse_up || !F || !C || !F->prolong_smooth_ok || c->smoother != OMG_SMOOTHER_GSRB ||
       (c->op != OP_LPL && c->op != OP_HELM) ||
@@ -1031,9 +1054,13 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
     }
     finish_halo(c, F, 1);
     {
+      // (the boundary boxes' refinement-boundary coarse parts are stored here,
+      // the interior boxes' by k_prolong_smooth: the level's whole buffer is
+      // current after this)
       Prof p(c, "smoother_gsrb", 0.5 * F->n_bnd * F->nc * F->nc * F->nc, lvl + 1);
       launch_gs_substep(F->view(), c->op, c->lambda, 1, 1 << 1, view_of(c, lvl), F->d_rb, F->has_rb,
-                        bc_for(c, lvl + 1, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd);
+                        bc_for(c, lvl + 1, 1), F->d_sendbuf, nullptr, c->stream, F->d_bnd, F->n_bnd,
+                        F->has_rb ? F->d_rbgv : nullptr, F->has_rb && F->d_rbgv ? 1 : 0);
     }
     finish_halo(c, F, 1);
   }
@@ -1227,26 +1254,26 @@ void materialize_phi(omg_ctx* c) {
   for (auto& kv : c->levels) materialize_level(c, &kv.second);
   c->phi_shift_pending = false;
 }
-// the plane-order rhs copies: every write of a level's rhs drops its copy
+// the ring-order rhs copies: every write of a level's rhs drops its copy
 void drop_rhs_lex(omg_ctx* c) {
   for (auto& kv : c->levels) kv.second.rhs_lex_ok = false;
 }
-// plane-order rhs buffers for the levels the compacted-plane lexicographic
+// ring-order rhs buffers for the levels the register-ring lexicographic
 // kernel serves (allocated outside any graph capture: tree setup, smoother
 // choice): 16^3 levels large enough that the sweep is bandwidth-bound; on
-// small levels the per-cycle copy costs more than it saves (C1: 0.255 ->
-// 0.293 ms with it on its 8^3 levels, profiles/r03/v7_README.txt)
-constexpr int kGsPlaneMinBoxes = 2048;
+// smaller levels the per-cycle copies cost more than they save (rings on
+// levels of >= 512 or >= 64 boxes: 0.2-2 % slower, profiles/r03/s16,
+// r04/s10_gs_ring_min_ab.txt)
+constexpr int kGsRingMinBoxes = 2048;
 // Called whenever the smoother or the operator changes (never inside a
 // capture): the buffers exist exactly on the levels the current methods use
 // them on, and are freed otherwise (a 512^3 level's are ~1.1 GiB).
 void ensure_rhs_lex(omg_ctx* c) {
   if (c->host_only) return;
   const bool want = c->smoother != OMG_SMOOTHER_GSRB && !c->no_gs_plane;
-  static const int min_boxes = getenv("OMG_GS_RING_MIN") ? atoi(getenv("OMG_GS_RING_MIN")) : kGsPlaneMinBoxes;
   for (auto& kv : c->levels) {
     Level& L = kv.second;
-    if (!want || L.n < min_boxes || !gs_lex_plane_ok(L.nc, c->op)) {
+    if (!want || L.n < kGsRingMinBoxes || !gs_lex_ring_ok(L.nc, c->op)) {
       if (L.d_rhs_lex || L.d_xlay) HIPCHK(hipStreamSynchronize(c->stream));   // (in use by queued sweeps)
       dfree(L.d_rhs_lex);
       dfree(L.d_xlay);
@@ -1257,7 +1284,12 @@ void ensure_rhs_lex(omg_ctx* c) {
     if (L.d_rhs_lex) continue;
     dmalloc(&L.d_rhs_lex, sizeof(double) * L.n * L.nc * L.nc * L.nc);
     dmalloc(&L.d_xlay, sizeof(double) * L.n * 2 * L.nc * L.nc);
-    if (!L.has_remote && !L.has_rb) dmalloc(&L.d_galt, sizeof(double) * L.n * 6 * (size_t)stored_face(L.nc));
+    // the two-ghost-set chains skip the fills between sweeps, so only where
+    // those fills exchange nothing: no remote or refinement-boundary faces,
+    // and no coarse faces owed to another rank's refinement boundaries
+    // (rbx.n_send: their fill_gc_lvl calls finish_rb after every sweep)
+    if (!L.has_remote && !L.has_rb && L.rbx.n_send == 0 && L.rbx.n_recv == 0)
+      dmalloc(&L.d_galt, sizeof(double) * L.n * 6 * (size_t)stored_face(L.nc));
     L.rhs_lex_ok = false;
   }
 }
@@ -1372,138 +1404,6 @@ int tail_top(omg_ctx* c, int max_lvl) {
     top = l;
   }
   return top;
-}
-
-// ---------------------------------------------------------------------------
-// The mid levels (MidArgs in omg_kernels.h): the levels top+1 .. mid_top right
-// above the coarse tail, each of at most kMidMaxBoxes boxes of 16^3 / 8^3,
-// all on this GPU, run as one launch for their down-steps and one for their
-// up-steps, P workgroups on one XCD with a barrier between steps.  Each
-// launch-per-step of the level-by-level path costs 4.5-6.5 us on MI355X even
-// for an empty kernel (profiles/r04); a barrier among the workgroups of one
-// XCD costs ~1 us.
-
-// the mid kernel's device words and argument blocks (once per context)
-void mid_alloc(omg_ctx* c) {
-  if (c->d_mid_sync) return;
-  dmalloc(&c->d_mid_sync, sizeof(unsigned long long) * 16 * (kMidMaxBoxes + 4), true);
-  dmalloc(&c->d_mid_err, sizeof(int), true);
-  for (int k = 0; k < 2; k++) {
-    dmalloc(&c->d_mid[k], sizeof(MidArgs));
-    c->h_mid[k] = new MidArgs;
-    std::memset(c->h_mid[k], 0xff, sizeof(MidArgs));
-  }
-}
-
-// The highest level of the run top+1 .. that qualifies (INT_MIN: none), for a
-// cycle whose highest level is max_lvl (mid levels lie strictly below it)
-int mid_top(omg_ctx* c, int top, int max_lvl) {
-  // (loopback: several contexts share the GPU, and two mid kernels waiting
-  // for their groups could hold each other's workgroup slots)
-  if (c->no_mid || c->capturing || (c->op != OP_LPL && c->op != OP_HELM) || c->loop) return INT_MIN;
-  const Level* T = level_ptr(c, top);
-  if (!T || (T->nc != 16 && T->nc != 8)) return INT_MIN;
-  int m = INT_MIN;
-  for (int l = top + 1; l < max_lvl && l - top + 1 <= kMidMaxLevels; l++) {
-    const Level* L = level_ptr(c, l);
-    const Level* C = level_ptr(c, l - 1);
-    if (!L || L->n < 1 || L->n > c->mid_max_boxes || L->n != (int)c->ids[l].size() || (L->nc != 16 && L->nc != 8) ||
-        L->has_rb || L->has_remote || L->n_pairs != L->n ||
-        !((size_t)L->n == 8 * C->parents.size() || C->nc * 2 == L->nc) || (int)C->parents.size() > c->mid_max_boxes)
-      break;
-    m = l;
-  }
-  if (m == INT_MIN || !level_ptr(c, m)->phi_gc_ok) return INT_MIN;
-  mid_alloc(c);
-  return m;
-}
-
-// down: the down-steps of mid_top .. top+1 (smoothing, residual +
-// restriction, fill and coarse rhs of the level below, as update_coarse);
-// up: the up-steps of top+1 .. mid_top (correction + fill, smoothing)
-void run_mid(omg_ctx* c, int top, int mtop, bool down) {
-  MidArgs A;
-  std::memset(&A, 0, sizeof(A));   // padding too: compared bytewise below
-  A.n_lvls = mtop - top + 1;
-  A.lambda = c->lambda;
-  A.sync = c->d_mid_sync;
-  A.err = c->d_mid_err;
-  int P = 1;
-  for (int l = top; l <= mtop; l++) {
-    Level* L = level_ptr(c, l);
-    MidLevel& M = A.lv[l - top];
-    M.L = L->view();
-    M.bc = bc_for(c, l, 1);
-    M.parents = L->d_parents;
-    M.n_par = (int)L->parents.size();
-    M.parent_local = L->d_parent_local;
-    M.dixp = L->d_dix;
-    if (l > top) P = std::max(P, L->n);
-    P = std::max(P, M.n_par);
-  }
-  A.P = P;
-  const bool lex = c->smoother != OMG_SMOOTHER_GSRB;
-  auto step = [&](int kind, int l, int e = 0, int colours = 0) {
-    if (A.n_steps >= kMidMaxSteps) throw OmgError("internal: too many mid-level steps");
-    A.st[A.n_steps++] = MidStep{(short)kind, (short)(l - top), (short)e, (short)colours};
-  };
-  auto smooth = [&](int l, int n_cycle) {
-    if (lex) {
-      for (int n = 1; n <= n_cycle; n++) {
-        step(MS_LEX, l);
-        step(MS_FILL, l);
-      }
-    } else {
-      for (int n = 1; n <= 2 * n_cycle; n++) step(MS_SUB, l, n & 1, 1 << (n & 1));
-    }
-  };
-  if (down) {
-    for (int l = mtop; l > top; l--) {
-      Level* L = level_ptr(c, l);
-      if (L->shift_pending) materialize_level(c, L);
-      smooth(l, c->n_cycle_down);
-      Level* C = level_ptr(c, l - 1);
-      C->rhs_lex_ok = false;
-      if (C->shift_pending) {   // overwritten by the restriction where every box is a parent
-        if (C->all_parents) C->shift_pending = false;
-        else materialize_level(c, C);
-      }
-      step(MS_RESID, l);
-      step(MS_FILL, l - 1);
-      if (!C->parents.empty()) step(MS_CRHS, l - 1);
-      phi_dirty(c, l - 1);
-      C->phi_gc_ok = true;
-    }
-  } else {
-    for (int l = top + 1; l <= mtop; l++) {
-      Level* L = level_ptr(c, l);
-      if (L->shift_pending) materialize_level(c, L);
-      step(MS_PFILL, l, 0, !lex && c->n_cycle_up >= 1 && !c->no_skip1);
-      smooth(l, c->n_cycle_up);
-      L->phi_gc_ok = true;
-    }
-    rb_stale_above(c, mtop);
-  }
-  const int k = down ? 0 : 1;
-  if (std::memcmp(&A, c->h_mid[k], sizeof(MidArgs)) != 0) {
-    *c->h_mid[k] = A;
-    launch_store_mid(A, c->d_mid[k], c->stream);
-  }
-  Prof p(c, down ? "mid_down" : "mid_up", 0.0, mtop);
-  launch_mid(c->d_mid[k], P, lex, c->op, ++c->mid_seq, c->stream);
-}
-
-// A failure of the mid kernel (sticky flag) raised at the next host wait
-void check_mid_err(omg_ctx* c) {
-  if (!c->d_mid_err) return;
-  int e = 0;
-  HIPCHK(hipMemcpy(&e, c->d_mid_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (e) {
-    c->no_mid = true;
-    HIPCHK(hipMemset(c->d_mid_err, 0, sizeof(int)));
-    throw OmgError(std::string("mid-level kernel failed (a wait timed out") +
-                   "): results of the last cycles are invalid; mid levels now launch by launch");
-  }
 }
 
 // Levels lowest..top of the V-cycle (down-smoothing of top .. up-smoothing of
@@ -1642,11 +1542,12 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     // tree.  (Agreeing over the transport instead, as round 3 did, cost a
     // host synchronisation per cycle.)  OMG_CHECK_COLLECTIVE checks it.
     // A level with refinement boundaries is consistent as long as the level
-    // below was not written since its last fill (rb_stale_above).  Those
-    // writes depend on per-rank state (pending mean shifts), so with more
-    // than one rank such a level is always refilled.
+    // below was not written since its last fill (rb_stale_above).  With a
+    // subtracted mean those writes depend on per-rank state (pending mean
+    // shifts, materialised where a rank has boxes), so with more than one
+    // rank such a level is then always refilled.
     Level* L = level_ptr(c, max_lvl);
-    const bool need = !(L && L->phi_gc_ok && (!L->any_rb || c->n_ranks == 1));
+    const bool need = !(L && L->phi_gc_ok && (!L->any_rb || c->n_ranks == 1 || !c->subtract_mean));
     if (c->n_ranks > 1 && c->check_collective && (allreduce(c, need ? 1.0 : 0.0, true) > 0.5) != need)
       throw OmgError("mg_fas_vcycle: the stand-alone fill decision differs across ranks "
                      "(an upload of phi was not made on every rank)");
@@ -1657,14 +1558,9 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   }
   const int top = tail_top(c, max_lvl);
   const bool tail = top >= min_lvl && !c->no_tail;
-  const int mtop = tail ? mid_top(c, top, max_lvl) : INT_MIN;
-  const bool tail_crhs = tail && mtop == INT_MIN && max_lvl > top && tail_crhs_ok(c, top);
+  const bool tail_crhs = tail && max_lvl > top && tail_crhs_ok(c, top);
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
-    if (mtop != INT_MIN && l == mtop) {   // mtop .. top+1 in one launch
-      run_mid(c, top, mtop, true);
-      break;
-    }
     const bool fused = smooth_resid_ok(c, l);
     smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
     update_coarse(c, l, fused, tail_crhs && l == top + 1);
@@ -1692,10 +1588,6 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
   }
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
-    if (mtop != INT_MIN && l <= mtop) {   // top+1 .. mtop in one launch
-      if (l == top + 1) run_mid(c, top, mtop, false);
-      continue;
-    }
     if (prolong_smooth(c, l - 1)) {
       smooth_boxes(c, l, c->n_cycle_up, 2);
     } else {
@@ -2296,7 +2188,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_xlay);
     dfree(L.d_galt);
     dfree(L.d_physbox);
-    dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0);
+    dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0); dfree(L.d_bndface);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
@@ -2469,8 +2361,9 @@ void build_plan(omg_ctx* c) {
     L.has_rb = !L.h_rb.empty() || L.rbx.n_recv > 0;
     L.has_remote = L.halo.n_send || L.halo.n_recv;
     L.has_phys = std::any_of(L.h_nbk.begin(), L.h_nbk.end(), [](int8_t k) { return k == NB_PHYS; });
-    // (one GPU, tiled box sizes: the red-black smoother's coarse-part buffer)
-    if (!L.h_rb.empty() && c->n_ranks == 1 && !c->host_only && !c->no_rbgv &&
+    // (tiled box sizes: the red-black smoother's coarse-part buffer, for the
+    // faces whose coarse box is on this GPU)
+    if (!L.h_rb.empty() && !c->host_only && !c->no_rbgv &&
         (L.nc == 16 || L.nc == 8 || L.nc == 4 || L.nc == 2))
       dmalloc(&L.d_rbgv, sizeof(double) * L.n * 6 * L.nc * L.nc);
     L.rbgv_ok = false;
@@ -2485,12 +2378,17 @@ void build_plan(omg_ctx* c) {
       L.n_physbox = (int)pb.size();
       L.d_physbox = to_device(pb);
     }
-    L.any_rb = L.any_phys = false;
+    L.any_rb = L.any_phys = L.any_rbx = false;
     for (int id : c->ids[l])
       for (int nb = 1; nb <= 6; nb++) {
         const int nid = T.nbr(id, nb);
         L.any_rb |= nid == 0;
         L.any_phys |= nid < 0;
+        if (nid == 0) {   // the coarse box across: the parent's neighbour
+          const int p_id = c->parent[id - 1];
+          const int p_nb = p_id > 0 ? T.nbr(p_id, nb) : 0;
+          L.any_rbx |= p_nb > 0 && !(l - 1 <= c->rep_lvl) && c->rank_of[p_nb - 1] != c->rank_of[id - 1];
+        }
       }
     {
       // boxes with a face toward another GPU (halo overlap in smooth_boxes)
@@ -2511,6 +2409,15 @@ void build_plan(omg_ctx* c) {
           for (int nb = 0; nb < 6; nb++)
             if (L.h_nbk[(size_t)b * 6 + nb] == NB_LOCAL && isb[L.h_nba[(size_t)b * 6 + nb]]) push0[b] |= 1u << nb;
         L.d_push0 = to_device(push0);
+        std::vector<int> bf;
+        for (int b : bnd)
+          for (int nb = 0; nb < 6; nb++)
+            if (L.h_nbk[(size_t)b * 6 + nb] == NB_PHYS || L.h_nbk[(size_t)b * 6 + nb] == NB_RB) {
+              bf.push_back(b);
+              break;
+            }
+        L.n_bndface = (int)bf.size();
+        L.d_bndface = to_device(bf);
       }
     }
     L.d_phi = L.d_data;
@@ -2709,15 +2616,14 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fuse_down = env_flag("OMG_NO_FUSE_DOWN");
     c->no_rb_fill_fuse = env_flag("OMG_NO_RB_FUSE");
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
-    c->gs_lex_plane = env_flag("OMG_GS_LEX_PLANE");
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
-    c->no_mid = !env_flag("OMG_MID");   // opt-in: measured slower
-    if (const char* v = getenv("OMG_MID_MAX_BOXES")) c->mid_max_boxes = std::min(std::max(std::atoi(v), 1), kMidMaxBoxes);
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
-    c->check_collective = env_flag("OMG_CHECK_COLLECTIVE");
+    // (on under OMG_DEBUG too: a rank that uploads phi alone would otherwise
+    // make halo exchanges the others skip, a hang or mispaired messages)
+    c->check_collective = env_flag("OMG_CHECK_COLLECTIVE") || c->debug;
     if (const char* v = getenv("OMG_GRAPH_FAIL")) c->graph_fail_at = std::atoi(v);   // tests only
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -2794,12 +2700,6 @@ int omg_ctx_destroy(omg_ctx* c) {
     delete c->h_tail;
     dfree(c->d_red);
     dfree(c->d_maxslots);
-    dfree(c->d_mid_sync);
-    dfree(c->d_mid_err);
-    for (int k = 0; k < 2; k++) {
-      dfree(c->d_mid[k]);
-      delete c->h_mid[k];
-    }
     for (auto& kv : c->graphs)
       if (kv.second) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -3227,7 +3127,6 @@ int omg_synchronize(omg_ctx* c) {
   return guarded([&] {
     host_sync(c, c->stream);
     host_sync(c, c->stream2);
-    check_mid_err(c);
   });
 }
 

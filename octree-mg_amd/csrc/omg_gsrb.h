@@ -169,18 +169,6 @@ __device__ __forceinline__ void op_pair(const OpCoef<OP>& K, const LevelView& L,
   }
 }
 
-// timing-only switch (wrong results; tools/ab_variants.sh): bit 0 = no
-// pushes to y/z neighbours, bit 1 = no y/z ghost-half loads
-#ifndef OMG_T_YZ
-#define OMG_T_YZ 0
-#endif
-
-// timing switch: 0 = refinement-boundary coarse operands loaded in the ghost
-// fill instead of prefetched
-#ifndef OMG_RB_PRE
-#define OMG_RB_PRE 1
-#endif
-
 // RB: the level has refinement-boundary faces (a separate instantiation keeps
 // their interpolation out of the plain kernels)
 template <int NC, int OP, int BS, int NT, bool PRE = false, bool RB = false>
@@ -205,7 +193,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
   // the stream-in (below), so the ghost fill after the substep finds them in
   // registers (the face's coarse box and child offset are in T: one level of
   // loads instead of kind -> record -> coarse cells).
-  constexpr bool RBP = RB && OMG_RB_PRE;
+  constexpr bool RBP = RB;
   constexpr int NF = 6 * NC * NC, NPF = RBP ? (NF + BS - 1) / BS : 1;
   RbCoarse rt[NPF];
 
@@ -224,7 +212,6 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     }
     for (int q = tid; q < 3 * FH; q += BS) {   // 6 faces x FH/2 double2
       const int nb = q / (FH / 2), r = q % (FH / 2);
-      if ((OMG_T_YZ & 2) && nb >= 2) continue;
       const v2d* gp = reinterpret_cast<const v2d*>(u + 2 * HV + nb * FS + o * FH) + r;
       v2d x = NT >= 2 ? __builtin_nontemporal_load(gp) : *gp;
       if (shift) {
@@ -335,7 +322,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     const int idx = ((i - 1) >> 1) + H * ((j - 1) + NC * (k - 1));
     return ((i + j + k) & 1) == e ? se[idx] : so[idx];
   };
-  face_push_local<NC>(L, T, colours, cellv, (OMG_T_YZ & 1) ? 0x3u : 0x3fu);
+  face_push_local<NC>(L, T, colours, cellv, 0x3fu);
   if (!T.nonlocal()) return;
   auto fill_cell = [&](int p, const RbCoarse* rc) {
     const int nb = p / (NC * NC) + 1, cell = p % (NC * NC);
@@ -352,8 +339,17 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
     else if (d == 2) { i1 = a; j1 = x1; k1 = c; }
     else { i1 = a; j1 = c; k1 = x1; }
     const double v1 = cellv(i1, j1, k1);
+    // colours bit 2: the physical / refinement-boundary ghosts of colour e
+    // only (the split fused down-step: other boxes of the level read the
+    // colour 1-e halves as they stood before this substep, k_face_gc forms
+    // them afterwards)
+    const bool keep = (colours & 4) && (((low ? 0 : NC + 1) + a + c) & 1) != e;
     if (kind == NB_REMOTE) {
       sendbuf[(long long)arg * NC * NC + (a - 1) + NC * (c - 1)] = v1;
+    } else if (keep) {
+      if constexpr (RBP) {   // (the stored coarse part is still wanted)
+        if (kind == NB_RB && rbs->gv_mode == 1) rbs->gv[fidx * (NC * NC) + cell] = rb_gv(*rc, a, c);
+      }
     } else if (kind == NB_PHYS) {
       const int i2 = d == 1 ? x2 : i1, j2 = d == 2 ? x2 : j1, k2 = d == 3 ? x2 : k1;
       const int gi = off_gh(L, nb, a, c);
@@ -387,14 +383,7 @@ __device__ __forceinline__ void gsrb_box(const LevelView& L, double lambda, int 
 template <int NC>
 constexpr int gs_lex_lds() { return (NC + 2) * (NC + 2) * (NC + 2) + NC * NC * NC; }
 
-// timing-only switch (wrong results): 1 = no sweep (load + store only),
-// 2 = no loads (sweep + store)
-#ifndef OMG_T_LEX
-#define OMG_T_LEX 0
-#endif
-// NTL: every load non-temporal (past this CU's L1: the mid kernel reads data
-// other workgroups of the launch wrote, omg_tiles.hip k_mid)
-template <int OP, int NC, bool NTL = false>
+template <int OP, int NC>
 __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, int b, double* lds) {
   constexpr int S = NC + 2, S3 = S * S * S, N3 = NC * NC * NC;
   double* P = lds;         // phi(0:nc+1)^3, i fastest (edges and corners unused)
@@ -402,18 +391,18 @@ __device__ __forceinline__ void gs_lex_box(const LevelView& L, double lambda, in
   const OpCoef<OP> K(L, lambda);
   double* u = boxp(L, 1, b);
   const double* f = boxp(L, 2, b);
-  for (int q = threadIdx.x; q < S3 && OMG_T_LEX != 2; q += blockDim.x) {
+  for (int q = threadIdx.x; q < S3; q += blockDim.x) {
     const int i = q % S, j = (q / S) % S, k = q / (S * S);
     const int nbd = (i == 0 || i == S - 1) + (j == 0 || j == S - 1) + (k == 0 || k == S - 1);
     const double* up = u + off_cell(L, i, j, k);
-    P[q] = nbd <= 1 ? (NTL ? __builtin_nontemporal_load(up) : *up) : 0.0;
+    P[q] = nbd <= 1 ? *up : 0.0;
   }
-  for (int q = threadIdx.x; q < N3 && OMG_T_LEX != 2; q += blockDim.x) {
+  for (int q = threadIdx.x; q < N3; q += blockDim.x) {
     const double* fp = f + off_int(L, q % NC + 1, (q / NC) % NC + 1, q / (NC * NC) + 1);
-    R[q] = NTL ? __builtin_nontemporal_load(fp) : *fp;
+    R[q] = *fp;
   }
   __syncthreads();
-  for (int d = 3; d <= 3 * NC && OMG_T_LEX != 1; d++) {
+  for (int d = 3; d <= 3 * NC; d++) {
     for (int p = threadIdx.x; p < NC * NC; p += blockDim.x) {
       const int j = p % NC + 1, k = p / NC + 1, i = d - j - k;
       if (i < 1 || i > NC) continue;

@@ -123,6 +123,11 @@ struct Level {
   // tree): decisions that choose collective calls use these, never the local
   // ones, so every rank takes the same branch (fas_vcycle's stand-alone fill)
   bool any_rb = false, any_phys = false;
+  // some refinement-boundary face of this level (on any rank) has its coarse
+  // box on another rank than its fine box (refinement-boundary exchange,
+  // finish_rb); the fused kernels that form refinement-boundary ghosts
+  // themselves need the coarse box on the same GPU
+  bool any_rbx = false;
   bool all_parents = false;      // every box of this rank at this level is a parent
   bool prolong_smooth_ok = false;  // k_prolong_smooth can serve this level (see build_plan)
   bool shift_pending = false;    // phi -= mean still to apply (see subtract_mean)
@@ -166,7 +171,7 @@ struct Level {
   Transfer rbx;         // refinement-boundary faces across ranks at this level (send: coarse idx at
                         // lvl-1, coarse-side nb, child offset; recv: box*6+nb of my fine face)
   double* d_scratch_rhs = nullptr;   // leaf sums of rhs for the next get_sum
-  double* d_rhs_lex = nullptr;       // rhs in plane order for the lexicographic smoother (ensure_rhs_lex)
+  double* d_rhs_lex = nullptr;       // rhs in ring order for the lexicographic smoother (ensure_rhs_lex)
   bool rhs_lex_ok = false;           // d_rhs_lex equals rhs (dropped by every rhs writer)
   double* d_xlay = nullptr;          // x boundary layers of the last register-ring sweep (k_fill_tile_xl)
   // the second ghost-face set of phi for chains of register-ring sweeps (6
@@ -177,6 +182,10 @@ struct Level {
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
   int* d_int = nullptr;
   int n_bnd = 0, n_int = 0;
+  // the boxes of d_bnd with a physical or refinement-boundary face: their
+  // ghosts there formed again (k_face_gc) after a split fused down-step
+  int* d_bndface = nullptr;
+  int n_bndface = 0;
   // [n]: for a box without remote faces, the faces (bit f = face f+1) whose
   // same-GPU neighbour has one (k_prolong_smooth pushes colour 0 there)
   uint8_t* d_push0 = nullptr;
@@ -245,7 +254,6 @@ struct omg_free_state;    // free-space boundary conditions (omg_api.cpp, omg_fr
 
 namespace omg {
 struct TailArgs;   // omg_kernels.h
-struct MidArgs;    // omg_kernels.h
 // slots of a multi-workgroup max-residual launch (launch_max, omg_device.h)
 constexpr int kMaxSlots = 256, kMaxSlotStride = 16;
 }
@@ -301,7 +309,6 @@ struct omg_ctx {
   bool no_rbgv = false;                // OMG_NO_RBGV: no stored refinement-boundary coarse parts
   bool no_rb_fill_fuse = false;        // OMG_NO_RB_FUSE: unfused correction + fill on refinement-boundary levels
   bool no_gs_plane = false;            // OMG_NO_GS_PLANE: lexicographic GS with the line-per-thread kernel
-  bool gs_lex_plane = false;           // OMG_GS_LEX_PLANE: the compacted-plane kernel instead of the register ring
   bool no_fill_xl = false;             // OMG_NO_FILL_XL: the plain tiled fill after register-ring sweeps
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
@@ -314,19 +321,6 @@ struct omg_ctx {
   // they change
   omg::TailArgs* d_tail = nullptr;
   omg::TailArgs* h_tail = nullptr;   // the last uploaded copy (host)
-  // the mid levels in one launch (run_mid, MidArgs in omg_kernels.h)
-  omg::MidArgs* d_mid[2] = {nullptr, nullptr};   // down / up programs (device)
-  omg::MidArgs* h_mid[2] = {nullptr, nullptr};   // the last uploaded copies
-  unsigned long long* d_mid_sync = nullptr;      // barrier words
-  int* d_mid_err = nullptr;                      // sticky failure flag of k_mid
-  unsigned long long mid_seq = 0;                // launches so far (the barrier words carry it)
-  bool no_mid = true;                            // unless OMG_MID: the mid levels launch by launch
-  // levels of at most this many boxes run in the mid kernel (OMG_MID_MAX_BOXES,
-  // 1..kMidMaxBoxes, A/B runs).  Its barrier costs 1.0-1.8 us at 8-64
-  // workgroups (tools/xcd_probe.hip v4), but one XCD's share of the memory
-  // bandwidth makes a step of a 64-box level slower than a whole-chip launch
-  // (C4 0.43 -> 0.60 ms per cycle with 64, profiles/r04)
-  int mid_max_boxes = 8;
   bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
   long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch

@@ -45,9 +45,8 @@ inline bool gs_tiled(int nc, int op, bool has_rb) {
 }
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
-// rl: rhs copy (launch_rhs_lex) for the register-ring kernel (reg) or the
-// compacted-plane kernel, on gs_lex_plane_ok levels; null: the
-// line-per-thread kernels
+// rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,
+// on gs_lex_ring_ok levels; null: the line-per-thread kernels
 // xl (register ring only, may be null): the swept boxes' new x boundary
 // layers, 512 doubles per box, for launch_fill_tile_xl
 // Two ghost-face sets for chains of register-ring sweeps (round 4): the
@@ -66,8 +65,7 @@ struct GhostSets {
   int phys_load;
 };
 void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl = nullptr,
-                   bool reg = true, double* xl = nullptr, const GhostSets* gs = nullptr,
-                   const GcBC* bc = nullptr);
+                   double* xl = nullptr, const GhostSets* gs = nullptr, const GcBC* bc = nullptr);
 // custom refinement-boundary faces on the host (omg_set_refinement_bnd): per
 // record (item b*6+nb-1) the coarse face and the box in the reference layout,
 // and the callback's ghost face back
@@ -77,9 +75,14 @@ void launch_rbh_scatter(const LevelView& L, int iv, const int* items, int n, con
 // the physical ghosts of phi of the listed boxes (bc_to_gc from the boxes'
 // final boundary cells), after a chain of ghost-set sweeps
 void launch_phys_gc(const LevelView& L, const GcBC& bc, const int* boxes, int n_boxes, hipStream_t st);
-bool gs_lex_plane_ok(int nc, int op);
-// the copy in ring order (reg) or in plane order
-void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg = true);
+// the physical and refinement-boundary ghosts of phi of the listed boxes from
+// their final boundary cells (C: the coarse level), after a split fused
+// down-step
+void launch_face_gc(const LevelView& L, const LevelView& C, const GcBC& bc, const int* boxes, int n_boxes,
+                    hipStream_t st);
+bool gs_lex_ring_ok(int nc, int op);
+// rhs copied into the ring kernel's order
+void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st);
 void launch_box_op(const LevelView& L, int op, double lambda, int i_out, hipStream_t st);
 void launch_residual(const LevelView& L, int op, double lambda, unsigned long long* maxbits,
                      hipStream_t st);
@@ -154,42 +157,6 @@ struct TailArgs {
 // how many of the tail's lowest levels qualify for the LDS-resident program
 constexpr int kTailLdsMaxLevels = 3;   // 8^3, 4^3, 2^3
 
-// The mid levels of the V-cycle, right above the coarse tail (levels of at
-// most kMidMaxBoxes boxes of 16^3 or 8^3, all on this GPU): their steps run
-// in ONE launch of P workgroups that all sit on one XCD (the launch has 8P
-// workgroups; the round-robin dealer puts every eighth on XCD `xcd`, the
-// others leave at once), one box per workgroup and step, with a barrier
-// among the P between steps.  The XCD's workgroups share one L2, so the
-// barrier needs no L2 write-back: stores drained (s_waitcnt), an arrival
-// word per workgroup, a release word, then the CU's L1 invalidated.  Each
-// step is one box program of the level-by-level path (same arithmetic).
-constexpr int kMidMaxLevels = 6, kMidMaxSteps = 112, kMidMaxBoxes = 64, kMidBS = 512;
-enum MidKind : short { MS_SUB = 0, MS_LEX = 1, MS_FILL = 2, MS_RESID = 3, MS_CRHS = 4, MS_PFILL = 5 };
-struct MidLevel {
-  LevelView L;
-  GcBC bc;
-  const int* parents;        // my_parents (local indices)
-  int n_par;
-  const int* parent_local;   // [n] parent at the level below (MS_RESID / MS_PFILL)
-  const int* dixp;
-};
-struct MidStep {
-  short kind, li;            // MidKind; level (lv index; MS_RESID restricts onto li-1, MS_PFILL corrects li from li-1)
-  short e, colours;          // MS_SUB: colour and pushed colours; MS_PFILL: skip1
-};
-struct MidArgs {
-  int n_lvls, n_steps, P, pad_;
-  double lambda;
-  MidLevel lv[kMidMaxLevels];
-  MidStep st[kMidMaxSteps];
-  // arrival words (16 apart) of the P workgroups, the release word, then two
-  // placement blocks (8 per-XCD ticket counters and the chosen XCD)
-  unsigned long long* sync;
-  int* err;                  // sticky: 1 = a wait timed out
-};
-void launch_store_mid(const MidArgs& A, MidArgs* d, hipStream_t st);
-// seq: this launch's number (monotonic per context; the barrier words carry it)
-void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long seq, hipStream_t st);
 void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st);   // dA: device memory
 void launch_store_tail(const TailArgs& A, TailArgs* d, hipStream_t st);   // *d = A in stream order
 

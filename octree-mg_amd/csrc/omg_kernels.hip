@@ -235,13 +235,7 @@ __global__ void __launch_bounds__(256) k_gs_lex_lds(LevelView L, double lambda) 
 // reference's i-fastest loop.  Lane l owns the lines (j, k) = l + 64 r; rhs of
 // its cells is read from L2 GS_PF planes ahead (one wave per box hides no
 // latency by itself).
-#ifndef OMG_GS_PF
-#define OMG_GS_PF 4
-#endif
-// timing-only (wrong results): 1 = no sweep, 2 = no rhs loads, 3 = no box load
-#ifndef OMG_T_LEXW
-#define OMG_T_LEXW 0
-#endif
+constexpr int kGsPF = 4;
 // + one dummy slot per thread: off-plane lanes store there, so the sweep is
 // branch-free and the same every plane (the compiler then keeps the rhs
 // prefetch in flight instead of draining it at each plane)
@@ -254,7 +248,7 @@ template <int OP, int NC, int T, int WPS>
 __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lambda) {
   using TL = Tl<NC>;
   constexpr int S = NC + 2, NL = (NC * NC + T - 1) / T, H = TL::H, HV = TL::HV, FS = TL::FS;
-  constexpr int D0 = 3, D1 = 3 * NC, PF = OMG_GS_PF, NQ = (TL::NST / 2 + T - 1) / T;
+  constexpr int D0 = 3, D1 = 3 * NC, PF = kGsPF, NQ = (TL::NST / 2 + T - 1) / T;
   // planes D0 .. D1 padded to whole groups of PF (the padding planes update nothing)
   constexpr int DP = D0 + ((D1 - D0 + PF) / PF) * PF - 1;
   __shared__ double P[gs_wave_lds<NC, T>()];
@@ -290,8 +284,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
 #pragma unroll
     for (int r = 0; r < NL; r++) {
       const int i = min(max(d - jk[r], 1), NC);   // off-plane lanes load a valid dummy
-      if (OMG_T_LEXW != 2) out[r] = f[(d & 1) * HV + ((i - 1) >> 1) + roff[r]];
-      else out[r] = 0.0;
+      out[r] = f[(d & 1) * HV + ((i - 1) >> 1) + roff[r]];
     }
   };
   // Persistent workgroups: box sequence q = blockIdx.x + G t (G a multiple of
@@ -323,7 +316,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
 #pragma unroll
     for (int r = 0; r < NQ; r++) {
       const int q2 = tid + T * r;
-      if (q2 < TL::NST / 2 && OMG_T_LEXW != 3) buf[r] = *reinterpret_cast<const v2d*>(u + 2 * q2);
+      if (q2 < TL::NST / 2) buf[r] = *reinterpret_cast<const v2d*>(u + 2 * q2);
     }
   };
   int q = blockIdx.x;
@@ -336,7 +329,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
 #pragma unroll
     for (int r = 0; r < NQ; r++) {
       const int q2 = tid + T * r;
-      if (q2 < TL::NST / 2 && OMG_T_LEXW != 3) {
+      if (q2 < TL::NST / 2) {
         P[scat[r] & 0xffff] = buf[r].x;
         P[scat[r] >> 16] = buf[r].y;
       }
@@ -344,7 +337,7 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
     if (q + G < L.n) issue(q + G, ringn);
     __syncthreads();
 #pragma unroll 1
-    for (int d0 = D0; d0 <= DP && OMG_T_LEXW != 1; d0 += PF) {
+    for (int d0 = D0; d0 <= DP; d0 += PF) {
 #pragma unroll
       for (int s = 0; s < PF; s++) {
         const int d = d0 + s;
@@ -400,229 +393,9 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_wave(LevelView L, double lamb
 }
 
 // ---------------------------------------------------------------------------
-// Lexicographic GS over compacted hyperplanes.  k_gs_lex_wave gives every
-// thread a fixed line (j, k) and walks all 46 planes, so 65 % of its slots
-// fall outside the box, and each lane reads the rhs of its own line: 64 cache
-// lines per wave-instruction.  Here the cells of plane d = i+j+k are numbered
-// (k, then j, ascending) and thread t takes the t-th: a 16^3 plane has at most
-// 192 cells, so of a 256-thread workgroup (four waves; fewer threads spill the
-// next box's prefetch) only the waves that hold cells of the plane work on it.
-// rhs is read from a copy in that plane order (k_rhs_lex, rebuilt only after a
-// write of the level's rhs), so each plane's rhs is one contiguous run.  Same
-// cells per plane, same operands and gs_value: bit-identical.  Measured
-// 1190 -> 1100 us per 512^3 sweep (profiles/r03/v7_README.txt).
-template <int NC>
-struct LexPlanes {
-  static constexpr int NPL = 3 * NC - 2, N3 = NC * NC * NC;
-  unsigned short cell[N3];       // dense (NC+2)^3 index of the t-th cell in plane order
-  unsigned short off[NPL + 1];   // first cell of plane d - 3
-  int maxn;                      // the largest plane
-};
-template <int NC>
-constexpr LexPlanes<NC> make_lex_planes() {
-  LexPlanes<NC> P{};
-  constexpr int S = NC + 2;
-  int t = 0;
-  P.maxn = 0;
-  for (int d = 3; d <= 3 * NC; d++) {
-    P.off[d - 3] = (unsigned short)t;
-    for (int k = 1; k <= NC; k++)
-      for (int j = 1; j <= NC; j++) {
-        const int i = d - j - k;
-        if (i >= 1 && i <= NC) P.cell[t++] = (unsigned short)(i + S * (j + S * k));
-      }
-    if (t - P.off[d - 3] > P.maxn) P.maxn = t - P.off[d - 3];
-  }
-  P.off[LexPlanes<NC>::NPL] = (unsigned short)t;
-  return P;
-}
-// 16^3 boxes only: the kernel pays off on large levels of 16^3 boxes
-// (gs_lex_plane_ok)
-constexpr LexPlanes<16> kLexPlanes16 = make_lex_planes<16>();
-static_assert(kLexPlanes16.off[LexPlanes<16>::NPL] == 4096 && kLexPlanes16.maxn == 192, "16^3 planes");
-__constant__ LexPlanes<16> dLexPlanes16 = kLexPlanes16;
-template <int NC>
-__device__ __forceinline__ const LexPlanes<NC>& lex_planes() {
-  static_assert(NC == 16, "16^3 boxes");
-  return dLexPlanes16;
-}
-template <int NC>
-constexpr int lex_maxn() { return kLexPlanes16.maxn; }
-// the size and the first cell of plane p = d - 3 in closed form (inclusion-
-// exclusion over the box's three extents), so the sweep computes them in
-// scalar registers instead of loading them: a load per plane would make every
-// plane wait for the whole prefetch queue (waits are in issue order)
-__host__ __device__ constexpr int lex_c2(int x) { return x >= 2 ? x * (x - 1) / 2 : 0; }
-__host__ __device__ constexpr int lex_c3(int x) { return x >= 3 ? x * (x - 1) * (x - 2) / 6 : 0; }
-template <int NC>
-__host__ __device__ constexpr int lex_plane_n(int p) {
-  return lex_c2(p + 2) - 3 * lex_c2(p - NC + 2) + 3 * lex_c2(p - 2 * NC + 2);
-}
-template <int NC>
-__host__ __device__ constexpr int lex_plane_off(int p) {
-  return lex_c3(p + 2) - 3 * lex_c3(p - NC + 2) + 3 * lex_c3(p - 2 * NC + 2);
-}
-template <int NC>
-constexpr bool lex_closed_form_ok(const LexPlanes<NC>& P) {
-  for (int p = 0; p < LexPlanes<NC>::NPL; p++)
-    if (lex_plane_off<NC>(p) != P.off[p] || lex_plane_n<NC>(p) != P.off[p + 1] - P.off[p]) return false;
-  return true;
-}
-static_assert(lex_closed_form_ok<16>(kLexPlanes16), "plane sizes");
-
-// rhs of every box in plane order: rl[b * NC^3 + t] = rhs at the t-th cell
-template <int NC>
-__global__ void __launch_bounds__(256) k_rhs_lex(LevelView L, double* __restrict__ rl) {
-  using TL = Tl<NC>;
-  constexpr int N3 = NC * NC * NC, S = NC + 2;
-  __shared__ double F[N3];
-  const LexPlanes<NC>& X = lex_planes<NC>();
-  const int b = blockIdx.x;
-  const v2d* f = reinterpret_cast<const v2d*>(boxp(L, 2, b));
-  for (int q = threadIdx.x; q < N3 / 2; q += blockDim.x) reinterpret_cast<v2d*>(F)[q] = f[q];
-  __syncthreads();
-  double* o = rl + (long long)b * N3;
-  for (int t = threadIdx.x; t < N3; t += blockDim.x) {
-    const int c = X.cell[t], i = c % S, j = (c / S) % S, k = c / (S * S);
-    o[t] = F[TL::oint(i, j, k)];
-  }
-}
-
-template <int OP, int NC, int T, int WPS>
-__global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lambda,
-                                                         const double* __restrict__ rl) {
-  using TL = Tl<NC>;
-  constexpr int S = NC + 2, N3 = NC * NC * NC, H = TL::H, HV = TL::HV, FS = TL::FS;
-  constexpr int NPL = LexPlanes<NC>::NPL, PF = OMG_GS_PF, NQ = (TL::NST / 2 + T - 1) / T;
-  constexpr int NLP = (lex_maxn<NC>() + T - 1) / T;   // cells per thread per plane
-  constexpr int NPP = ((NPL + PF - 1) / PF) * PF;     // planes padded to whole groups of PF
-  __shared__ double P[gs_wave_lds<NC, T>()];
-  const LexPlanes<NC>& X = lex_planes<NC>();
-  const int tid = threadIdx.x, G = gridDim.x;
-  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);   // this wave's first thread
-  const OpCoef<OP> K(L, lambda);
-  static_assert(NLP == 1 || T % 64 == 0, "wave-aligned slots");
-  auto dense = [&](int q) {
-    int i, j, k;
-    if (q < 2 * HV) {
-      TL::decode(q, i, j, k);
-    } else {
-      const int r0 = q - 2 * HV, nb = r0 / FS + 1, r1 = r0 % FS;
-      const int e = r1 >= H * NC, r = r1 - e * H * NC, ah = r % H, c = r / H + 1;
-      const int g = (nb & 1) ? 0 : NC + 1;
-      const int a = 2 * ah + 1 + ((1 + g + c + e) & 1);
-      const int d = (nb + 1) >> 1;
-      if (d == 1) { i = g; j = a; k = c; }
-      else if (d == 2) { i = a; j = g; k = c; }
-      else { i = a; j = c; k = g; }
-    }
-    return i + S * (j + S * k);
-  };
-  constexpr int NG2 = (HV + T - 1) / T;
-  unsigned scat[NQ], gath[NG2];
-#pragma unroll
-  for (int r = 0; r < NQ; r++) {
-    const int q2 = min(tid + T * r, TL::NST / 2 - 1);
-    scat[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
-  }
-#pragma unroll
-  for (int r = 0; r < NG2; r++) {
-    const int q2 = min(tid + T * r, HV - 1);
-    gath[r] = (unsigned)dense(2 * q2) | ((unsigned)dense(2 * q2 + 1) << 16);
-  }
-  // plane pl's rhs and LDS cell of this thread's slots (clamped: past-the-end
-  // slots and padding planes read a valid cell and update nothing)
-  auto plane_issue = [&](const double* rb, int pl, double* ov, int* oc) {
-    const int p = min(pl, NPL - 1), o = lex_plane_off<NC>(p), n = lex_plane_n<NC>(p);
-#pragma unroll
-    for (int r = 0; r < NLP; r++) {
-      const int idx = o + min(tid + T * r, n - 1);
-      oc[r] = X.cell[idx];
-      ov[r] = rb[idx];
-    }
-  };
-  double rv[PF][NLP], rvn[PF][NLP];
-  int rc[PF][NLP], rcn[PF][NLP];
-  v2d buf[NQ];
-  auto issue = [&](int q, double (*gv)[NLP], int (*gc)[NLP]) {
-    const int b = xcd_box(q, L.n);
-    const double* rb = rl + (long long)b * N3;
-#pragma unroll
-    for (int s = 0; s < PF; s++) plane_issue(rb, s, gv[s], gc[s]);
-    const double* u = boxp(L, 1, b);
-#pragma unroll
-    for (int r = 0; r < NQ; r++) {
-      const int q2 = tid + T * r;
-      if (q2 < TL::NST / 2) buf[r] = *reinterpret_cast<const v2d*>(u + 2 * q2);
-    }
-  };
-  int q = blockIdx.x;
-  if (q >= L.n) return;
-  issue(q, rv, rc);
-  for (; q < L.n; q += G) {
-    const int b = xcd_box(q, L.n);
-    double* __restrict__ u = boxp(L, 1, b);
-    const double* __restrict__ rb = rl + (long long)b * N3;
-#pragma unroll
-    for (int r = 0; r < NQ; r++) {
-      const int q2 = tid + T * r;
-      if (q2 < TL::NST / 2) {
-        P[scat[r] & 0xffff] = buf[r].x;
-        P[scat[r] >> 16] = buf[r].y;
-      }
-    }
-    if (q + G < L.n) issue(q + G, rvn, rcn);
-    __syncthreads();
-#pragma unroll 1
-    for (int p0 = 0; p0 < NPP; p0 += PF) {
-#pragma unroll
-      for (int s = 0; s < PF; s++) {
-        const int pl = p0 + s;
-        const int n = pl < NPL ? lex_plane_n<NC>(pl) : 0;
-#pragma unroll
-        for (int r = 0; r < NLP; r++) {
-          // waves past the plane's last cell skip it (a wave-uniform branch)
-          if (wbase + T * r >= n) continue;
-          const int c = rc[s][r];
-          Nbr7 st;
-          st.c = P[c];
-          st.xm = P[c - 1];
-          st.xp = P[c + 1];
-          st.ym = P[c - S];
-          st.yp = P[c + S];
-          st.zm = P[c - S * S];
-          st.zp = P[c + S * S];
-          const double nv = gs_value<OP>(K, st, rv[s][r]);
-          P[tid + T * r < n ? c : S * S * S + tid] = nv;
-        }
-        plane_issue(rb, pl + PF, rv[s], rc[s]);
-        __syncthreads();
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < NG2; r++) {
-      const int q2 = tid + T * r;
-      if (q2 >= HV) break;
-      v2d v;
-      v.x = P[gath[r] & 0xffff];
-      v.y = P[gath[r] >> 16];
-      *reinterpret_cast<v2d*>(u + 2 * q2) = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < PF; s++)
-#pragma unroll
-      for (int r = 0; r < NLP; r++) {
-        rv[s][r] = rvn[s][r];
-        rc[s][r] = rcn[s][r];
-      }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Lexicographic GS with the box in registers (round 3).  The plane kernels
-// above keep the box in LDS (46.6 KB: three boxes per CU) and pay a workgroup
-// barrier per hyperplane; their sweep is latency-bound at 36 % of HBM.
+// Lexicographic GS with the box in registers (round 3).  Kernels that keep
+// the box in LDS (k_gs_lex_wave: 46.6 KB, three boxes per CU) pay a workgroup
+// barrier per hyperplane; their sweep is latency-bound at 34-37 % of HBM.
 //
 // Here one wave sweeps one 16^3 box.  Lane l owns the four x-lines
 // (j, k) = (l % 16 + 1, 4 (l / 16) + r + 1), r = 0..3, and keeps each line's
@@ -640,8 +413,8 @@ __global__ void __launch_bounds__(T, WPS) k_gs_lex_plane(LevelView L, double lam
 // away (ds_bpermute), with the z ghosts at the box faces.  No LDS traffic for
 // phi and no barrier per step: the box passes through LDS only to be rotated
 // into and out of the ring (18 KB per box, so 8 boxes share a CU).  rhs comes
-// from a copy in the ring's order (k_rhs_reg, rebuilt after rhs writes like
-// the plane-order copy): the step-t values of all 256 lines are one
+// from a copy in the ring's order (k_rhs_reg, rebuilt after every write of
+// the level's rhs): the step-t values of all 256 lines are one
 // contiguous 2 KB run, prefetched PF steps ahead.  Every cell is updated
 // after its lower neighbours and before its upper ones, with the same
 // operands and gs_value as the reference's i-fastest loop: bit-identical.
@@ -662,20 +435,12 @@ __device__ __forceinline__ double dpp_row_next(double v, double old) {
   return __hiloint2double(hi, lo);
 }
 
-// ring-order rhs blocks rotated by the box index (1) or not (0)
-#ifndef OMG_GS_REG_SW
-#define OMG_GS_REG_SW 1
-#endif
-
-// z crossings between lane groups by ds_bpermute (0) or by the gfx950 row
-// swaps (1): the 16-lane rows hold the lane groups kq = 0, 1, 3, 2, so that
-// every crossing (kq 0-1, 1-2, 2-3) is a v_permlane16_swap or
-// v_permlane32_swap partner
-#ifndef OMG_GS_REG_PERM
-#define OMG_GS_REG_PERM 1
-#endif
+// z crossings between lane groups by the gfx950 row swaps: the 16-lane rows
+// hold the lane groups kq = 0, 1, 3, 2, so that every crossing (kq 0-1, 1-2,
+// 2-3) is a v_permlane16_swap or v_permlane32_swap partner (against
+// ds_bpermute: 837 -> 827 us per 512^3 sweep, profiles/r03)
 // lane group of 16-lane row x, and the row of lane group x (an involution)
-__device__ __forceinline__ int lex_grp(int x) { return OMG_GS_REG_PERM && x >= 2 ? 5 - x : x; }
+__device__ __forceinline__ int lex_grp(int x) { return x >= 2 ? 5 - x : x; }
 // the value of v in the lane of the partner row: x16 swaps rows 0-1, 2-3,
 // x32 rows 0-2, 1-3
 __device__ __forceinline__ double row_partner(double v, bool x32) {
@@ -710,38 +475,19 @@ __global__ void __launch_bounds__(256) k_rhs_reg(LevelView L, double* __restrict
     // and line pair
     const int s = d >> 8, r = 2 * ((d >> 7) & 1) + (d & 1), l = (d >> 1) & 63;
     const int j = (l & 15) + 1, k = 4 * lex_grp(l >> 4) + r + 1, i = ((s - j - k - 1) & 15) + 1;
-    o[(((s + OMG_GS_REG_SW * b) & 15) << 8) | (d & 255)] = F[TL::oint(i, j, k)];
+    o[(((s + b) & 15) << 8) | (d & 255)] = F[TL::oint(i, j, k)];
   }
 }
 
-#ifndef OMG_GS_REG_WPS
-#define OMG_GS_REG_WPS 2
-#endif
-// rhs copy read non-temporally (1) or with the default policy (0)
-#ifndef OMG_GS_REG_RNT
-#define OMG_GS_REG_RNT 0
-#endif
-// phi streams (rotation in and out) non-temporal (1) or default policy (0)
-#ifndef OMG_GS_REG_PNT
-#define OMG_GS_REG_PNT 1
-#endif
-// y ghosts read once per face (1) or once per line for both shifts (0)
-#ifndef OMG_GS_REG_G2
-#define OMG_GS_REG_G2 0
-#endif
-// timing-only (wrong results): 1 = no sweep (rotation in and out only),
-// 2 = no phi loads or stores (the sweep on whatever LDS holds), 3 = every
-// step's rhs from the box's first block (cache-hot), 4 = rhs loaded but not
-// waited for (its values unused)
-#ifndef OMG_T_RING
-#define OMG_T_RING 0
-#endif
+// phi streams (rotation in and out) non-temporal, the rhs copy with the
+// default policy (939 -> 833 us per 512^3 sweep against non-temporal rhs
+// loads, profiles/r03); two waves per SIMD (234 VGPRs)
 // DBL: two ghost-face sets (GhostSets, omg_kernels.h): the ghosts come from
 // gs.in (the physical ones formed here from the box's own boundary cells when
 // gs.phys_load), and the new boundary layers go to the same-GPU neighbours'
 // ghosts in gs.out instead of a fill pass after the sweep.
 template <int OP, int PF, bool DBL>
-__global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl,
+__global__ void __launch_bounds__(64, 2) k_gs_lex_reg(LevelView L, double lambda, const double* __restrict__ rl,
                                                                  double* __restrict__ xl, GhostSets gs, GcBC bc) {
   using TL = Tl<16>;
   constexpr int NC = 16, H = 8, HV = 2048, FH = 128, FS = 256, R = kLexRing, T0 = 3, T1 = 3 * NC;
@@ -795,7 +541,7 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
     for (int n = 0; n < 8; n++) {
       const int k = 4 * (n >> 1) + r + 1, e = n & 1;
       const double* src = u + e * HV + FH * (k - 1) + 2 * l;
-      buf[n] = OMG_T_RING == 2 ? v2d{0.0, 0.0} : (OMG_GS_REG_PNT ? ld_nt(src) : *reinterpret_cast<const v2d*>(src));
+      buf[n] = ld_nt(src);
     }
     const int kr = 4 * kq + r + 1;
     const double gx0 = gb[((j + kr) & 1) * FH + ((j - 1) >> 1) + H * (kr - 1)];
@@ -855,30 +601,18 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   // of the row read face j = 0 as lane j = 1 needs it, the others face j = 17
   // as lane j = 16 needs it; the slack keeps every step's index inside G)
   const int jk0 = j + 4 * kq + 1;                   // line r: jk0 + r
-#if OMG_GS_REG_G2
-  // two reads per line, face j = 0 (the value lane j = 1 keeps in the lower
-  // shift) and face j = 17 (lane j = 16, upper shift): each shift then
-  // writes into its own loaded register, no copies
-  const int gya = kLexGPad - 18 + 15 * (4 * kq + 1), gyb = kLexGFace + kLexGPad - 33 + 15 * (4 * kq + 1);
-#else
   const int gy0 = (j <= 8 ? kLexGPad - 18 : kLexGFace + kLexGPad - 33) + 15 * (4 * kq + 1);   // line r: + 15 r
-#endif
   // z ghosts: lanes of group 0 (line 0, k = 1) read face k = 0, group 3
   // (line 3, k = 16) face k = 17
   const int gz = kq < 2 ? 2 * kLexGFace + kLexGPad + 15 * j - 18 : 3 * kLexGFace + kLexGPad + 15 * j - 33;
-#if !OMG_GS_REG_PERM
-  const int lane_lo = (l + 48) & 63, lane_hi = (l + 16) & 63;
-#endif
 
   double rf[PF][4];
-  double sink = 0.0;   // OMG_T_RING == 4
   // the four lines' rhs of step t: two 16-B loads
   auto ld_rhs = [&](int t, double* out) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const v2d* p = reinterpret_cast<const v2d*>(rb + (OMG_T_RING == 3 ? 0 : ((t + OMG_GS_REG_SW * b) & 15) * 256) +
-                                                  h * 128 + 2 * l);
-      const v2d x = OMG_GS_REG_RNT ? __builtin_nontemporal_load(p) : *p;
+      const v2d* p = reinterpret_cast<const v2d*>(rb + ((t + b) & 15) * 256 + h * 128 + 2 * l);
+      const v2d x = *p;
       out[2 * h] = x.x;
       out[2 * h + 1] = x.y;
     }
@@ -887,34 +621,20 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
   for (int p = 0; p < PF; p++) ld_rhs(T0 + p, rf[(T0 + p) % PF]);
 
 #pragma unroll 1
-  for (int m = 0; m < 3 && OMG_T_RING != 1; m++) {
+  for (int m = 0; m < 3; m++) {
 #pragma unroll
     for (int s = 0; s < R; s++) {
       const int t = R * m + s;
       if (t < T0 || t > T1) continue;                 // wave-uniform
       const int sm = (s + R - 1) % R, sp = (s + 1) % R;
-#if OMG_GS_REG_G2
-      double gva[4], gvb[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        gva[r] = G[gya + 15 * r + t];
-        gvb[r] = G[gyb + 15 * r + t];
-      }
-#else
       double gv[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) gv[r] = G[gy0 + 15 * r + t];
-#endif
       const double gzv = G[gz + t];
-#if OMG_GS_REG_PERM
       // z crossings: group kq takes line 3 of group kq - 1 and line 0 of
       // group kq + 1; pairs 0-1 and 2-3 are x16 partners, 1-2 x32 partners
       const double zlo_n = row_partner(ring[3][sm], kq == 2);
       const double zhi_n = row_partner(ring[0][sp], kq == 1);
-#else
-      const double zlo_n = __shfl(ring[3][sm], lane_lo, 64);
-      const double zhi_n = __shfl(ring[0][sp], lane_hi, 64);
-#endif
       const double zlo = kq == 0 ? gzv : zlo_n;
       const double zhi = kq == 3 ? gzv : zhi_n;
       double nv[4];
@@ -924,17 +644,11 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
         st.c = ring[r][s];
         st.xm = ring[r][sm];
         st.xp = ring[r][sp];
-#if OMG_GS_REG_G2
-        st.ym = dpp_row_prev(ring[r][sm], gva[r]);
-        st.yp = dpp_row_next(ring[r][sp], gvb[r]);
-#else
         st.ym = dpp_row_prev(ring[r][sm], gv[r]);
         st.yp = dpp_row_next(ring[r][sp], gv[r]);
-#endif
         st.zm = r > 0 ? ring[r - 1][sm] : zlo;
         st.zp = r < 3 ? ring[r + 1][sp] : zhi;
-        nv[r] = gs_value<OP>(K, st, OMG_T_RING == 4 ? 0.0 : rf[s % PF][r]);
-        if (OMG_T_RING == 4) sink += rf[s % PF][r];
+        nv[r] = gs_value<OP>(K, st, rf[s % PF][r]);
       }
 #pragma unroll
       for (int r = 0; r < 4; r++)
@@ -948,7 +662,6 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
     }
   }
 
-  if (OMG_T_RING == 4 && sink == 12345.678) u[0] = sink;
   // the interior back, through stage in the stored order (the box pointer
   // made opaque: otherwise the store addresses are shared with the loads'
   // and held across the sweep, which spills)
@@ -997,14 +710,9 @@ __global__ void __launch_bounds__(64, OMG_GS_REG_WPS) k_gs_lex_reg(LevelView L, 
       const int kq2 = n >> 1, k = 4 * kq2 + r + 1, e = n & 1;
       const int i = 2 * ihr + 1 + ((1 + jr + k + e) & 1);
       const int ln = (jr - 1) + 16 * lex_grp(kq2);
-      if (OMG_T_RING != 2) {
-        double* dst = ub + e * HV + FH * (k - 1) + 2 * l;
-        const double x0 = stage[((i + jr + k) % R) * SR + ln], x1 = stage[((i + 2 + jr + k) % R) * SR + ln];
-        if (OMG_GS_REG_PNT)
-          st_nt(dst, x0, x1);
-        else
-          *reinterpret_cast<v2d*>(dst) = v2d{x0, x1};
-      }
+      double* dst = ub + e * HV + FH * (k - 1) + 2 * l;
+      const double x0 = stage[((i + jr + k) % R) * SR + ln], x1 = stage[((i + 2 + jr + k) % R) * SR + ln];
+      st_nt(dst, x0, x1);
     }
   }
 }
@@ -1375,9 +1083,6 @@ static void gs_lex_lds(const LevelView& L, double lambda, unsigned g, int block,
   }
 }
 
-#ifndef OMG_GS_T16
-#define OMG_GS_T16 256
-#endif
 // persistent grid: `per_cu` workgroups per CU (the LDS limit), a multiple of 8
 static unsigned gs_grid(int n, int per_cu) {
   static int cus = 0;
@@ -1395,17 +1100,13 @@ static void gs_lex_wave(const LevelView& L, double lambda, hipStream_t st) {
   switch (L.nc) {
     case 16:
       // 46.6 KB of LDS per box: 3 workgroups per CU
-      k_gs_lex_wave<OP, 16, OMG_GS_T16, (3 * OMG_GS_T16 / 64 + 3) / 4>
-          <<<gs_grid(L.n, 3), OMG_GS_T16, 0, st>>>(L, lambda);
+      k_gs_lex_wave<OP, 16, 256, 3><<<gs_grid(L.n, 3), 256, 0, st>>>(L, lambda);
       break;
     default: k_gs_lex_wave<OP, 8, 64, 4><<<gs_grid(L.n, 16), 64, 0, st>>>(L, lambda); break;
   }
 }
 
-#ifndef OMG_GS_TP16
-#define OMG_GS_TP16 256
-#endif
-bool gs_lex_plane_ok(int nc, int op) { return nc == 16 && (op == OP_LPL || op == OP_HELM); }
+bool gs_lex_ring_ok(int nc, int op) { return nc == 16 && (op == OP_LPL || op == OP_HELM); }
 
 // bc_to_gc (m_ghost_cells.f90:665-766) of phi on the physical faces of the
 // listed boxes, from their stored boundary cells: what the fill after the last
@@ -1430,60 +1131,42 @@ void launch_phys_gc(const LevelView& L, const GcBC& bc, const int* boxes, int n_
   if (n_boxes > 0) k_phys_gc<<<n_boxes, 256, 0, st>>>(L, bc, boxes);
 }
 
-void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st, bool reg) {
+void launch_rhs_lex(const LevelView& L, double* rl, hipStream_t st) {
   if (L.n == 0) return;
   if (L.nc != 16) throw std::runtime_error("launch_rhs_lex: 16^3 boxes only");
-  if (reg)
-    k_rhs_reg<<<L.n, 256, 0, st>>>(L, rl);
-  else
-    k_rhs_lex<16><<<L.n, 256, 0, st>>>(L, rl);
+  k_rhs_reg<<<L.n, 256, 0, st>>>(L, rl);
 }
 
-// rhs prefetch depth in steps (a divisor of the ring's 18): 1 measured
-// fastest (973 against 999 us for 3; 9 and 18 at one wave per SIMD slower)
-#ifndef OMG_GS_REG_PF
-#define OMG_GS_REG_PF 1
-#endif
+// rhs prefetch depth of the ring kernel in steps (a divisor of the ring's
+// 18): 1 measured fastest (973 against 999 us for 3; 9 and 18 at one wave per
+// SIMD slower)
+constexpr int kGsRegPF = 1;
 
-template <int OP>
-static void gs_lex_plane(const LevelView& L, double lambda, const double* rl, hipStream_t st) {
-  constexpr int T = OMG_GS_TP16;
-  k_gs_lex_plane<OP, 16, T, (3 * T / 64 + 3) / 4><<<gs_grid(L.n, 3), T, 0, st>>>(L, lambda, rl);
-}
-
-void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, bool reg, double* xl,
+void launch_gs_lex(const LevelView& L, int op, double lambda, hipStream_t st, const double* rl, double* xl,
                    const GhostSets* gs, const GcBC* bc) {
   if (L.n == 0) return;
   if (rl) {
-    if (!gs_lex_plane_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no plane-order kernel for this level");
-    if (reg) {
-      // one wave per box, one box per workgroup (8 per CU by their LDS)
-      if (gs && !bc) throw std::runtime_error("launch_gs_lex: ghost sets need the boundary conditions");
-      const GhostSets g0{nullptr, 0, nullptr, 0, 0};
-      const GcBC b0{};
-      if (gs) {
-        if (op == OP_HELM)
-          k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
-        else
-          k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
-      } else if (op == OP_HELM) {
-        k_gs_lex_reg<OP_HELM, OMG_GS_REG_PF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
-      } else {
-        k_gs_lex_reg<OP_LPL, OMG_GS_REG_PF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
-      }
-      return;
+    if (!gs_lex_ring_ok(L.nc, op)) throw std::runtime_error("launch_gs_lex: no ring kernel for this level");
+    // one wave per box, one box per workgroup (8 per CU by their LDS)
+    if (gs && !bc) throw std::runtime_error("launch_gs_lex: ghost sets need the boundary conditions");
+    const GhostSets g0{nullptr, 0, nullptr, 0, 0};
+    const GcBC b0{};
+    if (gs) {
+      if (op == OP_HELM)
+        k_gs_lex_reg<OP_HELM, kGsRegPF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
+      else
+        k_gs_lex_reg<OP_LPL, kGsRegPF, true><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, *gs, *bc);
+    } else if (op == OP_HELM) {
+      k_gs_lex_reg<OP_HELM, kGsRegPF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
+    } else {
+      k_gs_lex_reg<OP_LPL, kGsRegPF, false><<<L.n, 64, 0, st>>>(L, lambda, rl, xl, g0, b0);
     }
-    if (op == OP_HELM)
-      gs_lex_plane<OP_HELM>(L, lambda, rl, st);
-    else
-      gs_lex_plane<OP_LPL>(L, lambda, rl, st);
     return;
   }
-  static const bool wg = getenv("OMG_GS_LEX_WG") != nullptr;
-  if ((L.nc == 16 || L.nc == 8) && (op == OP_LPL || op == OP_HELM) && !wg) {
-    // persistent, software-pipelined (k_gs_lex_wave); OMG_GS_LEX_WG: the
-    // one-box-per-workgroup kernel (which the variable-coefficient operators
-    // keep: their eps loads would spill the pipelined kernel)
+  if ((L.nc == 16 || L.nc == 8) && (op == OP_LPL || op == OP_HELM)) {
+    // persistent, software-pipelined (k_gs_lex_wave); the variable-coefficient
+    // operators keep the one-box-per-workgroup kernel (their eps loads would
+    // spill the pipelined kernel)
     if (op == OP_HELM)
       gs_lex_wave<OP_HELM>(L, lambda, st);
     else

@@ -14,49 +14,15 @@
 #include "omg_gsrb.h"
 #include "omg_kernels.h"
 
-// the coarse tail's levels resident in LDS: 1 = those of at most 8^3 cells,
-// 2 = and a 16^3 top level (0: the global-memory box programs for every
-// level; A/B builds only)
-#ifndef OMG_TAIL_LDS
-#define OMG_TAIL_LDS 2
-#endif
-// k_prolong_smooth tuning: waves per SIMD it is compiled for; PRE issues the
-// substep's rhs loads before the correction phases (A/B builds only)
-#ifndef OMG_PS_WAVES
-#define OMG_PS_WAVES 8
-#endif
-#ifndef OMG_PS_PRE
-#define OMG_PS_PRE 0
-#endif
-// old ghost values by LDS-DMA (boxes without a physical face)
-#ifndef OMG_PS_OGLDS
-#define OMG_PS_OGLDS 1
-#endif
-// threads per 16^3 box
-#ifndef OMG_PS_BS16
-#define OMG_PS_BS16 512
-#endif
-// leaves per wave of the get_sum box sums (a wave per 64 threads)
-#ifndef OMG_SUMS_LPW
-#define OMG_SUMS_LPW 32
-#endif
-// rows of a box per chunk of the get_sum box sums
-#ifndef OMG_SUMS_R
-#define OMG_SUMS_R 4
-#endif
-// non-temporal loads in the get_sum box sums; loads / stores of the fused
-// rhs subtract
-#ifndef OMG_SUMS_NT
-#define OMG_SUMS_NT 1
-#endif
-#ifndef OMG_SUB_NT_LD
-#define OMG_SUB_NT_LD 0
-#endif
-#ifndef OMG_SUB_NT_ST
-#define OMG_SUB_NT_ST 0
-#endif
-
 namespace omg {
+
+// threads per 16^3 box of k_prolong_smooth; waves per SIMD it is compiled for
+constexpr int kPsBS16 = 512, kPsWaves = 8;
+// get_sum box sums: leaves per wave (a wave per 64 threads), rows of a box per
+// chunk, non-temporal loads (plain sums; the fused rhs subtract loads and
+// stores with the default policy)
+constexpr int kSumsLPW = 32, kSumsR = 4;
+constexpr bool kSumsNT = true, kSubNTLd = false, kSubNTSt = false;
 
 template <int NC, int OP, int BS>
 __device__ __forceinline__ void resid_restrict_core(const LevelView& F, const LevelView& Cv, double lambda,
@@ -191,27 +157,11 @@ __device__ __forceinline__ int sr_edge(int d, int t, bool lo, int nl, int a, int
   return ax == 0 ? Tl<NC>::ogh(fn, j, k) : (ax == 1 ? Tl<NC>::ogh(fn, i, k) : Tl<NC>::ogh(fn, i, j));
 }
 
-// k_smooth_resid: non-temporal loads of colour 1 and rhs (measured 85 us
-// slower at 512^3: the neighbours' loads of the same lines then miss L2);
-// EARLY: neighbour loads issued before the bulk loads (10 us faster); timing-only
-// switches (wrong results): no neighbour loads / no ghost recompute
-#ifndef OMG_SR_NT
-#define OMG_SR_NT 0
-#endif
-#ifndef OMG_SR_EARLY
-#define OMG_SR_EARLY 1
-#endif
-#ifndef OMG_SR_NOLOAD
-#define OMG_SR_NOLOAD 0
-#endif
-#ifndef OMG_SR_NOGHOST
-#define OMG_SR_NOGHOST 0
-#endif
-template <bool NT>
-__device__ __forceinline__ v2d sr_ld(const double* p) {
-  if (NT) return ld_nt(p);
-  return *reinterpret_cast<const v2d*>(p);
-}
+// k_smooth_resid loads colour 1 and rhs with the default policy (non-temporal
+// measured 85 us slower at 512^3: the neighbours' loads of the same lines then
+// miss L2), and issues the neighbour loads before the bulk loads (10 us
+// faster)
+__device__ __forceinline__ v2d sr_ld(const double* p) { return *reinterpret_cast<const v2d*>(p); }
 
 // The last down-smoothing substep of a level fused with update_coarse's
 // residual + restriction (k_smooth_resid).  The substep updates colour 0
@@ -247,18 +197,17 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
   auto bulk_loads = [&]() {
     // colour 1 and the colour-1 halves of the ghost faces
     for (int q = tid; q < HV / 2; q += BS)
-      reinterpret_cast<v2d*>(sb + HV)[q] = sr_ld<OMG_SR_NT>(u + HV + 2 * q);
+      reinterpret_cast<v2d*>(sb + HV)[q] = sr_ld(u + HV + 2 * q);
     for (int q = tid; q < 3 * FH; q += BS) {
       const int nb = q / (FH / 2), r = q % (FH / 2);
-      reinterpret_cast<v2d*>(sb + 2 * HV + nb * FS + FH)[r] = sr_ld<OMG_SR_NT>(u + 2 * HV + nb * FS + FH + 2 * r);
+      reinterpret_cast<v2d*>(sb + 2 * HV + nb * FS + FH)[r] = sr_ld(u + 2 * HV + nb * FS + FH + 2 * r);
     }
 #pragma unroll
     for (int r = 0; r < NR; r++) {
       const int q2 = tid + BS * r;
-      if (q2 < HV) fr[r] = sr_ld<OMG_SR_NT>(f + 2 * q2);
+      if (q2 < HV) fr[r] = sr_ld(f + 2 * q2);
     }
   };
-  if (!OMG_SR_EARLY) bulk_loads();
   // the neighbour-side operands of our colour-0 ghost cells: N's cell X at
   // (layer nl, a, c) has neighbours deep (N's second layer), across (our
   // boundary layer, LDS), and tangentially N's boundary cells (our colour-1
@@ -267,7 +216,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     const int p = tid + BS * g;
-    if (p >= 6 * FH || OMG_SR_NOLOAD) continue;
+    if (p >= 6 * FH) continue;
     const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
     // (physical and refinement-boundary faces have no neighbour box: their
     // argument is a BC code or a coarse box index, not a box of this level)
@@ -307,7 +256,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
       }
     }
   }
-  if (OMG_SR_EARLY) bulk_loads();
+  bulk_loads();
   __syncthreads();
 
   const OpCoef<OP> K(F, lambda);
@@ -329,7 +278,7 @@ __global__ void __launch_bounds__(BS) k_smooth_resid(LevelView F, LevelView Cv, 
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     const int p = tid + BS * g;
-    if (p >= 6 * FH || OMG_SR_NOGHOST) continue;
+    if (p >= 6 * FH) continue;
     const int nb = p / FH + 1, hi = p % FH, ah = hi % H, c = hi / H + 1;
     const bool low = nb & 1;
     const int gl = low ? 0 : NC + 1, a = 2 * ah + 1 + ((gl + 1 + c) & 1);
@@ -394,10 +343,10 @@ constexpr int prolong_cb() { return ((NC / 2 + 2) * (NC / 2 + 2) * (NC / 2 + 2) 
 // the edge cells the parent stores, for the siblings' boundary cells).  Loads
 // are all issued before any store: the res stores alias the phi/old loads, so
 // an interleaved loop would serialise every load behind the previous store.
-template <int NC, int BS, bool SUB, bool EDGES = false, bool NTL = false>
+template <int NC, int BS, bool SUB, bool EDGES = false>
 __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, int pb, int dx, int dy, int dz,
                                                    double* cb) {
-  auto ld = [](const double* p) { return NTL ? __builtin_nontemporal_load(p) : *p; };
+  auto ld = [](const double* p) { return *p; };
   constexpr int CB = NC / 2 + 2, N = CB * CB * CB, NQ = (N + BS - 1) / BS;
   const int tid = threadIdx.x;
   const int n1 = Cv.nc + 1;
@@ -439,8 +388,7 @@ __device__ __forceinline__ void load_parent_octant(const LevelView& Cv, int iv, 
 // save_old: FMG's `old = phi` of this level (m_multigrid.f90:127-129) for the
 // interior, from the pre-correction values loaded here anyway (the caller
 // copies the ghost faces before the launch; needs !skip1: every pair loaded).
-// NTL: the parent loads non-temporal too (the mid kernel, k_mid)
-template <int NC, int BS, bool SUB, bool RB = false, bool NTL = false>
+template <int NC, int BS, bool SUB, bool RB = false>
 __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const LevelView& F, int iv,
                                                  const int* parent_local, const int* dixp, const GcBC& bc,
                                                  double* sendbuf, int b, double* lds, bool skip1,
@@ -462,7 +410,7 @@ __device__ __forceinline__ void prolong_fill_box(const LevelView& Cv, const Leve
     const int q2 = tid + BS * r;
     if (q2 < npair) old[r] = ld_nt(u + 2 * q2);
   }
-  load_parent_octant<NC, BS, SUB, false, NTL>(Cv, iv, pb, dx, dy, dz, cb);
+  load_parent_octant<NC, BS, SUB>(Cv, iv, pb, dx, dy, dz, cb);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < NR; r++) {
@@ -583,14 +531,10 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
     const int q2 = tid + BS * r;
     if (q2 < HV / 2) old[r] = ld_nt(u + 2 * q2);
   }
-#if OMG_PS_PRE
-  GsrbRhs<NC, BS> pre;
-  gsrb_load_rhs<NC, BS, 2>(F, 1, b, pre);
-#endif
   // The old values in our colour-0 ghost halves (og below) go by LDS-DMA into
   // the colour-1 half of the tile, unused until the substep in a box without
   // a physical face: no registers held across the parent's loads.
-  const bool og_lds = OMG_PS_OGLDS && !phys && 6 * FH <= HV;   // fits the colour-1 half (NC >= 8)
+  const bool og_lds = !phys && 6 * FH <= HV;   // fits the colour-1 half (NC >= 8)
   if (og_lds && tid < 3 * FH) {   // 16-B chunks of the six face halves
     const int q = 2 * tid;
     __builtin_amdgcn_global_load_lds((glb_void*)(u + 2 * HV + (q / FH) * TL::FS + q % FH),
@@ -755,18 +699,14 @@ __device__ __forceinline__ void prolong_smooth_box(const LevelView& Cv, const Le
   // (the substep's epilogue stores the level's refinement-boundary coarse
   // parts for the substeps after it, RbSide::gv)
   const RbSide rbs{Cv, nullptr, rbgv, rbgv ? 1 : 0};
-#if OMG_PS_PRE
-  gsrb_box<NC, OP, BS, 2, true, RB>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, &pre, RB ? &rbs : nullptr);
-#else
   gsrb_box<NC, OP, BS, 2, true, RB>(F, lambda, 1, 2, bc, nullptr, nullptr, b, lds, nullptr, RB ? &rbs : nullptr);
-#endif
 }
 
 template <int NC, int OP, int BS, bool RB = false>
 // 8 waves per SIMD (4 workgroups of 16^3 per CU, the LDS limit): VGPRs <= 64;
 // the refinement-boundary form holds the coarse operands of its epilogue in
 // registers too (4 waves per SIMD)
-__global__ void __launch_bounds__(BS, RB ? 4 : OMG_PS_WAVES) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
+__global__ void __launch_bounds__(BS, RB ? 4 : kPsWaves) k_prolong_smooth(LevelView Cv, LevelView F, double lambda,
                                                        const int* parent_local, const int* dixp, GcBC bc,
                                                        int one_child, const int* list, const uint8_t* push0,
                                                        double* rbgv) {
@@ -791,7 +731,7 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
   else                                                                                                          \
     k_prolong_smooth<NC, OP_LPL, BS, true><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
                                                              list, push0, rbgv);
-    if (F.nc == 16) OMG_PSR(16, OMG_PS_BS16) else OMG_PSR(8, 256)
+    if (F.nc == 16) OMG_PSR(16, kPsBS16) else OMG_PSR(8, 256)
 #undef OMG_PSR
     return;
   }
@@ -803,7 +743,7 @@ void launch_prolong_smooth(const LevelView& C, const LevelView& F, int op, doubl
     k_prolong_smooth<NC, OP_LPL, BS><<<g, BS, 0, st>>>(C, F, lambda, parent_local, dixp, bc, one_child,  \
                                                        list, push0, nullptr);
   switch (F.nc) {
-    case 16: OMG_PS(16, OMG_PS_BS16) break;
+    case 16: OMG_PS(16, kPsBS16) break;
     case 8: OMG_PS(8, 256) break;
     case 4: OMG_PS(4, 256) break;
     default: OMG_PS(2, 256) break;
@@ -837,12 +777,12 @@ __device__ __forceinline__ void sums_st(double* p, double2 v) {
     *reinterpret_cast<double2*>(p) = v;
 }
 
-template <int NC, bool SUB, int LPW = OMG_SUMS_LPW>
+template <int NC, bool SUB, int LPW = kSumsLPW>
 __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int* __restrict__ leaves,
                                                   int n_leaves, double* __restrict__ out,
                                                   const double* __restrict__ mean) {
-  constexpr int H = NC / 2, R = OMG_SUMS_R < NC ? OMG_SUMS_R : NC, SEG = R * H;   // doubles of one colour in a chunk
-  constexpr bool NTL = SUB ? OMG_SUB_NT_LD : OMG_SUMS_NT;
+  constexpr int H = NC / 2, R = kSumsR < NC ? kSumsR : NC, SEG = R * H;   // doubles of one colour in a chunk
+  constexpr bool NTL = SUB ? kSubNTLd : kSumsNT;
   constexpr int CH2 = SEG;                        // double2 per box per chunk (2 colours)
   constexpr int PER = LPW * CH2 / 64;             // double2 per lane per chunk
   constexpr int P = 2 * SEG + 1;                  // LDS box stride (odd: no bank conflicts)
@@ -862,32 +802,37 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
     dst[r] = bb * P + seg * SEG + 2 * off;
   }
   const double m = SUB ? *mean : 0.0;
-  double2 v[PER];
+  // two chunks in flight (vmcnt counts loads and stores together, in issue
+  // order: with one chunk of lookahead every chunk's loads also waited for the
+  // previous chunk's stores)
+  double2 va[PER], vb[PER];
+  auto chunk_off = [](int c) { return H * (((c % (NC / R)) * R) + NC * (c / (NC / R))); };
 #pragma unroll
-  for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r]);
+  for (int r = 0; r < PER; r++) va[r] = sums_ld<NTL>(src[r]);
+#pragma unroll
+  for (int r = 0; r < PER; r++) vb[r] = sums_ld<NTL>(src[r] + chunk_off(1));
   double acc = 0.0;
   const double* my = lds + lane * P;
-  for (int c = 0; c < NCH; c++) {
+  auto process = [&](double2* v, int c) {
     __syncthreads();
-    const int rc = H * (((c % (NC / R)) * R) + NC * (c / (NC / R)));   // chunk offset
+    const int rc = chunk_off(c);
 #pragma unroll
     for (int r = 0; r < PER; r++) {
       if (SUB) {
         v[r].x = v[r].x - m;
         v[r].y = v[r].y - m;
-        if (own[r]) sums_st<OMG_SUB_NT_ST>(src[r] + rc, v[r]);
+        if (own[r]) sums_st<kSubNTSt>(src[r] + rc, v[r]);
       }
       lds[dst[r]] = v[r].x;
       lds[dst[r] + 1] = v[r].y;
     }
     __syncthreads();
-    const int k = c / (NC / R) + 1, j0 = (c % (NC / R)) * R + 1;
-    if (c + 1 < NCH) {
-      const int k1 = (c + 1) / (NC / R) + 1, j1 = ((c + 1) % (NC / R)) * R + 1;
-      const int r1 = H * ((j1 - 1) + NC * (k1 - 1));
+    if (c + 2 < NCH) {
+      const int r2 = chunk_off(c + 2);
 #pragma unroll
-      for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r] + r1);
+      for (int r = 0; r < PER; r++) v[r] = sums_ld<NTL>(src[r] + r2);
     }
+    const int k = c / (NC / R) + 1, j0 = (c % (NC / R)) * R + 1;
     if (lane < LPW) {
 #pragma unroll
       for (int rr = 0; rr < R; rr++) {
@@ -895,12 +840,17 @@ __global__ void __launch_bounds__(64) k_box_sums3(LevelView L, int iv, const int
         const double* A = my + ca * SEG + rr * H;
         const double* B = my + (1 - ca) * SEG + rr * H;
 #pragma unroll
-        for (int m = 0; m < H; m++) {
-          acc += A[m];
-          acc += B[m];
+        for (int q = 0; q < H; q++) {
+          acc += A[q];
+          acc += B[q];
         }
       }
     }
+  };
+  static_assert(NCH % 2 == 0, "chunks come in pairs");
+  for (int c = 0; c < NCH; c += 2) {
+    process(va, c);
+    process(vb, c + 1);
   }
   if (lane < LPW && b0 + lane < n_leaves) out[b0 + lane] = acc;
 }
@@ -1325,7 +1275,7 @@ bool launch_coarse_rhs_tile(const LevelView& C, int op, double lambda, const int
 
 void launch_box_sums(const LevelView& L, int iv, const int* leaves, int n, double* out, hipStream_t st) {
   if (n == 0) return;
-  const dim3 g((n + OMG_SUMS_LPW - 1) / OMG_SUMS_LPW);
+  const dim3 g((n + kSumsLPW - 1) / kSumsLPW);
   switch (L.nc) {
     case 16: k_box_sums3<16, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
     case 8: k_box_sums3<8, false><<<g, 64, 0, st>>>(L, iv, leaves, n, out, nullptr); break;
@@ -1339,7 +1289,7 @@ bool subtract_sums_nc(int nc) { return nc == 16 || nc == 8 || nc == 4; }
 void launch_subtract_sums(const LevelView& L, int iv, const int* leaves, int n, const double* mean, double* out,
                           hipStream_t st) {
   if (n == 0) return;
-  const dim3 g((n + OMG_SUMS_LPW - 1) / OMG_SUMS_LPW);
+  const dim3 g((n + kSumsLPW - 1) / kSumsLPW);
   switch (L.nc) {
     case 16: k_box_sums3<16, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
     case 8: k_box_sums3<8, true><<<g, 64, 0, st>>>(L, iv, leaves, n, out, mean); break;
@@ -1499,7 +1449,7 @@ constexpr int kTailLdsDoubles = 4 * (10 * 10 * 10 + 6 * 6 * 6 + 4 * 4 * 4);
 // the physical bc values of each face cell of each level, resolved once
 // (stored in rhs ghosts / tabulated / constant)
 constexpr int kTailLdsBcDoubles = 6 * (8 * 8 + 4 * 4 + 2 * 2);
-// OMG_TAIL_LDS >= 2: a 16^3 top level as well, phi and rhs only (its old is
+// A 16^3 top level as well, phi and rhs only (its old is
 // not used inside the tail, its res goes straight to HBM)
 constexpr int kTailBigS = 18, kTailBigS3 = kTailBigS * kTailBigS * kTailBigS;
 constexpr int kTailBigDoubles = 2 * kTailBigS3 + 6 * 16 * 16;
@@ -2151,7 +2101,7 @@ template <int OP, bool LEX>
 __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restrict__ dA) {
   // the global-memory box programs' LDS, which also holds the LDS-resident
   // levels while they are in use (the two never overlap in time)
-  constexpr int kSmall = kTailLdsDoubles + kTailLdsBcDoubles + (OMG_TAIL_LDS >= 2 ? kTailBigDoubles : 0);
+  constexpr int kSmall = kTailLdsDoubles + kTailLdsBcDoubles + kTailBigDoubles;
   __shared__ double lds[tail_lds<LEX>() > kSmall ? tail_lds<LEX>() : kSmall];
   __shared__ double red;
   __shared__ TailLdsLevel tll[kTailLdsLevels + 1];
@@ -2159,8 +2109,8 @@ __global__ void __launch_bounds__(kTailBS) k_coarse_tail(const TailArgs* __restr
   const int top = A.n_lvls - 1;
   // levels 0..ls live in LDS, and with big the 16^3 top level above them
   // (phi, rhs); the host decided which (run_tail)
-  const int ls = OMG_TAIL_LDS ? A.lds_levels - 1 : -1;
-  const bool big = OMG_TAIL_LDS >= 2 && A.lds_top;
+  const int ls = A.lds_levels - 1;
+  const bool big = A.lds_top;
   const TailBox XB = tail_big_box(lds);
   int ns = 0;
   auto stamp = [&]() {
@@ -2334,219 +2284,6 @@ void launch_coarse_tail(const TailArgs* dA, int gs_lex, int op, hipStream_t st) 
   }
 }
 
-// ---------------------------------------------------------------------------
-// The mid levels in one launch (MidArgs, omg_kernels.h).
-__device__ __forceinline__ int xcc_id() {
-  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): the XCD this wave runs on
-  return __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15;
-}
-
-constexpr long long kMidSpin = 1ll << 21;   // polls before a barrier gives up (~0.2 s)
-#ifndef OMG_MID_INV
-#define OMG_MID_INV 0
-#endif
-
-// the flag words: device-scope accesses (sc1: past this CU's L1, which
-// other CUs' stores never refresh; group-scope loads hit it and spin on a
-// stale value, tools/xcd_probe.hip v3)
-__device__ __forceinline__ unsigned long long mid_flag_ld(const MidArgs&, const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void mid_flag_st(const MidArgs&, unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the barrier among the P workgroups of one XCD; false: give up (timeout)
-__device__ __forceinline__ bool mid_barrier(const MidArgs& A, int w, unsigned long long val) {
-  unsigned long long* sync = A.sync;
-  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) in every wave: this workgroup's stores are in L2
-  __syncthreads();
-  bool ok = true;
-  if (w == 0) {
-    if (threadIdx.x < 64) {
-      const int l = threadIdx.x;
-      long long it = 0;
-      while (true) {
-        const unsigned long long v = l > 0 && l < A.P ? mid_flag_ld(A, sync + 16 * l) : val;
-        if (__all(v >= val)) break;
-        if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (l == 0) {
-        if (!ok) atomicOr(A.err, 1);
-        mid_flag_st(A, sync + 16 * kMidMaxBoxes, val);
-      }
-    }
-  } else if (threadIdx.x == 0) {
-    mid_flag_st(A, sync + 16 * w, val);
-    long long it = 0;
-    while (mid_flag_ld(A, sync + 16 * kMidMaxBoxes) < val) {
-      if (++it > kMidSpin || __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        atomicOr(A.err, 1);
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __shared__ int okw;
-  if (threadIdx.x == 0) okw = ok;
-  // Every load of the box programs in this kernel is non-temporal: those
-  // bypass this CU's L1 (which other CUs' stores never refresh) and read the
-  // XCD's L2, where every participant's stores are once its vmcnt(0) wait
-  // above has passed.  OMG_MID_INV=1 instead invalidates L1 (device-scope
-  // buffer_inv, one wave; the group-scope form leaves L1 alone outside
-  // thread-group-split mode): 2.6 us per barrier at 8 workgroups on the
-  // XCD, 15.6 us at 64 (tools/xcd_probe.hip).
-  if (OMG_MID_INV && threadIdx.x < 64) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  return okw != 0;
-}
-
-// one box program per step kind, each compiled on its own (__noinline__):
-// inlined into one kernel their register demands add up (256 VGPRs, spills
-// at the 128 the co-residency needs)
-template <int NC, int OP>
-__device__ __noinline__ void mid_sub(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  const MidLevel& M = A.lv[S.li];
-  gsrb_box<NC, OP, kMidBS, 2>(M.L, A.lambda, S.e, S.colours, M.bc, nullptr, nullptr, b, lds);
-}
-template <int NC, int OP>
-__device__ __noinline__ void mid_lex(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  gs_lex_box<OP, NC, true>(A.lv[S.li].L, A.lambda, b, lds);
-}
-template <int NC>
-__device__ __noinline__ void mid_fill(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  // k_fill_tile's box program: the interior into LDS, then the faces
-  const MidLevel& M = A.lv[S.li];
-  const FaceTopo T = load_topo(M.L, b);
-  const double* u = M.L.phi + (long long)b * M.L.stride;
-  for (int q = threadIdx.x; q < Tl<NC>::HV; q += kMidBS)
-    reinterpret_cast<v2d*>(lds)[q] = ld_nt(u + 2 * q);
-  __syncthreads();
-  tile_face_fill<NC>(M.L, b, T, lds, 3, M.bc, nullptr);
-}
-template <int NC, int OP>
-__device__ __noinline__ void mid_resid(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  const MidLevel& M = A.lv[S.li];
-  resid_restrict_box<NC, OP, kMidBS>(M.L, A.lv[S.li - 1].L, A.lambda, nullptr, 1, M.parent_local, M.dixp, b, lds);
-}
-template <int NC, int OP>
-__device__ __noinline__ void mid_crhs(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  const MidLevel& M = A.lv[S.li];
-  coarse_rhs_box<NC, OP, kMidBS, true>(M.L, A.lambda, M.parents[b], lds);
-}
-template <int NC>
-__device__ __noinline__ void mid_pfill(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  const MidLevel& M = A.lv[S.li];
-  prolong_fill_box<NC, kMidBS, true, false, true>(A.lv[S.li - 1].L, M.L, 4, M.parent_local, M.dixp, M.bc, nullptr,
-                                                   b, lds, S.colours != 0);
-}
-
-template <int NC, int OP, bool LEX>
-__device__ __forceinline__ void mid_box(const MidArgs& A, const MidStep& S, int b, double* lds) {
-  switch (S.kind) {
-    case MS_SUB: mid_sub<NC, OP>(A, S, b, lds); break;
-    case MS_LEX:
-      if constexpr (LEX) mid_lex<NC, OP>(A, S, b, lds);
-      break;
-    case MS_FILL: mid_fill<NC>(A, S, b, lds); break;
-    case MS_RESID: mid_resid<NC, OP>(A, S, b, lds); break;
-    case MS_CRHS: mid_crhs<NC, OP>(A, S, b, lds); break;
-    case MS_PFILL: mid_pfill<NC>(A, S, b, lds); break;
-  }
-}
-
-// (two workgroups per CU, so that the P <= 64 participants are resident on
-// the XCD's 32 CUs at once: 4 waves per SIMD, at most 128 VGPRs)
-template <int OP, bool LEX>
-__global__ void __launch_bounds__(kMidBS, 4) k_mid(const MidArgs* __restrict__ dA, unsigned long long seq) {
-  extern __shared__ double lds[];
-  const MidArgs& A = *dA;
-  const int P = A.P;
-  // The participants: the first P workgroups to arrive on one XCD, whichever
-  // fills first (the 8P workgroups are usually dealt round-robin, but kernels
-  // of other streams dispatched meanwhile shift that).  Each workgroup takes a
-  // ticket on its XCD's counter; the one completing a group of P names that
-  // XCD; ticket holders below P wait for the name and stay if it is theirs.
-  // The counters of this launch (parity seq & 1) were zeroed by the launch
-  // before it.
-  __shared__ int sh_w;
-  unsigned long long* place = A.sync + 16 * (kMidMaxBoxes + 1 + 2 * (seq & 1));
-  if (threadIdx.x == 0) {
-    const int x = xcc_id();
-    const unsigned long long t = atomicAdd(place + x, 1ull);
-    int wv = -1;
-    if (t < (unsigned long long)P) {
-      if (t == (unsigned long long)P - 1) atomicCAS(place + 8, 0ull, (unsigned long long)(x + 1));
-      long long it = 0;
-      unsigned long long win;
-      while ((win = __hip_atomic_load(place + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-        if (++it > kMidSpin) {
-          atomicOr(A.err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (win == (unsigned long long)(x + 1)) wv = (int)t;
-    }
-    sh_w = wv;
-  }
-  __syncthreads();
-  const int w = sh_w;
-  if (w < 0) return;
-  for (int s = 0; s < A.n_steps; s++) {
-    const MidStep S = A.st[s];
-    const MidLevel& M = A.lv[S.li];
-    const int n = S.kind == MS_CRHS ? M.n_par : M.L.n;
-    for (int b = w; b < n; b += P) {
-      if (M.L.nc == 16)
-        mid_box<16, OP, LEX>(A, S, b, lds);
-      else
-        mid_box<8, OP, LEX>(A, S, b, lds);
-      __syncthreads();
-    }
-    if (!mid_barrier(A, w, (seq << 8) | (unsigned long long)(s + 1))) return;
-  }
-  // the next launch's placement counters (nothing of this launch reads them;
-  // the next launch starts after this one has ended)
-  unsigned long long* next = A.sync + 16 * (kMidMaxBoxes + 1 + 2 * ((seq + 1) & 1));
-  if (w == 0 && threadIdx.x < 9) __hip_atomic_store(next + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-static_assert(sizeof(MidArgs) + 16 <= 4096, "MidArgs must fit the 4 KiB kernel-argument limit");
-__global__ void __launch_bounds__(256) k_store_mid(MidArgs A, MidArgs* d) {
-  const unsigned* s = reinterpret_cast<const unsigned*>(&A);
-  unsigned* o = reinterpret_cast<unsigned*>(d);
-  for (int i = threadIdx.x; i < (int)(sizeof(MidArgs) / 4); i += blockDim.x) o[i] = s[i];
-}
-
-void launch_store_mid(const MidArgs& A, MidArgs* d, hipStream_t st) { k_store_mid<<<1, 256, 0, st>>>(A, d); }
-
-void launch_mid(const MidArgs* dA, int P, int lex, int op, unsigned long long seq, hipStream_t st) {
-  // LDS: the largest box program (16^3 residual tile; lexicographic GS: the box in LDS)
-  const size_t lds = sizeof(double) * (lex ? gs_lex_lds<16>() : Tl<16>::NST);
-  const dim3 g(8 * P);
-#define OMG_MID(OPV, LX)                                                                     \
-  {                                                                                          \
-    static bool attr = false;                                                                \
-    if (!attr) {                                                                             \
-      (void)hipFuncSetAttribute((const void*)k_mid<OPV, LX>,                                 \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);       \
-      attr = true;                                                                           \
-    }                                                                                        \
-    k_mid<OPV, LX><<<g, kMidBS, lds, st>>>(dA, seq);                                         \
-  }
-  if (op == OP_HELM) {
-    if (lex) OMG_MID(OP_HELM, true) else OMG_MID(OP_HELM, false)
-  } else {
-    if (lex) OMG_MID(OP_LPL, true) else OMG_MID(OP_LPL, false)
-  }
-#undef OMG_MID
-}
 
 
 }  // namespace omg

@@ -86,12 +86,12 @@ CONFIGS = {
     # cut these trees along the octree and never do)
     "ref2_gs_v": ("8 32 32 32 6 v gs lpl 0 sol sol 2 lb 0", True, [1, 3, 4]),
     "ref3_gs_f": ("8 32 32 32 5 f gs lpl 0 sol sol 3 lb 1", True, [1, 3]),
-    "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1, 3]),
+    "ref3_gsrb_v": ("8 32 32 32 5 v gsrb lpl 0 d0 sol 3 lb 0", True, [1, 2, 3, 4]),
     "c4_ref2_box16": ("16 128 128 128 4 v gs lpl 0 sol sol 2 lb 0", True, [1, 3, 4]),
     # the bench's c4_refined configuration itself (bench.py: GSRB, box 16,
     # callback Dirichlet, one refined level): k_gsrb_tile<16> with refinement
     # boundaries and the fused correction + fill on a refined level
-    "c4_ref2_box16_gsrb": ("16 128 128 128 4 v gsrb lpl 0 sol sol 2 lb 0", True, [1, 3, 4]),
+    "c4_ref2_box16_gsrb": ("16 128 128 128 4 v gsrb lpl 0 sol sol 2 lb 0", True, [1, 2, 3, 4, 8]),
     # a custom refinement_bnd callback (lb "lbrb": omg_golden.f90's custom_rb,
     # sides_rb's form with other coefficients) on the refined trees: the
     # drop-in runs it on the host after each device fill; at 3 ranks the

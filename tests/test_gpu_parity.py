@@ -258,44 +258,28 @@ def test_refinement_bnd_callback_restating_sides_rb():
     assert calls and set(calls) == set(range(1, 7))
 
 
-# the mid levels (<= OMG_MID_MAX_BOXES boxes right above the coarse tail) in
-# one launch per half-cycle (k_mid: workgroups of one XCD, a barrier between
-# box programs, every load non-temporal), with the cap at 8 (default) and 64
-MID_CASES = ["16 128 128 128 2 v gsrb lpl 0 sol sol 1 lb 0",
-             "16 128 128 128 2 v gs helm 2 d0 sol 1 lb 0",
-             "8 64 64 64 2 v gsrb lpl 0 per sol 1 lb 0",
-             "8 64 64 64 2 f gs lpl 0 n0 sol 1 lb 1",
-             "16 128 128 128 2 v gsrb lpl 0 sol sol 2 lb 0"]
+# Every runtime switch of the library (omg_ctx_create reads them; DESIGN.md
+# §12 lists them) selects another, unfused or older, path through the same
+# arithmetic: each must reproduce the reference's goldens bit for bit.  The
+# configurations cover what the switches change: a refined GSRB tree at box
+# 16 (fused down-step with refinement-boundary faces, stored coarse parts,
+# fused correction + fill on the refined level), physical faces at box 16,
+# a periodic tree (pending mean shift, skip-1 correction) and GS with FMG.
+SWITCHES = ["OMG_NO_TAIL", "OMG_NO_FUSE_UP", "OMG_NO_SKIP1", "OMG_NO_FILL_TILE", "OMG_NO_FILL_CRHS",
+            "OMG_NO_TAIL_CRHS", "OMG_NO_RBGV", "OMG_NO_FUSE_DOWN", "OMG_NO_RB_FUSE", "OMG_NO_FUSE_DOWN_BC",
+            "OMG_NO_REV"]
+SWITCH_GOLDENS = ["c4_ref2_box16_gsrb", "u64_box16_gsrb_d0_one", "per32_gsrb_v", "ref3_gs_f"]
 
 
-def _mid_launches(dev):
-    n = 0
-    for lvl in dev.levels():
-        for fam in ("mid_down", "mid_up"):
-            n += dev.mg.ctx.kernel_stats(f"{fam}@{lvl}")[0]
-    return n
-
-
-@pytest.mark.parametrize("cap", ["8", "64"])
-@pytest.mark.parametrize("args", MID_CASES)
-def test_mid_levels_match_oracle(args, cap, monkeypatch):
-    monkeypatch.setenv("OMG_MID", "1")   # opt-in: slower than launch by launch
-    monkeypatch.setenv("OMG_MID_MAX_BOXES", cap)
-    cfg = parse(args)
-    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
-    for be in (dev, orc):
-        setup_problem(be)
-    c = dev.mg.ctx
-    c.call("reset_stats")
-    c.call("set_profiling", 1)
-    for _ in range(2):
-        if cfg["cycle"] == "f":
-            assert dev.fmg(True, True) == orc.fmg(True, True)
-        else:
-            assert dev.vcycle(True) == orc.vcycle(True)
-        _assert_same(dev, orc, ivs=(1, 2, 3, 4))
-    c.call("set_profiling", 0)
-    assert _mid_launches(dev) > 0, "the mid kernel did not run"
+@pytest.mark.parametrize("name", SWITCH_GOLDENS)
+@pytest.mark.parametrize("switch", SWITCHES)
+def test_runtime_switches_match_golden(switch, name, monkeypatch):
+    monkeypatch.setenv(switch, "1")
+    e = GOLDEN[name]
+    run = e["runs"]["1"]
+    out = run_problem(e["args"], backend="device")
+    assert out["history"] == run["history"]
+    assert out["phi_sha256"] == run["phi_sha256"]
 
 
 # the coarse tail forming its top level's fill and coarse rhs itself (the

@@ -1,12 +1,10 @@
-"""Lexicographic GS with the box in a register ring (k_gs_lex_reg) and over
-compacted hyperplanes (k_gs_lex_plane), bit for bit against the C oracle on
-every stored cell.  Both read rhs from a copy (ring order / plane order), so
-the copy must follow every change of rhs: between cycles through the API, and
-inside a cycle (update_coarse rewrites the rhs of the levels below).  They
-serve 16^3 levels of at least 2048 boxes, hence the 256^3 cases;
-OMG_GS_LEX_PLANE=1 selects the plane kernel and OMG_NO_GS_PLANE=1 the
-line-per-thread kernel (both read when a context is created), which must
-agree as well.  The ring runs an even number of sweeps with two ghost-face
+"""Lexicographic GS with the box in a register ring (k_gs_lex_reg), bit for
+bit against the C oracle on every stored cell.  It reads rhs from a copy in
+ring order, so the copy must follow every change of rhs: between cycles
+through the API, and inside a cycle (update_coarse rewrites the rhs of the
+levels below).  It serves 16^3 levels of at least 2048 boxes, hence the
+256^3 cases; OMG_NO_GS_PLANE=1 selects the line-per-thread kernel (read when
+a context is created), which must agree as well.  The ring runs an even number of sweeps with two ghost-face
 sets and no fill in between (round 4; each sweep pushes its boundary layers
 into the neighbours' other set, physical ghosts formed at load, k_phys_gc
 after the last sweep); OMG_NO_GS_DBL=1 keeps the fill after every sweep."""
@@ -35,8 +33,8 @@ GS_CASES = ["16 256 256 256 1 v gs lpl 0 d0 sol 1 lb 0",
             "16 64 64 64 2 v gs lpl 0 d0 sol 1 lb 0"]
 
 
-@pytest.mark.parametrize("env", [(), ("OMG_NO_GS_DBL",), ("OMG_GS_LEX_PLANE",), ("OMG_NO_GS_PLANE",)],
-                         ids=["ring", "ring-fill", "plane", "lines"])
+@pytest.mark.parametrize("env", [(), ("OMG_NO_GS_DBL",), ("OMG_NO_FILL_XL",), ("OMG_NO_GS_PLANE",)],
+                         ids=["ring", "ring-fill", "ring-plainfill", "lines"])
 @pytest.mark.parametrize("args", GS_CASES)
 def test_gs_rhs_changes_between_cycles(args, env, monkeypatch):
     """V-cycles, then a new rhs on the finest level (upload) and on a level
