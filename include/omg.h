@@ -55,6 +55,31 @@ int omg_get_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
  * instead of RCCL (same plans, kernels and reduction orders). */
 int omg_loopback_unique_id(long long tag, void *out /* OMG_UNIQUE_ID_BYTES */);
 
+/* Host transport: fills `out` with an id that makes omg_ctx_create use the
+ * caller's own host messaging instead of RCCL; omg_set_host_transport then
+ * installs it.  For ranks that cannot use RCCL, above all several MPI ranks
+ * sharing one GPU (RCCL refuses two ranks on one device): every exchange
+ * stages its segments through pinned host memory and waits on the host.
+ * Same plans, wire order, packing kernels and reduction orders as RCCL.  The
+ * Fortran drop-in installs MPI here (m_multigrid.f90), which is the
+ * reference's own transport (sort_and_transfer_buffers,
+ * src/m_communication.f90:37-66; mpi_allreduce, src/m_multigrid.f90:232,255). */
+int omg_host_unique_id(void *out /* OMG_UNIQUE_ID_BYTES */);
+/* One grouped round: send_bufs[i] (send_counts[i] doubles) to send_peers[i],
+ * receive recv_counts[i] doubles from recv_peers[i] into recv_bufs[i]; a
+ * pair's messages arrive in the order they were sent (every rank makes the
+ * same sequence of rounds).  Returns 0 on success. */
+typedef int (*omg_host_exchange_fn)(void *user, int n_send, const int *send_peers, const long long *send_counts,
+                                    const double *const *send_bufs, int n_recv, const int *recv_peers,
+                                    const long long *recv_counts, double *const *recv_bufs);
+/* MPI_Allgather of n doubles per rank into all (n_ranks * n, rank order). */
+typedef int (*omg_host_allgather_fn)(void *user, const double *mine, int n, double *all);
+int omg_set_host_transport(omg_ctx *ctx, omg_host_exchange_fn exchange, omg_host_allgather_fn allgather,
+                           void *user);
+/* Number of visible HIP devices (a rank count above it means ranks share a
+ * GPU, where only the host transport works). */
+int omg_device_count(int *n);
+
 /* Create a context on HIP device `device` (device < 0: rank modulo the number
  * of visible devices; OMG_DEVICE_NONE: a plan-only context that builds the
  * host tables of omg_tree_setup and touches no device, for inspecting the
@@ -213,7 +238,7 @@ int omg_plan_transfer(omg_ctx *ctx, int lvl, int which, int dir, int cap, int *p
  * mg_comm_init, src/m_communication.f90:14-35, as the transport sees it):
  * *n_ranks = the ranks it joins (ncclCommCount for RCCL), *transport = one of
  * OMG_TRANSPORT_*. */
-enum { OMG_TRANSPORT_NONE = 0, OMG_TRANSPORT_RCCL = 1, OMG_TRANSPORT_LOOPBACK = 2 };
+enum { OMG_TRANSPORT_NONE = 0, OMG_TRANSPORT_RCCL = 1, OMG_TRANSPORT_LOOPBACK = 2, OMG_TRANSPORT_HOST = 3 };
 int omg_comm_info(omg_ctx *ctx, int *n_ranks, int *transport);
 
 /* Stream / timing helpers for benchmarks. */

@@ -382,6 +382,66 @@ std::vector<double> loop_allgather(omg_ctx* c, double v) {
 }
 
 // ---------------------------------------------------------------------------
+// Host transport (omg_set_host_transport): the caller's messaging (the
+// Fortran drop-in: MPI, the reference's own transport) over pinned host
+// staging.  Every round waits on the host: the segments leave the device
+// after the stream's work so far, arrive before anything queued after.
+constexpr char kHostMagic[16] = "OMG-HOSTXPRT-v1";
+
+double* host_stage(double*& p, size_t& cap, size_t n) {
+  if (n > cap) {
+    if (p) HIPCHK(hipHostFree(p));
+    p = nullptr;
+    HIPCHK(hipHostMalloc(&p, sizeof(double) * std::max<size_t>(n, 1)));
+    cap = n;
+  }
+  return p;
+}
+
+void host_exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recvbuf, hipStream_t st) {
+  if (!c->hx_exchange) throw OmgError("host transport: omg_set_host_transport was not called");
+  const size_t per = (size_t)T.item_doubles;
+  size_t ns = 0, nr = 0;
+  for (auto& p : T.send) ns = std::max(ns, ((size_t)p.offset + p.items.size() / T.send_ints) * per);
+  for (auto& p : T.recv) nr = std::max(nr, ((size_t)p.offset + p.items.size() / T.recv_ints) * per);
+  double* hs = host_stage(c->h_xsend, c->h_xsend_n, ns);
+  double* hr = host_stage(c->h_xrecv, c->h_xrecv_n, nr);
+  std::vector<int> sp, rp;
+  std::vector<long long> sn, rn;
+  std::vector<const double*> sb;
+  std::vector<double*> rb;
+  for (auto& p : T.send) {
+    const size_t n = p.items.size() / T.send_ints * per;
+    HIPCHK(hipMemcpyAsync(hs + (size_t)p.offset * per, sendbuf + (size_t)p.offset * per, n * sizeof(double),
+                          hipMemcpyDeviceToHost, st));
+    sp.push_back(p.peer);
+    sn.push_back((long long)n);
+    sb.push_back(hs + (size_t)p.offset * per);
+  }
+  for (auto& p : T.recv) {
+    rp.push_back(p.peer);
+    rn.push_back((long long)(p.items.size() / T.recv_ints * per));
+    rb.push_back(hr + (size_t)p.offset * per);
+  }
+  host_sync(c, st);
+  if (c->hx_exchange(c->hx_user, (int)sp.size(), sp.data(), sn.data(), sb.data(), (int)rp.size(), rp.data(),
+                     rn.data(), rb.data()) != 0)
+    throw OmgError("host transport: the exchange callback failed");
+  for (size_t i = 0; i < rp.size(); i++)
+    HIPCHK(hipMemcpyAsync(recvbuf + (rb[i] - hr), rb[i], (size_t)rn[i] * sizeof(double), hipMemcpyHostToDevice,
+                          st));
+  host_sync(c, st);   // (the staging is reused by the next round)
+}
+
+std::vector<double> host_allgather(omg_ctx* c, double v) {
+  if (!c->hx_allgather) throw OmgError("host transport: omg_set_host_transport was not called");
+  std::vector<double> all(c->n_ranks);
+  if (c->hx_allgather(c->hx_user, &v, 1, all.data()) != 0)
+    throw OmgError("host transport: the allgather callback failed");
+  return all;
+}
+
+// ---------------------------------------------------------------------------
 // profiling: HIP events around kernel families on the context stream
 constexpr int NO_LVL = INT_MIN;
 
@@ -447,6 +507,10 @@ void exchange(omg_ctx* c, const Transfer& T, const double* sendbuf, double* recv
   Prof prof(c, st == c->stream ? "comm" : "comm_overlap", (double)T.n_recv * T.item_doubles, lvl, st);
   if (c->loop) {
     loop_exchange(c, T, sendbuf, recvbuf, st);
+    return;
+  }
+  if (c->host_xport) {
+    host_exchange(c, T, sendbuf, recvbuf, st);
     return;
   }
   ncclComm_t comm = (ncclComm_t)c->nccl;
@@ -1120,6 +1184,8 @@ double allreduce(omg_ctx* c, double v, bool is_max) {
   std::vector<double> all(c->n_ranks);
   if (c->loop) {
     all = loop_allgather(c, v);
+  } else if (c->host_xport) {
+    all = host_allgather(c, v);
   } else {
     double* d = c->d_scalar + 8;
     c->h_scalar[1] = v;
@@ -1208,10 +1274,10 @@ void mean_device(omg_ctx* c, int ch) {
   double* all = red_all(c, ch);
   if (n == 1) {
     all = red_acc(c, ch);
-  } else if (c->loop) {
+  } else if (c->loop || c->host_xport) {
     HIPCHK(hipMemcpyAsync(c->h_scalar + 4, red_acc(c, ch), 8, hipMemcpyDeviceToHost, c->stream));
     host_sync(c, c->stream);
-    std::vector<double> v = loop_allgather(c, c->h_scalar[4]);
+    std::vector<double> v = c->loop ? loop_allgather(c, c->h_scalar[4]) : host_allgather(c, c->h_scalar[4]);
     for (int r = 0; r < n; r++) c->h_scalar[8 + r] = v[r];
     HIPCHK(hipMemcpyAsync(all, c->h_scalar + 8, 8 * n, hipMemcpyHostToDevice, c->stream));
   } else {
@@ -2580,6 +2646,26 @@ int omg_loopback_unique_id(long long tag, void* out) {
   });
 }
 
+int omg_host_unique_id(void* out) {
+  return guarded([&] {
+    std::memset(out, 0, OMG_UNIQUE_ID_BYTES);
+    std::memcpy(out, kHostMagic, sizeof(kHostMagic));
+  });
+}
+
+int omg_set_host_transport(omg_ctx* c, omg_host_exchange_fn exchange, omg_host_allgather_fn allgather, void* user) {
+  return guarded([&] {
+    if (!c->host_xport) throw OmgError("omg_set_host_transport: the context was not created with omg_host_unique_id");
+    c->hx_exchange = exchange;
+    c->hx_allgather = allgather;
+    c->hx_user = user;
+  });
+}
+
+int omg_device_count(int* n) {
+  return guarded([&] { HIPCHK(hipGetDeviceCount(n)); });
+}
+
 int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void* unique_id) {
   return guarded([&] {
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw OmgError("bad rank / n_ranks");
@@ -2668,6 +2754,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
       }
       if (g->n_ranks != n_ranks) throw OmgError("loopback group: n_ranks mismatch");
       c->loop = g;
+    } else if (n_ranks > 1 && std::memcmp(unique_id, kHostMagic, sizeof(kHostMagic)) == 0) {
+      c->host_xport = true;   // the callbacks come with omg_set_host_transport
     } else if (n_ranks > 1) {
       ncclUniqueId id;
       std::memcpy(&id, unique_id, sizeof(id));
@@ -2712,6 +2800,8 @@ int omg_ctx_destroy(omg_ctx* c) {
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
+    if (c->h_xsend) (void)hipHostFree(c->h_xsend);
+    if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
     if (c->nccl) (void)ncclCommDestroy((ncclComm_t)c->nccl);
     if (c->loop) {   // the last context of a loopback group removes it
       std::lock_guard<std::mutex> lk(g_loop_mu);
@@ -3116,6 +3206,9 @@ int omg_comm_info(omg_ctx* c, int* n_ranks, int* transport) {
     } else if (c->loop) {
       *n_ranks = c->loop->n_ranks;
       *transport = OMG_TRANSPORT_LOOPBACK;
+    } else if (c->host_xport) {
+      *n_ranks = c->n_ranks;
+      *transport = OMG_TRANSPORT_HOST;
     } else {
       *n_ranks = c->n_ranks;
       *transport = OMG_TRANSPORT_NONE;

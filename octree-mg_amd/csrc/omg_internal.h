@@ -20,6 +20,8 @@
 #include <string>
 #include <vector>
 
+#include "../../include/omg.h"   // (the host-transport callback types)
+
 namespace omg {
 
 // NB_RBREM: refinement boundary whose coarse neighbour lives on another rank;
@@ -321,6 +323,15 @@ struct omg_ctx {
   // they change
   omg::TailArgs* d_tail = nullptr;
   omg::TailArgs* h_tail = nullptr;   // the last uploaded copy (host)
+  // host transport (omg_set_host_transport): the caller's messaging, staged
+  // through pinned host memory
+  bool host_xport = false;
+  omg_host_exchange_fn hx_exchange = nullptr;
+  omg_host_allgather_fn hx_allgather = nullptr;
+  void* hx_user = nullptr;
+  double* h_xsend = nullptr;
+  double* h_xrecv = nullptr;
+  size_t h_xsend_n = 0, h_xrecv_n = 0;
   bool tail_timing = false;             // OMG_TAIL_TIMING: print the tail's phase times
   long long* d_tail_stamps = nullptr;
   double* h_scalar = nullptr;          // pinned host scratch

@@ -23,6 +23,9 @@ SIGNATURES = {
     "omg_last_error": (C.c_char_p, []),
     "omg_get_unique_id": (_I, [C.c_char_p]),
     "omg_loopback_unique_id": (_I, [C.c_longlong, C.c_char_p]),
+    "omg_host_unique_id": (_I, [C.c_char_p]),
+    "omg_set_host_transport": (_I, [_P, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "omg_device_count": (_I, [C.POINTER(_I)]),
     "omg_plan_transfer": (_I, [_P, _I, _I, _I, _I, _IP, C.POINTER(C.c_longlong), C.POINTER(_I),
                                C.POINTER(_I)]),
     "omg_ctx_create": (_I, [C.POINTER(_P), _I, _I, _I, C.c_char_p]),

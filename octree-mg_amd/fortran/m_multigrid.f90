@@ -46,6 +46,9 @@ module m_multigrid
   integer(c_int), allocatable :: ctx_key(:)
   real(c_double), allocatable :: ctx_key_dr(:)
 
+  !> The communicator of the host transport (mpi_exchange, mpi_allgather_dp)
+  integer :: xport_comm = MPI_COMM_NULL
+
   !> Resident mode (opt-in, see mg_gpu_set_resident): the data stays on the
   !> GPU between calls instead of round-tripping through mg%boxes(:)%cc.
   logical :: resident = .false.
@@ -357,7 +360,12 @@ contains
        key(o + id)              = mg%boxes(id)%lvl
        key(o + n + id)          = mg%boxes(id)%parent
        key(o + 2*n + 8*(id-1) + 1 : o + 2*n + 8*id)   = mg%boxes(id)%children
-       key(o + 10*n + 6*(id-1) + 1 : o + 10*n + 6*id) = mg%boxes(id)%neighbors
+       ! physical faces as mg_physical_boundary: the bc type that
+       ! mg_phi_bc_store / mg_poisson_free_3d write into those slots
+       ! (m_ghost_cells.f90:66-78) is device state that omg_phi_bc_store
+       ! keeps, not a change of the tree
+       key(o + 10*n + 6*(id-1) + 1 : o + 10*n + 6*id) = &
+            merge(mg_physical_boundary, mg%boxes(id)%neighbors, mg%boxes(id)%neighbors < mg_no_box)
        key(o + 16*n + 3*(id-1) + 1 : o + 16*n + 3*id) = mg%boxes(id)%ix
        key(o + 19*n + id)       = mg%boxes(id)%rank
     end do
@@ -415,6 +423,7 @@ contains
     integer(c_int), allocatable  :: key(:)
     real(c_double), allocatable  :: dr(:)
     integer                      :: n, nlev, o, ierr
+    logical                      :: host_xport
 
 #if NDIM != 3
     error stop "octree-mg GPU backend: only NDIM == 3 is supported"
@@ -429,12 +438,23 @@ contains
     if (allocated(ctx_key)) deallocate(ctx_key)
 
     uid = 0
+    host_xport = .false.
     if (mg%n_cpu > 1) then
-       if (mg%my_rank == 0) call omg_ok(omg_get_unique_id(uid), "get_unique_id")
-       call mpi_bcast(uid, omg_unique_id_bytes, MPI_BYTE, 0, mg%comm, ierr)
+       host_xport = use_host_transport(mg)
+       if (host_xport) then
+          call omg_ok(omg_host_unique_id(uid), "host_unique_id")
+       else
+          if (mg%my_rank == 0) call omg_ok(omg_get_unique_id(uid), "get_unique_id")
+          call mpi_bcast(uid, omg_unique_id_bytes, MPI_BYTE, 0, mg%comm, ierr)
+       end if
     end if
     call omg_ok(omg_ctx_create(ctx, -1_c_int, int(mg%my_rank, c_int), &
          int(mg%n_cpu, c_int), uid), "ctx_create")
+    if (host_xport) then
+       xport_comm = mg%comm
+       call omg_ok(omg_set_host_transport(ctx, c_funloc(mpi_exchange), c_funloc(mpi_allgather_dp), &
+            c_null_ptr), "set_host_transport")
+    end if
 
     call tree_key(mg, key, dr)
     n = mg%n_boxes
@@ -625,6 +645,71 @@ contains
     call omg_ok(omg_set_bc_faces(ctx, int(iv, c_int), face_off, face_type, data, n_data), &
          "set_bc_faces")
   end subroutine tabulate_bc
+
+  !> The transport of a multi-rank context.  RCCL (xGMI) when every rank has
+  !> a GPU of its own; the host transport over MPI, the reference's own
+  !> transport (sort_and_transfer_buffers, m_communication.f90:37-66;
+  !> mpi_allreduce, m_multigrid.f90:232,255), when ranks share a GPU (RCCL
+  !> refuses two ranks on one device) or when OMG_TRANSPORT=host is set.
+  !> Decided alike on every rank.
+  logical function use_host_transport(mg)
+    type(mg_t), intent(in) :: mg
+    integer(c_int)         :: nd
+    integer                :: mine, lowest, ierr, ln, st
+    character(len=16)      :: env
+    call get_environment_variable("OMG_TRANSPORT", env, ln, st)
+    mine = 0
+    if (st == 0 .and. trim(env) == "host") mine = 1
+    call omg_ok(omg_device_count(nd), "device_count")
+    if (nd < mg%n_cpu) mine = 1
+    call mpi_allreduce(mine, lowest, 1, MPI_INTEGER, MPI_MAX, mg%comm, ierr)
+    use_host_transport = lowest == 1
+  end function use_host_transport
+
+  !> omg_host_exchange_fn over MPI: nonblocking sends and receives of one
+  !> round, then a wait on all (messages of a pair keep their order: same
+  !> communicator, same tag).
+  integer(c_int) function mpi_exchange(user, n_send, send_peers, send_counts, send_bufs, &
+       n_recv, recv_peers, recv_counts, recv_bufs) bind(C)
+    type(c_ptr), value            :: user
+    integer(c_int), value         :: n_send, n_recv
+    integer(c_int), intent(in)    :: send_peers(*), recv_peers(*)
+    integer(c_long_long), intent(in) :: send_counts(*), recv_counts(*)
+    type(c_ptr), intent(in)       :: send_bufs(*), recv_bufs(*)
+    real(c_double), pointer       :: buf(:)
+    integer, allocatable          :: req(:)
+    integer                       :: i, ierr, nreq
+    integer, parameter            :: tag = 7291
+
+    allocate(req(max(n_send + n_recv, 1)))
+    nreq = 0
+    do i = 1, n_recv
+       call c_f_pointer(recv_bufs(i), buf, [recv_counts(i)])
+       nreq = nreq + 1
+       call mpi_irecv(buf, int(recv_counts(i)), MPI_DOUBLE_PRECISION, int(recv_peers(i)), tag, &
+            xport_comm, req(nreq), ierr)
+    end do
+    do i = 1, n_send
+       call c_f_pointer(send_bufs(i), buf, [send_counts(i)])
+       nreq = nreq + 1
+       call mpi_isend(buf, int(send_counts(i)), MPI_DOUBLE_PRECISION, int(send_peers(i)), tag, &
+            xport_comm, req(nreq), ierr)
+    end do
+    call mpi_waitall(nreq, req, MPI_STATUSES_IGNORE, ierr)
+    mpi_exchange = int(ierr, c_int)
+  end function mpi_exchange
+
+  !> omg_host_allgather_fn over MPI
+  integer(c_int) function mpi_allgather_dp(user, mine, n, all) bind(C)
+    type(c_ptr), value         :: user
+    integer(c_int), value      :: n
+    real(c_double), intent(in) :: mine(n)
+    real(c_double), intent(out) :: all(*)
+    integer                    :: ierr
+    call mpi_allgather(mine, int(n), MPI_DOUBLE_PRECISION, all, int(n), MPI_DOUBLE_PRECISION, &
+         xport_comm, ierr)
+    mpi_allgather_dp = int(ierr, c_int)
+  end function mpi_allgather_dp
 
   !> The device's refinement_bnd hand-back (omg_set_refinement_bnd): for
   !> each record, the box's variable iv (reference layout) goes into

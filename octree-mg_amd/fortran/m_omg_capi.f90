@@ -13,6 +13,7 @@ module m_omg_capi
 
   public :: omg_error_message
   public :: omg_get_unique_id, omg_ctx_create, omg_ctx_destroy
+  public :: omg_host_unique_id, omg_set_host_transport, omg_device_count
   public :: omg_tree_setup, omg_set_operator, omg_set_smoother
   public :: omg_set_subtract_mean, omg_set_bc, omg_set_bc_faces
   public :: omg_level_size, omg_upload_level, omg_download_level
@@ -32,6 +33,27 @@ module m_omg_capi
        integer(c_int8_t), intent(out) :: out(*)
        integer(c_int) :: ierr
      end function omg_get_unique_id
+
+     function omg_host_unique_id(out) bind(C, name="omg_host_unique_id") result(ierr)
+       import :: c_int, c_int8_t
+       integer(c_int8_t), intent(out) :: out(*)
+       integer(c_int) :: ierr
+     end function omg_host_unique_id
+
+     function omg_set_host_transport(ctx, exchange, allgather, user) &
+          bind(C, name="omg_set_host_transport") result(ierr)
+       import :: c_ptr, c_int, c_funptr
+       type(c_ptr), value    :: ctx
+       type(c_funptr), value :: exchange, allgather
+       type(c_ptr), value    :: user
+       integer(c_int) :: ierr
+     end function omg_set_host_transport
+
+     function omg_device_count(n) bind(C, name="omg_device_count") result(ierr)
+       import :: c_int
+       integer(c_int), intent(out) :: n
+       integer(c_int) :: ierr
+     end function omg_device_count
 
      function omg_ctx_create(ctx, device, rank, n_ranks, unique_id) &
           bind(C, name="omg_ctx_create") result(ierr)

@@ -75,6 +75,54 @@ def test_dropin_golden(name):
                 assert hashlib.sha256(f.read()).hexdigest() == ref[key]
 
 
+MPIEXEC = "/opt/conda/bin/mpiexec"
+# every configuration the reference ran at 2-4 ranks, at the largest such
+# count (5, 6 and 8 ranks stay with the loopback replay,
+# tests/test_gpu_multirank.py)
+MULTI = sorted({n: max(int(r) for r in e["runs"] if 1 < int(r) <= 4)
+                for n, e in GOLDEN.items()
+                if not e.get("big") and any(1 < int(r) <= 4 for r in e["runs"])}.items())
+
+
+def _rank_dumps(fn):
+    """The golden driver's per-rank dumps (<fn>.r<rank>) in the one-rank
+    order (tests/golden/make_golden.py read_rank_dumps)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(ROOT, "tests", "golden",
+                                                                              "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg.read_rank_dumps(fn)
+
+
+@pytest.mark.gpu
+@needs_driver
+@pytest.mark.parametrize("name,ranks", MULTI)
+def test_dropin_golden_multirank(name, ranks):
+    """`mpiexec -n R` of the golden driver linked against the drop-in: R MPI
+    ranks on one GPU, which RCCL refuses, so the drop-in takes the host
+    transport over MPI (include/omg.h omg_set_host_transport; same plans,
+    packing kernels and reduction orders as RCCL).  The printed history and
+    every rank's final phi must be the reference's R-rank run, bit for bit:
+    the Fortran drop-in's multi-rank bookkeeping (ranks, my_ids uploads and
+    downloads, collective calls) end to end."""
+    run = GOLDEN[name]["runs"][str(ranks)]
+    key = "phi_sha256" if "phi_sha256" in run else "rhs_sha256" if "rhs_sha256" in run else None
+    with tempfile.TemporaryDirectory() as td:
+        dump = os.path.join(td, "dump.bin") if key else None
+        cmd = [MPIEXEC, "-n", str(ranks), DRIVER] + GOLDEN[name]["args"].split() + [dump or "x"]
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        if "error" in run:
+            assert p.returncode != 0
+            assert "ERROR STOP: " + run["error"] in p.stdout + p.stderr
+            assert parse(p.stdout) == run["history"]
+            return
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+        assert parse(p.stdout) == run["history"]
+        if dump:
+            assert hashlib.sha256(_rank_dumps(dump)).hexdigest() == run[key]
+
+
 REF_PROGRAMS = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_programs.json")))["runs"]
 
 
@@ -88,7 +136,9 @@ def test_reference_programs_unchanged(name):
     exe = os.path.join(BUILD, run["program"])
     if not os.path.exists(exe):
         pytest.skip("Fortran drop-in not built")
-    p = subprocess.run([exe] + run["args"].split(), capture_output=True, text=True, timeout=300)
+    ranks = run.get("ranks", 1)   # `mpiexec -n 4 test_refinement`: 4 ranks on one GPU, host transport
+    cmd = ([MPIEXEC, "-n", str(ranks)] if ranks > 1 else []) + [exe] + run["args"].split()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     lines = [ln.rstrip() for ln in p.stdout.splitlines()
              if "max solution error" in ln or "max err" in ln]
