@@ -510,7 +510,9 @@ def main():
         return
     import torch
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        # (more ranks than GPUs: they share, and the library takes its host
+        # transport, octree-mg_amd/mg.py _use_host_transport)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
 
     domain = domain_for(a.mode, world)
     main_run = run_c3(omg, domain, dist, rank, world, local_rank, a.steps, a.warmup,

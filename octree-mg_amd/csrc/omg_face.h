@@ -21,6 +21,9 @@ __device__ __forceinline__ void st_nt(double* p, double x, double y) {
   v2d t = {x, y};
   __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(p));
 }
+__device__ __forceinline__ void st_v2(double* p, double x, double y) {
+  *reinterpret_cast<v2d*>(p) = v2d{x, y};
+}
 
 // The seven stencil values of two neighbouring same-colour cells of one row
 // (colour indices ih, ih+1, ih even) of colour e, from a stored box in LDS:

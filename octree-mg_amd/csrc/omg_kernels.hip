@@ -429,6 +429,13 @@ __device__ __forceinline__ double dpp_row_prev(double v, double old) {
   const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x111, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
 }
+// the value of the lane two further on in this lane's 16-lane row (row_shl:2;
+// the last two lanes of the row get their own value, unused)
+__device__ __forceinline__ double dpp_row_shl2(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), 0x102, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x102, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double dpp_row_next(double v, double old) {
   const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x101, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x101, 0xf, 0xf, false);
@@ -678,22 +685,41 @@ __global__ void __launch_bounds__(64, 2) k_gs_lex_reg(LevelView L, double lambda
       // ghosts of the other set: x faces from this lane's line, y faces from
       // the j = 1 / 16 lanes, z faces from planes k = 1 (line 0, group 0)
       // and k = 16 (line 3, group 3)
+      // Every push is a 16-B pair: the two same-colour cells a and a+2 of a
+      // face row are adjacent in the stored face (index (a-1)>>1).  Along a
+      // 16-lane row the partner is the lane two further on (DPP row_shl:2),
+      // and the lanes whose index is even store the pair.
       const int kr = 4 * kq + r + 1;
-      auto push = [&](int f, int a, int c, double v) {   // toward face f+1's neighbour
-        const int nbo = (f & 1) ? f : f + 2;               // the neighbour's opposite face
-        gs.out[(long long)T.arg(f) * gs.out_stride + TL::ogh(nbo, a, c) - 2 * HV] = v;
+      auto push2 = [&](int f, int a, int c, double v0, double v1) {   // toward face f+1's neighbour
+        const int nbo = (f & 1) ? f : f + 2;                           // the neighbour's opposite face
+        st_v2(gs.out + (long long)T.arg(f) * gs.out_stride + TL::ogh(nbo, a, c) - 2 * HV, v0, v1);
       };
-      if (T.kind(0) == NB_LOCAL) push(0, j, kr, stage[((1 + j + kr) % R) * SR + l]);
-      if (T.kind(1) == NB_LOCAL) push(1, j, kr, stage[((NC + j + kr) % R) * SR + l]);
+      const bool pair_lane = !(((l & 15) >> 1) & 1);   // index ((l & 15)) >> 1 even
+      if (T.kind(0) == NB_LOCAL) {
+        const double v = stage[((1 + j + kr) % R) * SR + l], w = dpp_row_shl2(v);
+        if (pair_lane) push2(0, j, kr, v, w);
+      }
+      if (T.kind(1) == NB_LOCAL) {
+        const double v = stage[((NC + j + kr) % R) * SR + l], w = dpp_row_shl2(v);
+        if (pair_lane) push2(1, j, kr, v, w);
+      }
       const int a = (l & 15) + 1, gq = l >> 4, kg = 4 * gq + r + 1, lg = 16 * lex_grp(gq);
-      if (T.kind(2) == NB_LOCAL) push(2, a, kg, stage[((a + 1 + kg) % R) * SR + lg]);
-      if (T.kind(3) == NB_LOCAL) push(3, a, kg, stage[((a + NC + kg) % R) * SR + lg + 15]);
+      if (T.kind(2) == NB_LOCAL) {
+        const double v = stage[((a + 1 + kg) % R) * SR + lg], w = dpp_row_shl2(v);
+        if (pair_lane) push2(2, a, kg, v, w);
+      }
+      if (T.kind(3) == NB_LOCAL) {
+        const double v = stage[((a + NC + kg) % R) * SR + lg + 15], w = dpp_row_shl2(v);
+        if (pair_lane) push2(3, a, kg, v, w);
+      }
       if ((r == 0 && T.kind(4) == NB_LOCAL) || (r == 3 && T.kind(5) == NB_LOCAL)) {
+        // a lane's four cells i = 4q+1 .. 4q+4: the two of each colour are
+        // i and i+2, one pair per colour
         const int ln = (j - 1) + (r == 0 ? 0 : 16 * lex_grp(3)), k0 = r == 0 ? 1 : NC;
 #pragma unroll
-        for (int ii = 0; ii < 4; ii++) {
+        for (int ii = 0; ii < 2; ii++) {
           const int i = 4 * (l >> 4) + ii + 1;
-          push(r == 0 ? 4 : 5, i, j, stage[((i + j + k0) % R) * SR + ln]);
+          push2(r == 0 ? 4 : 5, i, j, stage[((i + j + k0) % R) * SR + ln], stage[((i + 2 + j + k0) % R) * SR + ln]);
         }
       }
     }

@@ -120,6 +120,30 @@ def loopback_unique_id(tag: int) -> bytes:
     return buf.raw
 
 
+def host_unique_id() -> bytes:
+    """Id that selects the host transport (omg_host_unique_id)."""
+    buf = C.create_string_buffer(128)
+    check(lib().omg_host_unique_id(buf))
+    return buf.raw
+
+
+def device_count() -> int:
+    n = _I()
+    check(lib().omg_device_count(C.byref(n)))
+    return n.value
+
+
+# omg_host_exchange_fn / omg_host_allgather_fn (include/omg.h)
+_XCHG_FN = C.CFUNCTYPE(_I, C.c_void_p, _I, C.POINTER(_I), C.POINTER(C.c_longlong), C.POINTER(C.c_void_p),
+                       _I, C.POINTER(_I), C.POINTER(C.c_longlong), C.POINTER(C.c_void_p))
+_AGATH_FN = C.CFUNCTYPE(_I, C.c_void_p, C.POINTER(_D), _I, C.POINTER(_D))
+
+
+def _host_view(ptr, n):
+    """A float64 numpy view of n doubles of pinned host staging."""
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(_D)), shape=(int(n),))
+
+
 class Context:
     """One device context (one rank, one GPU)."""
 
@@ -141,6 +165,41 @@ class Context:
             pass
 
     after_call = None   # e.g. re-raise what a host callback raised during the call
+
+    def set_host_transport(self, group=None):
+        """The host transport over torch.distributed (gloo, CPU tensors):
+        omg_set_host_transport with an isend / irecv round and an all_gather
+        (the ranks share a GPU, which RCCL refuses).  Messages of a pair keep
+        their order (one group, one tag)."""
+        import torch
+        import torch.distributed as dist
+
+        def exchange(user, ns, sp, sn, sb, nr, rp, rn, rb):
+            try:
+                reqs = [dist.irecv(torch.from_numpy(_host_view(rb[i], rn[i])), src=int(rp[i]), group=group)
+                        for i in range(nr)]
+                reqs += [dist.isend(torch.from_numpy(_host_view(sb[i], sn[i])), dst=int(sp[i]), group=group)
+                         for i in range(ns)]
+                for r in reqs:
+                    r.wait()
+                return 0
+            except Exception:   # noqa: BLE001  (the library raises "the exchange callback failed")
+                return 1
+
+        def allgather(user, mine, n, out):
+            try:
+                world = dist.get_world_size(group)
+                t = torch.from_numpy(np.array(_host_view(C.cast(mine, C.c_void_p), n)))
+                parts = [torch.empty_like(t) for _ in range(world)]
+                dist.all_gather(parts, t, group=group)
+                _host_view(C.cast(out, C.c_void_p), n * world)[:] = torch.cat(parts).numpy()
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+
+        self._xport = (_XCHG_FN(exchange), _AGATH_FN(allgather))   # (kept alive with the context)
+        check(self.L.omg_set_host_transport(self.h, C.cast(self._xport[0], C.c_void_p),
+                                            C.cast(self._xport[1], C.c_void_p), None))
 
     def call(self, name, *args):
         check(getattr(self.L, "omg_" + name)(self.h, *args))
@@ -192,7 +251,7 @@ class Context:
         "rccl" (ncclCommCount) or "loopback" (omg_comm_info)."""
         n, t = _I(), _I()
         self.call("comm_info", C.byref(n), C.byref(t))
-        return n.value, {0: "none", 1: "rccl", 2: "loopback"}[t.value]
+        return n.value, {0: "none", 1: "rccl", 2: "loopback", 3: "host"}[t.value]
 
     def host_sync_count(self):
         """Host waits on the context's streams so far (omg_host_sync_count)."""

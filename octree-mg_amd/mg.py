@@ -281,15 +281,25 @@ def mg_allocate_storage(mg: MG, device_index=None):
     if device_index is None:
         device_index = int(os.environ.get("LOCAL_RANK", mg.device_index if mg.n_cpu == 1 else 0))
     uid = None
+    host = False
     if isinstance(mg.comm, Loopback):
         uid = device.loopback_unique_id(mg.comm.tag) if mg.comm.n_ranks > 1 else None
         device_index = 0
     elif mg.n_cpu > 1:
         import torch.distributed as dist
-        obj = [device.unique_id() if mg.my_rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+        host = _use_host_transport(mg)
+        if host:
+            # ranks share a GPU (RCCL refuses that): the host transport over
+            # the torch.distributed group, rank r on GPU r mod ndev
+            uid = device.host_unique_id()
+            device_index = mg.my_rank % max(device.device_count(), 1)
+        else:
+            obj = [device.unique_id() if mg.my_rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
     mg.ctx = device.Context(device_index, mg.my_rank, mg.n_cpu, uid)
+    if host:
+        mg.ctx.set_host_transport(mg.comm)
     if mg.coarse_replication_cells:
         mg.ctx.call("set_coarse_replication", int(mg.coarse_replication_cells))
     arrs = _tree_arrays(mg)
@@ -298,6 +308,17 @@ def mg_allocate_storage(mg: MG, device_index=None):
     mg.is_allocated = True
     mg._push_methods()
     mg.push_bc()
+
+
+def _use_host_transport(mg: MG) -> bool:
+    """The host transport when the ranks outnumber the visible GPUs or
+    OMG_TRANSPORT=host; agreed over the group (as the Fortran drop-in does)."""
+    import torch
+    import torch.distributed as dist
+    want = os.environ.get("OMG_TRANSPORT") == "host" or device.device_count() < mg.n_cpu
+    t = torch.tensor([1 if want else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=mg.comm)
+    return bool(t[0])
 
 
 def mg_deallocate_storage(mg: MG):

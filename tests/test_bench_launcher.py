@@ -78,3 +78,15 @@ def test_cpu_baseline_timeout_leaves_no_process(tmp_path):
             break
         time.sleep(0.1)
     assert alive() == 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    """The N > 1 bench path end to end on real hardware before the driver's
+    multi-GPU run: `bench.py --gpus 2` on a one-GPU box starts two ranks that
+    share the GPU, so the library takes the host transport over the gloo
+    group (RCCL refuses two ranks on one device); the line must report two
+    GPUs, the host transport and the weak-scaling workload."""
+    out = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--mode", "weak256", "--no-cpu-baseline")
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["value"] > 0
+    assert out["comm"]["transport"] == "host", out["comm"]

@@ -4,7 +4,7 @@ mkdir -p gpurun_out/r05
 OMG_LIB=$PWD/octree-mg_amd/_variants/libomg_r05_before.so timeout -k 10 120 python tools/c4_launch_counts.py 4 > gpurun_out/r05/s5_c4_launches_4ranks_before.txt 2>&1 || exit 1
 timeout -k 10 120 python tools/c4_launch_counts.py 4 > gpurun_out/r05/s5_c4_launches_4ranks_after.txt 2>&1 || exit 1
 paste gpurun_out/r05/s5_c4_launches_4ranks_before.txt gpurun_out/r05/s5_c4_launches_4ranks_after.txt | cut -c1-160
-timeout -k 10 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py tests/test_fortran_dropin.py tests/test_gpu_smoothers.py tests/test_gpu_parity.py tests/test_gpu_free_space.py tests/test_gpu_failures.py -m gpu > gpurun_out/r05/s5_pytest_gpu.log 2>&1
+timeout -k 10 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r05/s5_pytest_gpu.log 2>&1
 rc=$?
 tail -3 gpurun_out/r05/s5_pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
