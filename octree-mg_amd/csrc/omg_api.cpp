@@ -1114,7 +1114,8 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
     {
       Prof p(c, "prolong_fill", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl + 1);
       launch_prolong_fill(C->view(), F->sweep_view(), 4, F->d_parent_local, F->d_dix, bc_for(c, lvl + 1, 1),
-                          F->d_sendbuf, true, !c->no_skip1, c->stream, F->d_bnd, F->n_bnd);
+                          F->d_sendbuf, true, !c->no_skip1, c->stream, F->d_bnd, F->n_bnd, false,
+                          F->h_rb.empty() ? nullptr : F->d_rb);
     }
     finish_halo(c, F, 1);
     {

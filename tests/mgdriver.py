@@ -532,18 +532,19 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
     def body(be, rank, reduce):
         hist = _cycles(be, cfg, reduce)
         be.mg.ctx.call("synchronize")
-        return hist, _owned_phi(be), be.tree
+        t = be.tree   # (copied: run_loopback frees the storage, which empties the level lists)
+        order = [(lvl, [int(i) for i in t.lvls[lvl].ids]) for lvl in range(t.lowest_lvl, t.highest_lvl + 1)]
+        return hist, _owned_phi(be), (order, t.rank.copy())
 
     res = run_loopback(args, n_ranks, body, n_its, timeout, rep_cells)
     out = [r[0] for r in res]
     phis = [r[1] for r in res]
-    trees = [r[2] for r in res]
+    order, owners = res[0][2]
     assert all(h == out[0] for h in out)
-    tree = trees[0]
     h = hashlib.sha256()
-    for lvl in range(tree.lowest_lvl, tree.highest_lvl + 1):
-        for id_ in tree.lvls[lvl].ids:
-            key = (lvl, int(id_))
-            owner = int(tree.rank[id_])
+    for lvl, ids in order:
+        for id_ in ids:
+            key = (lvl, id_)
+            owner = int(owners[id_])
             h.update(phis[owner][key] if key in phis[owner] else phis[0][key])
     return {"history": out[0], "phi_sha256": h.hexdigest()}
