@@ -798,6 +798,19 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     if (n == 1 && absorb) phi_mean_ready(c);
     const double* shift = (n == 1 && absorb) ? red_mean(c, 0) : nullptr;
     if (n == 1) L->shift_pending = false;
+    // substeps n, n+1, n+2 in one pass (k_gsrb3) into phi's other buffer: it
+    // reads the neighbours' cells in their boxes, which equal its ghosts only
+    // when they are consistent (phi_gc_ok), and writes every ghost face
+    if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
+      double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
+      {
+        Prof p(c, "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
+        launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
+      }
+      L->d_phi = other;
+      n += 2;
+      continue;
+    }
     if (L->n_bnd && L->n_int && !odd && gs_tiled(L->nc, c->op, L->has_rb)) {
       // boxes with faces on other GPUs first; their halo travels on the comm
       // stream while the interior boxes run (the substep reads only its own
@@ -2254,6 +2267,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
     dfree(L.d_galt);
+    dfree(L.d_phi_buf); dfree(L.d_b3); L.n_b3 = 0;
     dfree(L.d_physbox);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0); dfree(L.d_bndface);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
@@ -2271,6 +2285,71 @@ void free_levels(omg_ctx* c) {
     c->h_face_type_lvl[iv].clear();
     dfree(c->d_face_data[iv]);
   }
+}
+
+// k_gsrb3's columns (launch_gsrb3): a level of at least kB3MinBoxes boxes of
+// 16^3 whose faces are all same-GPU boxes of the level (a periodic uniform
+// level on one GPU) is tiled by columns of kB3TX boxes in x and up to kB3MaxZ
+// in z, each with the boxes around it; the level then gets phi's second
+// buffer.  Columns are ordered by z block, then Morton order in x / y, so that
+// each XCD's run of workgroups (xcd_box) is one compact patch whose halo
+// columns its own L2 holds.  Any face or tiling that does not fit: no records.
+void build_block3(omg_ctx* c, Level& L) {
+  if (g_host_only || c->host_only || L.nc != 16 || L.n < kB3MinBoxes || L.replicated) return;
+  for (int8_t k : L.h_nbk)
+    if (k != NB_LOCAL) return;
+  const int n = L.n;
+  // face f: 0 x-, 1 x+, 2 y-, 3 y+, 4 z-, 5 z+
+  auto nb = [&](int b, int f) { return L.h_nba[(size_t)b * 6 + f]; };
+  auto ixd = [&](int b, int d) { return c->ix[(size_t)(L.ids[b] - 1) * 3 + d] - 1; };
+  auto spread = [](unsigned v) {
+    unsigned long long r = 0;
+    for (int q = 0; q < 20; q++) r |= (unsigned long long)((v >> q) & 1u) << (2 * q);
+    return r;
+  };
+  std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
+  std::vector<int> covered(n, 0);
+  for (int h = 0; h < n; h++) {
+    if (ixd(h, 0) % kB3TX || ixd(h, 2) % kB3MaxZ) continue;
+    std::vector<int> zc{h};
+    while ((int)zc.size() < kB3MaxZ) {
+      const int up = nb(zc.back(), 5);
+      if (ixd(up, 2) % kB3MaxZ == 0) break;   // the next column's first box
+      zc.push_back(up);
+    }
+    const int len = (int)zc.size();
+    std::vector<int> r(kB3Rec, 0);
+    r[0] = len;
+    for (int zs = 0; zs <= len + 1; zs++) {
+      const int cb = zs == 0 ? nb(zc[0], 4) : (zs == len + 1 ? nb(zc[len - 1], 5) : zc[zs - 1]);
+      int* row = &r[1 + kB3S * zs];
+      // the tile's row of boxes along x, then the rows below and above it in
+      // y; a grid: the rows' x neighbours agree with the y neighbours' chain
+      row[kB3TX + 2] = nb(cb, 0);
+      for (int xs = 1; xs <= kB3TX + 1; xs++) row[(kB3TX + 2) + xs] = xs == 1 ? cb : nb(row[(kB3TX + 2) + xs - 1], 1);
+      for (int xs = 0; xs < kB3TX + 2; xs++) {
+        const int mid = row[(kB3TX + 2) + xs];
+        row[xs] = nb(mid, 2);
+        row[2 * (kB3TX + 2) + xs] = nb(mid, 3);
+        if (zs >= 1 && zs <= len && xs >= 1 && xs <= kB3TX) covered[mid]++;
+      }
+      for (int ys = 0; ys < 3; ys += 2)
+        for (int xs = 0; xs + 1 < kB3TX + 2; xs++)
+          if (nb(row[(kB3TX + 2) * ys + xs], 1) != row[(kB3TX + 2) * ys + xs + 1]) return;
+    }
+    const unsigned long long key = ((unsigned long long)(ixd(h, 2) / kB3MaxZ) << 40) |
+                                   (spread((unsigned)(ixd(h, 0) / kB3TX)) | (spread((unsigned)ixd(h, 1)) << 1));
+    cols.emplace_back(key, std::move(r));
+  }
+  for (int b = 0; b < n; b++)
+    if (covered[b] != 1) return;
+  std::sort(cols.begin(), cols.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<int> flat;
+  flat.reserve(cols.size() * kB3Rec);
+  for (auto& cr : cols) flat.insert(flat.end(), cr.second.begin(), cr.second.end());
+  L.n_b3 = (int)cols.size();
+  L.d_b3 = to_device(flat);
+  dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)L.n * L.stride, true);
 }
 
 void build_plan(omg_ctx* c) {
@@ -2488,6 +2567,7 @@ void build_plan(omg_ctx* c) {
       }
     }
     L.d_phi = L.d_data;
+    build_block3(c, L);
     L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);
     L.d_nba = to_device(L.h_nba);
@@ -2705,6 +2785,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
+    c->no_block3 = env_flag("OMG_NO_BLOCK3");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

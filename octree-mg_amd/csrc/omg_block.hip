@@ -1,0 +1,307 @@
+// omg_block.hip — three red-black substeps of a level in one pass (k_gsrb3).
+//
+// smooth_boxes (m_multigrid.f90:404-424) runs substeps e, 1-e, e with a ghost
+// fill after each; every substep of the one-substep kernel (omg_sweep.hip)
+// streams half of phi and half of rhs in and half of phi out (12 B per cell
+// plus the ghost halves), so three cost 36 B per cell.  Here one workgroup
+// streams a column of boxes plane by plane (z) and runs the three substeps as
+// a pipeline over the planes (2.5-D temporal blocking): each plane of phi and
+// rhs is read once and the final plane written once, 24 B per cell plus the
+// pushed ghost faces.
+//
+// Tile: one box's 16 x 16 columns and three halo columns on each side
+// (22 x 22, one thread per column), read from the eight boxes around the box
+// in x and y.  At plane iteration t the thread holds the loaded plane t
+// (stage 0) and computes stage 1 (substep 1) at plane t-1, stage 2 at t-2 and
+// stage 3 at t-3: each stage's z neighbours are the same thread's registers
+// (the stage below, one plane lower and the one just computed one plane
+// higher), its x / y neighbours the stage below's plane in LDS, written at
+// iteration t-1.  Stage s is valid on the columns at distance <= 3-s from the
+// box (stage 3 on the box), and the first three planes below and above the
+// column only feed the pipeline.  Cells that a substep does not update keep
+// the value of the stage below.  The operands of every update are the values
+// the reference's substep reads (the neighbours' boundary cells are its ghost
+// values after the fill), in the same expression: bit-identical.
+//
+// In place would race (the halo columns are other workgroups' boxes), so the
+// pass reads one phi buffer and writes the level's other one (the host swaps
+// Level::d_phi): every interior cell, and every box's six ghost faces, pushed
+// by the box that owns the cell.  Levels whose faces are all same-GPU boxes,
+// 16^3 boxes, Laplacian / Helmholtz, with consistent ghosts on entry (they
+// are not read: a neighbour's cells are read in its box).
+#include <stdexcept>
+
+#ifndef B3_AHEAD
+#define B3_AHEAD 4
+#endif
+#ifndef B3_WAVES
+#define B3_WAVES 1
+#endif
+
+#include "omg_device.h"
+#include "omg_face.h"
+#include "omg_kernels.h"
+
+namespace omg {
+
+namespace {
+
+constexpr int B3NC = 16, B3H = 8, B3HV = B3H * B3NC * B3NC, B3FH = B3H * B3NC, B3FS = 2 * B3FH;
+constexpr int B3NPX = (kB3TX * B3NC + 8) / 2;   // cell pairs per row: x in [-4, kB3TX*16+3]
+constexpr int B3NY = B3NC + 6;                   // rows: y in [-3, 18]
+constexpr int B3NT = B3NPX * B3NY;               // compute threads with a pair
+constexpr int B3NW = (B3NT + 63) / 64;           // compute waves
+constexpr int B3BS = 64 * (B3NW + 1);            // and the store wave
+constexpr int B3CP = kB3TX * B3H;                // pairs per row of the tile's boxes
+constexpr int B3LP = B3NPX + 2;                  // LDS row pitch (a pad pair on each side)
+constexpr int B3PL = B3LP * (B3NY + 2);          // LDS doubles per plane (a pad row on each side)
+constexpr int B3XS = kB3TX + 2;                  // record slots per row
+constexpr int kB3Ahead = B3_AHEAD;               // planes of loads in flight
+
+// ghost slot of face nb (1..6) at tangential (a, c) (omg_device.h off_gh)
+__device__ __forceinline__ int b3_gh(int nb, int a, int c) {
+  const int g = (nb & 1) ? 0 : B3NC + 1;
+  return 2 * B3HV + (nb - 1) * B3FS + ((g + a + c) & 1) * B3FH + ((a - 1) >> 1) + B3H * (c - 1);
+}
+
+// an opaque register copy: the loaded value dies here, so the next load can
+// land in its register (a plain copy keeps the loaded register alive for as
+// long as the copy lives, and the loop then moves in-flight loads around,
+// which waits for them)
+__device__ __forceinline__ double b3_take(double v) {
+  double r;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// A store the compiler does not count: its s_waitcnt bookkeeping treats
+// vmcnt as out of order once stores and loads are both pending and then waits
+// for vmcnt(0) at every load use, which would drain the loads in flight two
+// planes ahead.  Loads return in order among themselves, so the counted waits
+// it computes from the loads alone stay correct with these stores pending
+// (they only make the hardware wait longer); nothing in the kernel reads what
+// they write.  base: wave-uniform, off: bytes (< 4 GiB).
+__device__ __forceinline__ void b3_st(double* base, unsigned off, double v) {
+  asm volatile("global_store_dwordx2 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(v), "s"(base));
+}
+__device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
+}
+
+}  // namespace
+
+// Workgroup = B3NW compute waves and one store wave.  A compute thread holds
+// one pair of x-neighbour cells (x0, x0+1), x0 even, in one row: one cell of
+// each colour in every plane.  Every substep updates exactly one cell of the
+// pair, the colour-e cell (stages 1 and 3) or the colour-(1-e) one (stage 2),
+// and its six operands are the pair's other cell (register), the neighbour
+// pair's cell across (LDS), the same pair in the rows above and below (LDS)
+// and the same column one plane down and up (registers).  The three active
+// cells of one iteration (planes t-1, t-2, t-3) lie on the same side of the
+// pair; the update adds its two x operands in either order (x+ + x- = x- + x+
+// exactly), so the side needs no select.  The stage planes in LDS hold one
+// value per pair (the colour that stage wrote).  Colour e of phi is not read:
+// substep 1 overwrites it without reading it (the operators here have no
+// centre term in the update), as the one-substep kernel does.
+//
+// The compute waves issue no store: a wave's loads and stores share one
+// counter (vmcnt), so a wave that stores waits for its stores at every later
+// wait for a load, and the loads run kB3Ahead planes ahead only if nothing
+// else is pending.  The final plane t-3 goes to LDS; the store wave writes it
+// to HBM during the next iteration, with every ghost face it is part of.
+// Addresses are 32-bit byte offsets from wave-uniform bases (the host admits
+// levels whose phi and rhs each stay under 4 GiB).
+template <int OP>
+__global__ void __launch_bounds__(B3BS, B3_WAVES) k_gsrb3(LevelView L, double* __restrict__ dst,
+                                                          const int* __restrict__ cols, double lambda, int e,
+                                                          const double* __restrict__ shift) {
+  __shared__ double pl[2][3][B3PL];
+  __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
+  __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
+  __shared__ int len_s;
+  const int tid = threadIdx.x;
+  const int cq = xcd_box(blockIdx.x, gridDim.x);
+  if (tid < kB3Rec) {
+    const int v = cols[(long long)cq * kB3Rec + tid];
+    if (tid == 0) len_s = v;
+    else bo[tid - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+  }
+  for (int q = tid; q < 2 * 3 * B3PL; q += B3BS) (&pl[0][0][0])[q] = 0.0;
+  __syncthreads();
+  const int len = len_s, zend = B3NC * len;
+  constexpr unsigned PB = 8u * B3H * B3NC;   // bytes per plane of one colour
+  auto zbox = [&](int t, int& k) {
+    const int zs = t < 0 ? 0 : (t >= zend ? len + 1 : (t >> 4) + 1);
+    k = t - B3NC * (zs - 1) + 1;
+    return zs;
+  };
+
+  if (tid >= B3NW * 64) {
+    // ---- the store wave: plane t-4 (written to fin by iteration t-1) ------
+    const int l = tid - B3NW * 64;
+    double* __restrict__ dse = dst + e * B3HV;
+    double* __restrict__ dso = dst + (1 - e) * B3HV;
+    auto flush = [&](int t) {
+      const int z = t - 4;
+      if (z < 0 || z >= zend) return;
+      int k;
+      const int r0 = kB3S * zbox(z, k);
+      const double(*F)[2] = fin[z & 1];
+      // colour e is on the left of the pairs of row j at plane z when
+      // (j - 1 + z) is even... (the compute side's test at plane z: y + z + 1)
+      auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
+      // the pairs: interior of both colours, and the z faces of the boxes
+      // below / above when the plane is a box's first / last layer
+#pragma unroll
+      for (int r = 0; r < B3NC * B3CP / 64; r++) {
+        const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
+        const int xs = 1 + pc / B3H, ih = pc % B3H, j = jr + 1;
+        const unsigned o = bo[r0 + xs + B3XS] + 8u * (ih + B3H * (j - 1)) + PB * (k - 1);
+        const double ve = F[q][0], vo = F[q][1];
+        b3_st(dse, o, ve);
+        b3_st(dso, o, vo);
+        if (k == 1 || k == B3NC) {
+          const bool lf = leftv(jr);
+          const double vl = lf ? ve : vo, vr = lf ? vo : ve;
+          const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
+          const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
+          b3_st(dst, g + 8u * b3_gh(nb, il, j), vl);
+          b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), vr);
+        }
+      }
+      // x faces: per row the cells x = 0, 15, 16, 31 (lane: row l/4, which l%4)
+      {
+        const int jr = l >> 2, w = l & 3, j = jr + 1;
+        const int pc = w == 0 ? 0 : (w == 1 ? B3H - 1 : (w == 2 ? B3H : 2 * B3H - 1));
+        const int xs = 1 + pc / B3H;
+        const bool lf = leftv(jr), wantl = (w & 1) == 0;   // x = 0, 16: a left cell; 15, 31: right
+        const double v = (wantl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
+        const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
+        b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+      }
+      // y faces: the cells of rows j = 1 (lanes 0..31) and j = 16 (32..63)
+      {
+        const int jr = l < 32 ? 0 : B3NC - 1, x = l & 31;
+        const int pc = x >> 1, xs = 1 + pc / B3H, i = x - B3NC * (xs - 1) + 1;
+        const bool lf = leftv(jr), isl = (x & 1) == 0;
+        const double v = (isl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
+        const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
+        b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+      }
+    };
+    for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
+#pragma unroll
+      for (int u = 0; u < kB3Ahead; u++) {
+        flush(t + u);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  // ---- the compute waves ---------------------------------------------------
+  const bool act = tid < B3NT;
+  const int p = tid % B3NPX, y = tid / B3NPX - 3;     // (threads past B3NT: a row inside the tile's y+ box)
+  const int x0 = 2 * p - 4;
+  const int xs = x0 < 0 ? 0 : (x0 < kB3TX * B3NC ? 1 + x0 / B3NC : kB3TX + 1);
+  const int ys = y < 0 ? 0 : (y < B3NC ? 1 : 2);
+  const int ih = (x0 - B3NC * (xs - 1)) >> 1, j = y - B3NC * (ys - 1) + 1;
+  const int slot = xs + B3XS * ys;
+  const unsigned xyb = 8u * (ih + B3H * (j - 1));
+  const int li = act ? (p + 1) + B3LP * (y + 4) : B3LP + 1;
+  const bool ctr = act && xs >= 1 && xs <= kB3TX && ys == 1;
+  const int fi = ctr ? (j - 1) * B3CP + (xs - 1) * B3H + ih : 0;
+  const double m = shift ? *shift : 0.0;
+  const OpCoef<OP> K(L, lambda);
+  // colour 1-e of phi; rhs of colour e / 1-e
+  const double* __restrict__ src = L.phi + (1 - e) * B3HV;
+  const double* __restrict__ rhe = L.data + L.vstride + e * B3HV;
+  const double* __restrict__ rho = L.data + L.vstride + (1 - e) * B3HV;
+
+  // plane t: colour 1-e of phi, both colours of rhs (no branch: the waits
+  // for these loads are counted; planes past the end reload the last one)
+  auto load = [&](int t, double& q, double& fe, double& fo) {
+    int k;
+    const int zs = zbox(min(t, zend + 2), k);
+    const unsigned o = bo[kB3S * zs + slot] + xyb + PB * (k - 1);
+    q = b3_ld(src, o);
+    fe = b3_ld(rhe, o);
+    fo = b3_ld(rho, o);
+  };
+
+  // V0: colour 1-e as loaded, planes t-2, t-1; V1: colour e after substep 1,
+  // planes t-3, t-2; V2: colour 1-e after substep 2, planes t-4, t-3; rhs of
+  // colour e at planes t-1, t-2, t-3 and of colour 1-e at t-1, t-2
+  double oa = 0.0, ob = 0.0, ea = 0.0, eb = 0.0, wa = 0.0, wb = 0.0;
+  double re1 = 0.0, re2 = 0.0, re3 = 0.0, ro1 = 0.0, ro2 = 0.0;
+  auto step = [&](int t, double& q, double& fe, double& fo) {
+    const double ot = shift ? b3_take(q) - m : b3_take(q);
+    const double ret = b3_take(fe), rot = b3_take(fo);
+    load(t + kB3Ahead, q, fe, fo);
+    const double* P0 = pl[t & 1][0];
+    const double* P1 = pl[t & 1][1];
+    const double* P2 = pl[t & 1][2];
+    // the active cells are the pair's left ones (x0) when colour e is there
+    // at plane t-1; the neighbour pair across is on that side
+    const int far = ((y + t) & 1) == e ? li - 1 : li + 1;
+    Nbr7 n;
+    n.c = 0.0;
+    // substep 1 (colour e) at plane t-1
+    n.xm = P0[far]; n.xp = ob;
+    n.ym = P0[li - B3LP]; n.yp = P0[li + B3LP]; n.zm = oa; n.zp = ot;
+    const double s1 = gs_value<OP>(K, n, re1);
+    // substep 2 (colour 1-e) at plane t-2
+    n.xm = P1[far]; n.xp = eb;
+    n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
+    const double s2 = gs_value<OP>(K, n, ro2);
+    // substep 3 (colour e) at plane t-3
+    n.xm = P2[far]; n.xp = wb;
+    n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
+    const double s3 = gs_value<OP>(K, n, re3);
+    // plane t-3 is final (colour e = s3, colour 1-e = wb): to the store wave
+    if (ctr) {
+      double* F = fin[(t - 3) & 1][fi];
+      F[0] = s3;
+      F[1] = wb;
+    }
+    if (act) {
+      double* W = pl[(t + 1) & 1][0];
+      W[li] = ot;
+      W[B3PL + li] = s1;
+      W[2 * B3PL + li] = s2;
+    }
+    __syncthreads();
+    oa = ob; ob = ot;
+    ea = eb; eb = s1;
+    wa = wb; wb = s2;
+    re3 = re2; re2 = re1; re1 = ret;
+    ro2 = ro1; ro1 = rot;
+  };
+  // kB3Ahead planes in flight.  The loop issues every load, planes -3 .. in
+  // kB3Ahead extra leading steps that compute nothing used: loads issued
+  // before the loop land in other registers than the loop's, and its first
+  // wait would drain them all.  Trailing steps past the column compute
+  // nothing used either (their loads reload the last plane); the store wave
+  // writes plane zend-1 in iteration zend+3.
+  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead];
+#pragma unroll
+  for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = 0.0;
+  for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
+#pragma unroll
+    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u]);
+  }
+}
+
+bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
+
+void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
+                  const double* shift, hipStream_t st) {
+  if (n_cols <= 0) return;
+  if (L.nc != B3NC) throw std::runtime_error("launch_gsrb3: box size must be 16");
+  if (op == OP_HELM)
+    k_gsrb3<OP_HELM><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+  else
+    k_gsrb3<OP_LPL><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+}
+
+}  // namespace omg

@@ -179,6 +179,12 @@ struct Level {
   // the second ghost-face set of phi for chains of register-ring sweeps (6
   // faces per box, the stored face layout; GhostSets in omg_kernels.h)
   double* d_galt = nullptr;
+  // three substeps per pass (k_gsrb3, launch_gsrb3): phi's second buffer (the
+  // pass reads d_phi and writes the other one; d_phi is d_data's var 1 or
+  // this) and the workgroups' box records (n_b3 columns); null: not eligible
+  double* d_phi_buf = nullptr;
+  int* d_b3 = nullptr;
+  int n_b3 = 0;
   int* d_physbox = nullptr;          // boxes with a physical face (k_phys_gc after such a chain)
   int n_physbox = 0;
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
@@ -314,6 +320,7 @@ struct omg_ctx {
   bool no_fill_xl = false;             // OMG_NO_FILL_XL: the plain tiled fill after register-ring sweeps
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
+  bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

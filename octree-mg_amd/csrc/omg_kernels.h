@@ -43,6 +43,23 @@ inline bool gs_tiled(int nc, int op, bool has_rb) {
   (void)has_rb;
   return nc == 16 || nc == 8 || nc == 4 || nc == 2;
 }
+// Three red-black substeps (colours e, 1-e, e) of a level in one pass
+// (k_gsrb3, omg_block.hip): reads phi from L.phi, writes every interior cell
+// and ghost face to dst (the level's other phi buffer).  cols: per workgroup a
+// record of kB3Rec ints, [0] = number of boxes in the column (1..kB3MaxZ),
+// then for slots zs = 0..len+1 (the box below the column, its boxes from
+// low to high z, the box above) at 1 + kB3S*zs the boxes xs + (kB3TX+2)*ys
+// (xs = 0: the x neighbour below the tile, 1..kB3TX: the tile's boxes,
+// kB3TX+1: the one above; ys = 0 / 1 / 2 likewise in y; edges by neighbour of
+// neighbour).  Levels of 16^3 boxes whose faces are all same-GPU boxes.
+constexpr int kB3TX = 2;                         // boxes per tile in x
+constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
+constexpr int kB3MaxZ = 4;                       // boxes per column in z
+constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
+constexpr int kB3MinBoxes = 512;                 // smaller levels: one substep per launch
+bool gsrb3_op_ok(int op);
+void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
+                  const double* shift, hipStream_t st);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,

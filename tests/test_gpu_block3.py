@@ -1,0 +1,83 @@
+"""Three red-black substeps per pass (k_gsrb3, octree-mg_amd/csrc/omg_block.hip)
+against the C oracle, every stored cell of every variable after each cycle.
+
+The pass runs on levels of at least kB3MinBoxes (512) boxes of 16^3 whose
+faces are all same-GPU boxes (periodic uniform levels), for runs of three
+consecutive substeps of smooth_boxes (m_multigrid.f90:404-424), and writes
+phi into the level's second buffer.  The cases cover what changes around it:
+odd and even numbers of passes per cycle (phi left in either buffer between
+cycles and across FMG), the pending mean shift absorbed by its first substep
+(periodic Laplacian), Helmholtz, FMG with and without a guess, and the level
+with the pass switched off (OMG_NO_BLOCK3) in the same process."""
+import numpy as np
+import pytest
+
+from tests.mgdriver import OPS, DeviceBackend, OracleBackend, parse, setup_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _stored_mask(nc):
+    s = nc + 2
+    ix = np.arange(s)
+    bnd = ((ix == 0) | (ix == s - 1)).astype(int)
+    return (bnd[:, None, None] + bnd[None, :, None] + bnd[None, None, :]) < 2
+
+
+def _assert_same(dev, orc, ivs=(1, 2, 3, 4)):
+    for lvl in dev.levels():
+        if not len(dev.my_ids(lvl)):
+            continue
+        m = _stored_mask(dev.tree.box_size_lvl[lvl])
+        for iv in ivs:
+            a, b = dev.get_level(lvl, iv), orc.get_level(lvl, iv)
+            assert np.array_equal(a[:, m].view(np.uint64), b[:, m].view(np.uint64)), (lvl, iv)
+
+
+def _pair(args, down, up):
+    cfg = parse(args)
+    dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
+    import pyoracle  # on sys.path once OracleBackend exists (checker only)
+    dev.mg.n_cycle_down, dev.mg.n_cycle_up = down, up
+    dev.mg._push_methods()
+    op = OPS[cfg["op"]]
+    orc.o.configure(op=op, lam=cfg["lam"], smoother=pyoracle.GSRB, n_cycle_down=down, n_cycle_up=up,
+                    subtract_mean=cfg["op"] == "lpl" and cfg["bc"] == "per")
+    for be in (dev, orc):
+        setup_problem(be)
+    return dev, orc
+
+
+# (n_cycle_down, n_cycle_up): down-smoothing runs 2*down-1 substeps before the
+# fused last one, up-smoothing 2*up-1 after the fused first one
+@pytest.mark.parametrize("down,up", [(2, 2), (3, 1), (1, 3), (4, 4)])
+@pytest.mark.parametrize("args", ["16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0",
+                                  "16 128 128 128 3 v gsrb helm 2 per sol 1 lb 0"])
+def test_block3_vcycles_match_oracle(args, down, up):
+    dev, orc = _pair(args, down, up)
+    for _ in range(3):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc)
+
+
+@pytest.mark.parametrize("have_guess", [False, True])
+def test_block3_fmg_matches_oracle(have_guess):
+    dev, orc = _pair("16 128 128 128 2 f gsrb lpl 0 per sol 1 lb 0", 2, 2)
+    for _ in range(2):
+        assert dev.fmg(have_guess, True) == orc.fmg(have_guess, True)
+        _assert_same(dev, orc)
+
+
+def test_block3_switch_off_same_bits(monkeypatch):
+    """OMG_NO_BLOCK3=1 (one substep per launch) and the default give the same
+    state after each cycle."""
+    args = "16 128 128 128 2 v gsrb lpl 0 per sol 1 lb 0"
+    dev, orc = _pair(args, 3, 2)
+    monkeypatch.setenv("OMG_NO_BLOCK3", "1")
+    ref = DeviceBackend(parse(args))
+    ref.mg.n_cycle_down, ref.mg.n_cycle_up = 3, 2
+    ref.mg._push_methods()
+    setup_problem(ref)
+    for _ in range(2):
+        assert dev.vcycle(True) == ref.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, ref)
