@@ -31,7 +31,11 @@ value = finest-level cells x V-cycles / s over all ranks (the BASELINE metric).
 roofline: the red-black smoother kernel on the finest level, algorithmic 12 B
 per level cell per substep (24 B per cell update), timed with
 HIP events on the library's stream in a separate profiled cycle, against
-8 TB/s HBM3E; traffic from the committed rocprofv3 PMC summary.
+8 TB/s HBM3E; traffic from the committed rocprofv3 PMC summary.  On C3's
+periodic finest level the kernel is k_gsrb3 (three substeps per pass,
+omg_block.hip): the same rule over its 1.5 cell updates per level cell, and
+beside it the pass's own minimum HBM bytes (phi of one colour and rhs in,
+phi and the ghost faces out: 20 B per cell + 12 KiB per box).
 cpu_baseline: the reference itself (oracle/_ref, amdflang -O2 + MPICH) on the
 host cores of this box at P = 1, 8 and the job's CPU share (rank 0, N = 1).
 """
@@ -62,24 +66,28 @@ METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
 # also reports what these do not account for
-KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
+KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
                    "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
 COMM_FAMILIES = ("comm", "comm_overlap")
 
 
-def pmc_traffic(per_gpu_cells):
+def pmc_traffic(per_gpu_cells, block3=False):
     """HBM bytes per launch of the finest-level smoother from the newest
     committed PMC summary (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2
-    + WRITE_SIZE, the MI355X guide's gfx950 correction), or None."""
+    + WRITE_SIZE, the MI355X guide's gfx950 correction), or None.  block3:
+    k_gsrb3 (one workgroup per column of 2 x 4 boxes; its loads are 8 B per
+    lane, for which the guide's x2 is uncalibrated)."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_smoother.json")), reverse=True):
+    name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1>") if block3 else \
+        ("pmc_smoother.json", r"void omg::k_gsrb_tile<16, 1[,>]")
+    wgs = per_gpu_cells // BOX ** 3 // (8 if block3 else 1)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
         try:
             d = json.load(open(f))
             for k, e in d["kernels"].items():
-                if re.match(r"void omg::k_gsrb_tile<16, 1[,>]", k) and "hbm_bytes_per_launch" in e:
-                    if e["workgroups"] == per_gpu_cells // BOX ** 3:
-                        return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+                if re.match(pat, k) and "hbm_bytes_per_launch" in e and e["workgroups"] == wgs:
+                    return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
         except (OSError, ValueError, KeyError):
             continue
     return None, None
@@ -243,25 +251,36 @@ def profile_cycle(omg, mg, timer, cycle):
     # side-stream work overlaps and can make it negative)
     kern["profiled_cycle_ms"] = round(tp * 1e3, 4)
     kern["unaccounted_ms"] = round(tp * 1e3 - total - comm.get("comm", {}).get("ms", 0.0), 4)
-    smoother = mg.ctx.kernel_stats(f"smoother_gsrb@{hi}")
+    # the finest level's red-black smoother: k_gsrb3 where it runs (three
+    # substeps per pass), else the one-substep kernel
+    smoother = mg.ctx.kernel_stats(f"smoother_gsrb3@{hi}")
+    smoother = (True,) + tuple(smoother) if smoother[0] else (False,) + tuple(mg.ctx.kernel_stats(f"smoother_gsrb@{hi}"))
     return kern, comm, smoother
 
 
 def roofline(smoother, per_gpu_cells, boxes_hi, hi):
-    n, ms, upd = smoother
+    block3, n, ms, upd = smoother
     if not (n and ms > 0):
         return None
     alg_bytes = 24.0 * upd / n          # 24 B per cell update, per launch
     dur = ms * 1e-3 / n
     achieved = alg_bytes / dur / 1e9
-    traffic, tsrc = pmc_traffic(per_gpu_cells)
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": f"k_gsrb_tile<16,OP_LPL> on level {hi} ({boxes_hi} boxes)",
-            "launches": n, "avg_launch_us": dur * 1e6,
-            "alg_bytes_per_launch": alg_bytes,
-            "alg_bytes_rule": "24 B per cell update x (level cells / 2) per substep",
-            "traffic_source": tsrc}
+    traffic, tsrc = pmc_traffic(per_gpu_cells, block3)
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+           "kernel": (f"k_gsrb3<OP_LPL> (three red-black substeps per pass) on level {hi} ({boxes_hi} boxes)"
+                      if block3 else f"k_gsrb_tile<16,OP_LPL> on level {hi} ({boxes_hi} boxes)"),
+           "launches": n, "avg_launch_us": dur * 1e6,
+           "alg_bytes_per_launch": alg_bytes,
+           "alg_bytes_rule": "24 B per cell update x (level cells / 2) per substep" +
+                             (", 3 substeps per launch" if block3 else ""),
+           "traffic_source": tsrc}
+    if block3:
+        cells = upd / n / 1.5
+        own = 20.0 * cells + 6 * BOX * BOX * 8 * boxes_hi
+        out["pass_min_bytes_per_launch"] = own
+        out["pass_min_frac"] = own / dur / 1e9 / HBM_PEAK_GBS
+    return out
 
 
 def run_c3(omg, domain, dist, rank, world, dev, steps, warmup, profile=True):

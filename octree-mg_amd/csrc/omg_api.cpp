@@ -972,53 +972,11 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
          !F->any_rbx;
 }
 
-// Whether the level's last four down-substeps, the residual and the
-// restriction run as one k_gsrb4r pass (launch_gsrb4r): the levels k_gsrb3
-// serves (Level::d_b3), with the fused down-step available and a level below
-// of 16^3 boxes.  With n_cycle_down == 2 the pass is the level's whole
-// down-smoothing, and its first substep reads the ghosts, which must be
-// consistent now (more cycles: the substeps before it leave them so).
-bool block4_ok(omg_ctx* c, int lvl) {
-  const Level* F = level_ptr(c, lvl);
-  const Level* C = level_ptr(c, lvl - 1);
-  static const bool on = getenv("OMG_BLOCK4") != nullptr;   // (experiment: slower so far)
-  return on && F && C && F->d_b3 && !c->no_block3 && gsrb3_op_ok(c->op) && c->n_substeps == 2 &&
-         c->n_cycle_down >= 2 && C->nc == 16 && (c->n_cycle_down > 2 || F->phi_gc_ok);
-}
-
-// the level's last four down-substeps, its residual and the restriction of
-// phi and res (k_gsrb4r); update_coarse's fused step for block4_ok levels
-void run_block4(omg_ctx* c, int lvl) {
-  Level* L = level_ptr(c, lvl);
-  const int first = 2 * c->n_cycle_down - 3;   // the pass's first substep
-  rb_stale_above(c, lvl);
-  const double* shift = nullptr;
-  if (L->shift_pending) {
-    if (first == 1) {   // absorbed by the pass's loads (smooth_boxes' absorb)
-      phi_mean_ready(c);
-      shift = red_mean(c, 0);
-    } else {
-      materialize_level(c, L);
-    }
-    L->shift_pending = false;
-  }
-  if (!L->phi_gc_ok) throw OmgError("internal: k_gsrb4r needs consistent ghosts");
-  double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
-  {
-    Prof p(c, "smooth_resid4", 2.0 * L->n * L->nc * L->nc * L->nc, lvl);
-    launch_gsrb4r(L->view(), view_of(c, lvl - 1), other, L->d_b3, L->n_b3, c->op, c->lambda, first & 1, shift,
-                  c->stream);
-  }
-  L->d_phi = other;
-  L->phi_gc_ok = true;
-}
-
 // update_coarse (m_multigrid.f90:347-384); fused: the level's last down
-// substep is still to do (smooth_resid_ok), k_smooth_resid runs it; block4:
-// its last four (block4_ok), k_gsrb4r runs them
+// substep is still to do (smooth_resid_ok), k_smooth_resid runs it
 // with tail_crhs the coarse tail forms lvl-1's ghosts and coarse rhs itself
 // (its top level, TailArgs::top_crhs): only the residual and the restriction here
-void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = false, bool block4 = false) {
+void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = false) {
   Level* F = level_ptr(c, lvl);
   if (Level* Cl = level_ptr(c, lvl - 1)) {
     Cl->rhs_lex_ok = false;   // its rhs is rewritten below
@@ -1078,8 +1036,6 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
         launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
                               F->d_dix, c->stream, F->d_bnd, F->n_bnd);
       }
-    } else if (fused && block4) {
-      run_block4(c, lvl);
     } else if (fused) {
       Prof p(c, "smooth_resid", (double)F->n * F->nc * F->nc * F->nc, lvl);
       if (!launch_smooth_resid(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, 1, F->d_parent_local,
@@ -1686,9 +1642,8 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
     const bool fused = smooth_resid_ok(c, l);
-    const bool block4 = fused && !c->levels[l].has_remote && block4_ok(c, l);
-    if (!block4 || c->n_cycle_down > 2) smooth_boxes(c, l, c->n_cycle_down, 1, block4 ? 4 : (fused ? 1 : 0));
-    update_coarse(c, l, fused, tail_crhs && l == top + 1, block4);
+    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
+    update_coarse(c, l, fused, tail_crhs && l == top + 1);
   }
   if (tail) {
     run_tail(c, top, tail_crhs);
@@ -2340,7 +2295,7 @@ void free_levels(omg_ctx* c) {
 // each XCD's run of workgroups (xcd_box) is one compact patch whose halo
 // columns its own L2 holds.  Any face or tiling that does not fit: no records.
 void build_block3(omg_ctx* c, Level& L) {
-  if (g_host_only || c->host_only || L.nc != 16 || L.n < kB3MinBoxes || L.replicated) return;
+  if (g_host_only || c->host_only || L.nc != 16 || L.n < c->b3_min_boxes || L.replicated) return;
   for (int8_t k : L.h_nbk)
     if (k != NB_LOCAL) return;
   const int n = L.n;
@@ -2354,12 +2309,15 @@ void build_block3(omg_ctx* c, Level& L) {
   };
   std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
   std::vector<int> covered(n, 0);
+  // columns of kB3MaxZ boxes (on the 4096-box level of C3, two-box columns,
+  // twice the workgroups, took 110 us a pass against 102)
+  const int nzb = kB3MaxZ;
   for (int h = 0; h < n; h++) {
-    if (ixd(h, 0) % kB3TX || ixd(h, 2) % kB3MaxZ) continue;
+    if (ixd(h, 0) % kB3TX || ixd(h, 2) % nzb) continue;
     std::vector<int> zc{h};
-    while ((int)zc.size() < kB3MaxZ) {
+    while ((int)zc.size() < nzb) {
       const int up = nb(zc.back(), 5);
-      if (ixd(up, 2) % kB3MaxZ == 0) break;   // the next column's first box
+      if (ixd(up, 2) % nzb == 0) break;   // the next column's first box
       zc.push_back(up);
     }
     const int len = (int)zc.size();
@@ -2382,14 +2340,7 @@ void build_block3(omg_ctx* c, Level& L) {
         for (int xs = 0; xs + 1 < kB3TX + 2; xs++)
           if (nb(row[(kB3TX + 2) * ys + xs], 1) != row[(kB3TX + 2) * ys + xs + 1]) return;
     }
-    // the parents of the column's boxes (launch_gsrb4r's restriction)
-    for (int zs = 1; zs <= len; zs++)
-      for (int xs = 1; xs <= kB3TX; xs++) {
-        const int b = r[1 + kB3S * zs + xs + (kB3TX + 2)], q = kB3Par + 2 * ((zs - 1) * kB3TX + xs - 1);
-        r[q] = b < (int)L.parent_local.size() ? L.parent_local[b] : -1;
-        r[q + 1] = b < (int)L.dix_packed.size() ? L.dix_packed[b] : 0;
-      }
-    const unsigned long long key = ((unsigned long long)(ixd(h, 2) / kB3MaxZ) << 40) |
+    const unsigned long long key = ((unsigned long long)(ixd(h, 2) / nzb) << 40) |
                                    (spread((unsigned)(ixd(h, 0) / kB3TX)) | (spread((unsigned)ixd(h, 1)) << 1));
     cols.emplace_back(key, std::move(r));
   }
@@ -2619,6 +2570,7 @@ void build_plan(omg_ctx* c) {
       }
     }
     L.d_phi = L.d_data;
+    build_block3(c, L);
     L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);
     L.d_nba = to_device(L.h_nba);
@@ -2723,8 +2675,6 @@ void build_plan(omg_ctx* c) {
       }
     }
   }
-  // (after the grid transfers: the records carry each box's parent)
-  for (int l = c->lowest; l <= c->highest; l++) build_block3(c, c->levels[l]);
   // communication buffers, sized for the largest transfer touching each level
   if (c->n_ranks > 1) {
     std::map<int, size_t> sendn, recvn;
@@ -2839,6 +2789,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_block3 = env_flag("OMG_NO_BLOCK3");
+    // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
+    if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

@@ -32,6 +32,11 @@ enum Op : int { OP_LPL = 1, OP_VLPL = 2, OP_HELM = 3, OP_VHELM = 4, OP_AHELM = 5
 
 constexpr int kMaxVars = 16;
 
+// k_gsrb3 (omg_block.hip): levels of fewer boxes take one substep per launch
+// (a 512-box level: 57 us per pass against 3 x 8.5 us, latency-bound; 4096
+// boxes: 102 against 126)
+constexpr int kB3MinBoxes = 4096;
+
 // Physical boundary condition of one variable (mg%bc(:, iv)).
 struct BCVar {
   int type[6];
@@ -321,6 +326,7 @@ struct omg_ctx {
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
+  int b3_min_boxes = omg::kB3MinBoxes;  // smallest level for k_gsrb3 (OMG_BLOCK3_MIN_BOXES, tests)
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending
   double* d_scalar = nullptr;          // small device scratch

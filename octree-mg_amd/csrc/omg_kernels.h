@@ -55,22 +55,10 @@ inline bool gs_tiled(int nc, int op, bool has_rb) {
 constexpr int kB3TX = 2;                         // boxes per tile in x
 constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
 constexpr int kB3MaxZ = 4;                       // boxes per column in z
-// then at kB3Par, per box of the column (zs-1)*kB3TX + xs-1: its parent on
-// the level below (local index, -1: on another rank) and child offset (dix
-// packed as Level::dix_packed), for launch_gsrb4r's restriction
-constexpr int kB3Par = 1 + kB3S * (kB3MaxZ + 2);
-constexpr int kB3Rec = (kB3Par + 2 * kB3MaxZ * kB3TX + 15) / 16 * 16;
-constexpr int kB3MinBoxes = 512;                 // smaller levels: one substep per launch
+constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
 bool gsrb3_op_ok(int op);
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st);
-// Four red-black substeps (colours e, 1-e, e, 1-e), then update_coarse's
-// residual into res and the restriction of phi and res onto the parents on C
-// (k_gsrb4r, omg_block.hip): the level's down-smoothing end and residual in
-// one pass, on the levels launch_gsrb3 serves whose level below has 16^3
-// boxes.  dst as for launch_gsrb3.
-void launch_gsrb4r(const LevelView& L, const LevelView& C, double* dst, const int* cols, int n_cols, int op,
-                   double lambda, int e, const double* shift, hipStream_t st);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,

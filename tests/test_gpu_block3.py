@@ -1,7 +1,7 @@
 """Three red-black substeps per pass (k_gsrb3, octree-mg_amd/csrc/omg_block.hip)
 against the C oracle, every stored cell of every variable after each cycle.
 
-The pass runs on levels of at least kB3MinBoxes (512) boxes of 16^3 whose
+The pass runs on levels of at least kB3MinBoxes boxes of 16^3 whose
 faces are all same-GPU boxes (periodic uniform levels), for runs of three
 consecutive substeps of smooth_boxes (m_multigrid.f90:404-424), and writes
 phi into the level's second buffer.  The cases cover what changes around it:
@@ -15,6 +15,15 @@ import pytest
 from tests.mgdriver import OPS, DeviceBackend, OracleBackend, parse, setup_problem
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _small_levels(monkeypatch):
+    """The 128^3 trees here have a 512-box finest level; the pass serves
+    levels of 4096 boxes and up by default (kB3MinBoxes), so lower the bound
+    for these tests (read at context creation); the full-size golden
+    c3_per512_box16 runs the default bound."""
+    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", "512")
 
 
 def _stored_mask(nc):
