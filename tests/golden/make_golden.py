@@ -26,7 +26,8 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 # name: (box nx ny nz n_its cycle smoother op lambda bc rhs n_levels lb maxres), dump?, ranks
 # BIG: too large for the CPU oracle in the quick CPU suite (the device is
 # compared with the reference's numbers directly; tests/test_gpu_parity.py)
-BIG = {"c3_per512_box16", "c2_256_box16_gsrb_d0", "c2_256_box16_gs_d0", "c5_helm256_box16_gsrb_d0"}
+BIG = {"c3_per512_box16", "c2_256_box16_gsrb_d0", "c2_256_box16_gs_d0", "c5_helm256_box16_gsrb_d0",
+       "per256_box16_helm_v", "per256_box16_gsrb_f"}
 CONFIGS = {
     # tests/test_uniform_grid 8 64 64 64 10 f, as shipped (GS)
     "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
@@ -59,6 +60,11 @@ CONFIGS = {
     # (2, 4 and 8 ranks: the BASELINE C3 configuration on 8 GPUs, and the
     # MPICH allreduce order of get_sum at the bench's size)
     "c3_per512_box16": ("16 512 512 512 3 v gsrb lpl 0 per sol 1 lb 0", True, [1, 2, 4, 8]),
+    # periodic 256^3 at box 16: the 4096-box level runs k_gsrb3 (three
+    # red-black substeps per pass) at its default size bound, Helmholtz (no
+    # subtract_mean) and FMG with the max residual
+    "per256_box16_helm_v": ("16 256 256 256 3 v gsrb helm 10 per sol 1 lb 0", True, [1]),
+    "per256_box16_gsrb_f": ("16 256 256 256 2 f gsrb lpl 0 per sol 1 lb 1", True, [1]),
     # SURVEY §8(d) C2 at its own size: 256^3, box 16, Dirichlet 0, GSRB and
     # the reference tests' lexicographic GS
     "c2_256_box16_gsrb_d0": ("16 256 256 256 3 v gsrb lpl 0 d0 sol 1 lb 0", True, [1]),
