@@ -146,9 +146,10 @@ class OracleBackend:
         self.o = pyoracle.Oracle(self.tree, n_vars(cfg), n_ranks)
         op = OPS[cfg["op"]]
         sm = pyoracle.GSRB if cfg["smoother"] == "gsrb" else pyoracle.GS
-        # laplacian_set_methods only: periodic => subtract_mean (m_laplacian.f90:16-20);
-        # vlaplacian_set_methods sets it false (m_vlaplacian.f90:21)
-        sub = op == pyoracle.LAPLACIAN and cfg["bc"] == "per"
+        # omg_golden calls mg_set_methods before building the tree, and
+        # mg_build_rectangle sets subtract_mean for a fully periodic domain
+        # (m_build_tree.f90:36-38) whatever the operator's set_methods cleared
+        sub = cfg["bc"] == "per"
         self.o.configure(op=op, lam=cfg["lam"], smoother=sm, subtract_mean=sub)
         _apply_bc(cfg, self.tree, lambda iv, nb, t, v: self.o.set_bc(iv, nb, t, v),
                   lambda iv, a, b, c: self.o.set_bc_faces(iv, a, b, c))
@@ -213,8 +214,9 @@ class DeviceBackend:
 
     def _build(self, shift):
         cfg, mg = self.cfg, self.mg
+        # set_methods ran in __init__, before the build, as in omg_golden: the
+        # build's subtract_mean for a fully periodic domain stands
         build_tree(cfg, mg, mg.n_cpu, mg.my_rank, shift)
-        omg.mg_set_methods(mg)
 
         def set_bc(iv, nb, t, v):
             mg.bc[nb][iv] = omg.BC(t, v)

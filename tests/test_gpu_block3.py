@@ -51,7 +51,7 @@ def _pair(args, down, up):
     dev.mg._push_methods()
     op = OPS[cfg["op"]]
     orc.o.configure(op=op, lam=cfg["lam"], smoother=pyoracle.GSRB, n_cycle_down=down, n_cycle_up=up,
-                    subtract_mean=cfg["op"] == "lpl" and cfg["bc"] == "per")
+                    subtract_mean=cfg["bc"] == "per")
     for be in (dev, orc):
         setup_problem(be)
     return dev, orc
