@@ -803,9 +803,13 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // when they are consistent (phi_gc_ok), and writes every ghost face
     if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
+      // the down-smoothing's last pass before k_smooth_resid (skip_last: it
+      // runs the next substep, colour 0, and forms colour 0's ghosts itself
+      // from colour 1, reading colour 1's only): push colour e = 1 alone
+      const bool push1 = !(skip_last == 1 && n + 2 == n_sub && e == 1);
       {
         Prof p(c, "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
+        launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, push1);
       }
       L->d_phi = other;
       n += 2;

@@ -108,7 +108,7 @@ __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
 template <int OP>
 __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict__ dst,
                                                           const int* __restrict__ cols, double lambda, int e,
-                                                          const double* __restrict__ shift) {
+                                                          const double* __restrict__ shift, int push1) {
   __shared__ double pl[2][3][B3PL];
   __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
   __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
@@ -141,9 +141,10 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
       int k;
       const int r0 = kB3S * zbox(z, k);
       const double(*F)[2] = fin[z & 1];
-      // colour e is on the left of the pairs of row j at plane z when
-      // (j - 1 + z) is even... (the compute side's test at plane z: y + z + 1)
+      // colour e is the left cell of the pairs of row jr (0-based) at plane z
       auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
+      // push1 == 0: only the colour-e cells go to the neighbours' ghosts (the
+      // caller's next kernel forms the other colour's ghosts itself)
       // the pairs: interior of both colours, and the z faces of the boxes
       // below / above when the plane is a box's first / last layer
 #pragma unroll
@@ -159,8 +160,8 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
           const double vl = lf ? ve : vo, vr = lf ? vo : ve;
           const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
-          b3_st(dst, g + 8u * b3_gh(nb, il, j), vl);
-          b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), vr);
+          if (push1 || lf) b3_st(dst, g + 8u * b3_gh(nb, il, j), vl);
+          if (push1 || !lf) b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), vr);
         }
       }
       // x faces: per row the cells x = 0, 15, 16, 31 (lane: row l/4, which l%4)
@@ -171,7 +172,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const bool lf = leftv(jr), wantl = (w & 1) == 0;   // x = 0, 16: a left cell; 15, 31: right
         const double v = (wantl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
         const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
-        b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+        if (push1 || wantl == lf) b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
       }
       // y faces: the cells of rows j = 1 (lanes 0..31) and j = 16 (32..63)
       {
@@ -180,7 +181,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const bool lf = leftv(jr), isl = (x & 1) == 0;
         const double v = (isl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
         const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
-        b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+        if (push1 || isl == lf) b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
       }
     };
     for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
@@ -289,13 +290,13 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
 
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st) {
+                  const double* shift, hipStream_t st, bool push1) {
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb3: box size must be 16");
   if (op == OP_HELM)
-    k_gsrb3<OP_HELM><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+    k_gsrb3<OP_HELM><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, push1 ? 1 : 0);
   else
-    k_gsrb3<OP_LPL><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+    k_gsrb3<OP_LPL><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, push1 ? 1 : 0);
 }
 
 }  // namespace omg

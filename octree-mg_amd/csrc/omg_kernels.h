@@ -57,8 +57,11 @@ constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
 constexpr int kB3MaxZ = 4;                       // boxes per column in z
 constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
 bool gsrb3_op_ok(int op);
+// push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
+// halves are left stale: only for a pass that k_smooth_resid follows, which
+// reads colour e's and forms colour 1-e's itself)
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st);
+                  const double* shift, hipStream_t st, bool push1 = true);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,
