@@ -1152,6 +1152,31 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
   return true;
 }
 
+// correct_children(l-1) + fill of l + up-smoothing substeps 1-3 of l in one
+// k_gsrb3 pass (its correct_children form); returns whether it ran (the caller
+// then starts smooth_boxes at substep 4).  Levels with k_gsrb3's coarse
+// records (build_block3c), whose coarse level has consistent ghosts (the
+// reference's correction reads the parents' ghost cells; the pass reads the
+// neighbour parents' cells).
+bool correct_block3(omg_ctx* c, int l) {
+  Level* F = level_ptr(c, l);
+  Level* C = level_ptr(c, l - 1);
+  if (!F || !C || !F->d_b3c || c->no_block3 || c->no_block3p || c->smoother != OMG_SMOOTHER_GSRB ||
+      !gsrb3_op_ok(c->op) || c->n_cycle_up * c->n_substeps < 3 || !C->phi_gc_ok || C->shift_pending)
+    return false;
+  if (F->shift_pending) materialize_level(c, F);
+  rb_stale_above(c, l);
+  double* other = F->d_phi == F->d_data ? F->d_phi_buf : F->d_data;
+  {
+    Prof p(c, "smoother_gsrb3p", 1.5 * F->n * F->nc * F->nc * F->nc, l);
+    const LevelView cv = C->view();
+    launch_gsrb3(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, true, &cv, F->d_b3c);
+  }
+  F->d_phi = other;
+  F->phi_gc_ok = true;
+  return true;
+}
+
 // correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
 // V-cycle and FMG run them (m_multigrid.f90:127-136, 216-219); fused when every
 // box of lvl+1 has its parent on this GPU (refinement-boundary ghosts are
@@ -1672,7 +1697,9 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     }
   }
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
-    if (prolong_smooth(c, l - 1)) {
+    if (correct_block3(c, l)) {
+      smooth_boxes(c, l, c->n_cycle_up, 4);
+    } else if (prolong_smooth(c, l - 1)) {
       smooth_boxes(c, l, c->n_cycle_up, 2);
     } else {
       correct_and_fill(c, l - 1, c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_up >= 1);
@@ -2271,7 +2298,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
     dfree(L.d_galt);
-    dfree(L.d_phi_buf); dfree(L.d_b3); L.n_b3 = 0;
+    dfree(L.d_phi_buf); dfree(L.d_b3); dfree(L.d_b3c); L.n_b3 = 0; L.h_b3.clear();
     dfree(L.d_physbox);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0); dfree(L.d_bndface);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
@@ -2356,7 +2383,65 @@ void build_block3(omg_ctx* c, Level& L) {
   for (auto& cr : cols) flat.insert(flat.end(), cr.second.begin(), cr.second.end());
   L.n_b3 = (int)cols.size();
   L.d_b3 = to_device(flat);
+  L.h_b3 = std::move(flat);
   dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)L.n * L.stride, true);
+}
+
+// k_gsrb3's correct_children form (launch_gsrb3's ccols) for the columns of F:
+// every column of an even number of boxes starts at a coarse box's corner in x
+// and z, its fine boxes are the children of its coarse boxes, and every coarse
+// box is the own box of exactly two columns (its two halves in y), on a
+// coarse level of 16^3 boxes whose faces are all same-GPU boxes.
+void build_block3c(omg_ctx* c, Level& F, const Level& C) {
+  (void)c;
+  if (!F.d_b3 || F.h_b3.empty() || C.nc != 16 || C.replicated || C.n == 0 || F.n != 8 * C.n) return;
+  for (int8_t k : C.h_nbk)
+    if (k != NB_LOCAL) return;
+  for (int b = 0; b < F.n; b++)
+    if (F.parent_local[b] < 0) return;
+  auto nbc = [&](int b, int f) { return C.h_nba[(size_t)b * 6 + f]; };
+  auto dix = [&](int b, int q) { return (F.dix_packed[b] >> (10 * q)) & 1023; };
+  std::vector<int> out((size_t)F.n_b3 * kB3CRec, 0);
+  std::vector<int> own(C.n, 0);
+  for (int q = 0; q < F.n_b3; q++) {
+    const int* r = &F.h_b3[(size_t)q * kB3Rec];
+    const int len = r[0], lenc = len / 2;
+    if (len % 2) return;
+    auto fine = [&](int zs, int xs) { return r[1 + kB3S * zs + (kB3TX + 2) + xs]; };
+    const int b0 = fine(1, 1);
+    if (dix(b0, 0) != 0 || dix(b0, 2) != 0) return;
+    int* o = &out[(size_t)q * kB3CRec];
+    o[0] = dix(b0, 1);
+    int zc[kB3MaxZ / 2 + 2];
+    zc[1] = F.parent_local[b0];
+    for (int z = 2; z <= lenc; z++) zc[z] = nbc(zc[z - 1], 5);
+    zc[0] = nbc(zc[1], 4);
+    zc[lenc + 1] = nbc(zc[lenc], 5);
+    for (int z = 0; z <= lenc + 1; z++) {
+      int* row = o + 1 + 9 * z;
+      row[4] = zc[z];
+      row[3] = nbc(zc[z], 0);
+      row[5] = nbc(zc[z], 1);
+      for (int xs = 0; xs < 3; xs++) {
+        row[xs] = nbc(row[3 + xs], 2);
+        row[6 + xs] = nbc(row[3 + xs], 3);
+      }
+      for (int ys = 0; ys < 3; ys += 2)
+        for (int xs = 0; xs < 2; xs++)
+          if (nbc(row[3 * ys + xs], 1) != row[3 * ys + xs + 1]) return;
+      if (z >= 1 && z <= lenc) own[zc[z]]++;
+    }
+    for (int zs = 1; zs <= len; zs++)
+      for (int xs = 1; xs <= kB3TX; xs++) {
+        const int fb = fine(zs, xs);
+        if (F.parent_local[fb] != zc[(zs + 1) / 2] || dix(fb, 0) != (xs - 1) * 8 || dix(fb, 1) != o[0] ||
+            dix(fb, 2) != ((zs - 1) & 1) * 8)
+          return;
+      }
+  }
+  for (int b = 0; b < C.n; b++)
+    if (own[b] != 2) return;
+  F.d_b3c = to_device(out);
 }
 
 void build_plan(omg_ctx* c) {
@@ -2678,6 +2763,7 @@ void build_plan(omg_ctx* c) {
         }
       }
     }
+    build_block3c(c, F, C);
   }
   // communication buffers, sized for the largest transfer touching each level
   if (c->n_ranks > 1) {
@@ -2793,6 +2879,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_block3 = env_flag("OMG_NO_BLOCK3");
+    c->no_block3p = env_flag("OMG_NO_BLOCK3P");
     // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
     if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");

@@ -52,6 +52,12 @@ constexpr int B3XS = kB3TX + 2;                  // record slots per row
 // planes of loads in flight (2 / 3 / 4 / 5 / 6 ahead measured: 4 best, C3
 // 4.68 ms; more costs a workgroup per CU, profiles/r05/s17)
 constexpr int kB3Ahead = 4;
+static_assert(kB3Ahead % 2 == 0, "coarse planes are loaded on the even planes' steps");
+// the correction form: the coarse tile of a plane, cx in [-3, kB3TX*8+2] and
+// cy in [-3, 10] around the column's coarse cells (the fine tile's parents
+// and their x / y taps), in a ring of four coarse planes
+static_assert(kB3TX == 2, "a column spans one coarse box in x");
+constexpr int B3CX = kB3TX * B3H + 6, B3CY = B3H + 6, B3CT = B3CX * B3CY;
 
 // ghost slot of face nb (1..6) at tangential (a, c) (omg_device.h off_gh)
 __device__ __forceinline__ int b3_gh(int nb, int a, int c) {
@@ -105,20 +111,41 @@ __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
 // to HBM during the next iteration, with every ghost face it is part of.
 // Addresses are 32-bit byte offsets from wave-uniform bases (the host admits
 // levels whose phi and rhs each stay under 4 GiB).
-template <int OP>
+//
+// PRO (the correct_children form, launch_gsrb3's `coarse`): the pass starts
+// from phi before correct_children.  The colour 1-e it reads gets the
+// prolonged correction as it is loaded (prolong_at's expression, omg_tiles.hip,
+// from the coarse tile in LDS: phi - old of the coarse level, a plane of it
+// loaded on every other step, kB3Ahead steps ahead like the fine planes);
+// colour e needs none (substep 1 overwrites it).  The store wave also stores
+// the coarse level's res = phi - old, which correct_children leaves there: the
+// column's own coarse cells, interior and the faces they are ghosts of.
+template <int OP, bool PRO>
 __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict__ dst,
                                                           const int* __restrict__ cols, double lambda, int e,
-                                                          const double* __restrict__ shift, int push1) {
+                                                          const double* __restrict__ shift, int push1, LevelView C,
+                                                          const int* __restrict__ ccols) {
   __shared__ double pl[2][3][B3PL];
   __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
   __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
-  __shared__ int len_s;
+  __shared__ double rc[PRO ? 4 : 1][PRO ? B3CT : 1];   // coarse phi - old, plane c in rc[c & 3]
+  __shared__ unsigned cbo[PRO ? 36 : 1];      // the coarse record, byte offsets
+  __shared__ int len_s, cyo_s;
   const int tid = threadIdx.x;
   const int cq = xcd_box(blockIdx.x, gridDim.x);
   if (tid < kB3Rec) {
     const int v = cols[(long long)cq * kB3Rec + tid];
     if (tid == 0) len_s = v;
     else bo[tid - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+  }
+  if (PRO) {
+    const int q = tid - kB3Rec;
+    if (q >= 0 && q < 37) {
+      const int v = ccols[(long long)cq * kB3CRec + q];
+      if (q == 0) cyo_s = v;
+      else cbo[q - 1] = (unsigned)v * (unsigned)(C.stride * 8);
+    }
+    for (int q2 = tid; q2 < 4 * B3CT; q2 += B3BS) (&rc[0][0])[q2] = 0.0;
   }
   for (int q = tid; q < 2 * 3 * B3PL; q += B3BS) (&pl[0][0][0])[q] = 0.0;
   __syncthreads();
@@ -129,6 +156,36 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     k = t - B3NC * (zs - 1) + 1;
     return zs;
   };
+  // ---- PRO: the coarse tile cell this thread loads (cx, cy relative to the
+  // column's first coarse cell; threads past the tile load a duplicate)
+  const int cyo = PRO ? cyo_s : 0, lenc = len >> 1;
+  const double* __restrict__ cold = C.data + 2 * C.vstride;
+  const int ct = tid < B3CT ? tid : B3CT - 1;
+  const int cxr = ct % B3CX - 3, cyy = cyo + ct / B3CX - 3;
+  const int xsc = cxr < 0 ? 0 : (cxr < B3NC ? 1 : 2), ysc = cyy < 0 ? 0 : (cyy < B3NC ? 1 : 2);
+  const int icc = cxr - B3NC * (xsc - 1) + 1, jcc = cyy - B3NC * (ysc - 1) + 1;
+  const unsigned cxy = 8u * (((icc - 1) >> 1) + B3H * (jcc - 1));
+  auto cload = [&](int c, double& a, double& b) {
+    const int zsc = c < 0 ? 0 : (c >= B3NC * lenc ? lenc + 1 : (c >> 4) + 1);
+    const int kc = c - B3NC * (zsc - 1) + 1;
+    const unsigned o = cbo[9 * zsc + 3 * ysc + xsc] + 8u * B3HV * ((icc + jcc + kc) & 1) + cxy + PB * (kc - 1);
+    a = b3_ld(C.phi, o);
+    b = b3_ld(cold, o);
+  };
+  if (PRO) {
+    // coarse planes -2 and -1 (the first fine planes' parents and z taps)
+    // before the loop, whose loads reach plane 0 first
+    if (tid < B3NW * 64) {
+      double a0, b0, a1, b1;
+      cload(-2, a0, b0);
+      cload(-1, a1, b1);
+      if (tid < B3CT) {
+        rc[2][tid] = a0 - b0;
+        rc[3][tid] = a1 - b1;
+      }
+    }
+    __syncthreads();
+  }
 
   if (tid >= B3NW * 64) {
     // ---- the store wave: plane t-4 (written to fin by iteration t-1) ------
@@ -184,10 +241,29 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         if (push1 || isl == lf) b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
       }
     };
+    // PRO: res of the column's own coarse cells, plane cs in steps 2cs (rows
+    // 0-3) and 2cs+1 (rows 4-7); rc holds it from step 2cs-1 to 2cs+3
+    double* __restrict__ cres = C.data + 3 * C.vstride;
+    auto cflush = [&](int t) {
+      if (t < 0 || t >= zend) return;
+      const int cs = t >> 1, q = l + 64 * (t & 1), cxq = q & 15, cyq = q >> 4;
+      const double v = rc[cs & 3][(cxq + 3) + B3CX * (cyq + 3)];
+      const int ic = cxq + 1, jc = cyo + cyq + 1, zsc = (cs >> 4) + 1, kc = (cs & 15) + 1;
+      const unsigned* cb = cbo + 9 * zsc;
+      const unsigned o = 8u * (((ic + jc + kc) & 1) * B3HV + ((ic - 1) >> 1) + B3H * (jc - 1) + B3FH * (kc - 1));
+      b3_st(cres, cb[4] + o, v);
+      if (ic == 1) b3_st(cres, cb[3] + 8u * b3_gh(2, jc, kc), v);
+      if (ic == B3NC) b3_st(cres, cb[5] + 8u * b3_gh(1, jc, kc), v);
+      if (jc == 1) b3_st(cres, cb[1] + 8u * b3_gh(4, ic, kc), v);
+      if (jc == B3NC) b3_st(cres, cb[7] + 8u * b3_gh(3, ic, kc), v);
+      if (kc == 1) b3_st(cres, cb[4 - 9] + 8u * b3_gh(6, ic, jc), v);
+      if (kc == B3NC) b3_st(cres, cb[4 + 9] + 8u * b3_gh(5, ic, jc), v);
+    };
     for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
 #pragma unroll
       for (int u = 0; u < kB3Ahead; u++) {
         flush(t + u);
+        if (PRO) cflush(t + u);
         __syncthreads();
       }
     }
@@ -229,10 +305,35 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // colour e at planes t-1, t-2, t-3 and of colour 1-e at t-1, t-2
   double oa = 0.0, ob = 0.0, ea = 0.0, eb = 0.0, wa = 0.0, wb = 0.0;
   double re1 = 0.0, re2 = 0.0, re3 = 0.0, ro1 = 0.0, ro2 = 0.0;
-  auto step = [&](int t, double& q, double& fe, double& fo) {
-    const double ot = shift ? b3_take(q) - m : b3_take(q);
+  // PRO: this thread's coarse cell (the parent of its pair) in the tile
+  const int ci = act ? (p + 1) + B3CX * ((y >> 1) + 3) : B3CX + 1;
+  // cl (PRO): an even plane's step, which takes coarse plane t/2+1 to the
+  // ring and loads plane (t+kB3Ahead)/2+1
+  auto step = [&](int t, double& q, double& fe, double& fo, double& ca, double& cb, bool cl) {
+    double ot = shift ? b3_take(q) - m : b3_take(q);
     const double ret = b3_take(fe), rot = b3_take(fo);
+    double cr = 0.0;
+    if (PRO && cl) cr = b3_take(ca) - b3_take(cb);
     load(t + kB3Ahead, q, fe, fo);
+    if (PRO && cl) cload(min((t + kB3Ahead) / 2 + 1, B3NC * lenc + 2), ca, cb);
+    if (PRO) {
+      // phi += prolong(phi - old) on the colour-(1-e) cell (prolong_at): the
+      // parent, its x tap on the cell's side, its y / z taps by the parity of
+      // the cell's row / plane (the column starts at even x, y and z)
+      const int cz0 = t >> 1;
+      const double* R0 = rc[cz0 & 3];
+      const double* Rz = rc[((t & 1) ? cz0 + 1 : cz0 - 1) & 3];
+      const bool lft = ((y + t) & 1) == e;
+      const double f0 = 0.25 * R0[ci];
+      const double fx = 0.25 * R0[lft ? ci - 1 : ci + 1];
+      const double fy = 0.25 * R0[(y & 1) ? ci + B3CX : ci - B3CX];
+      const double fz = 0.25 * Rz[ci];
+      ot = ot + (f0 + fx + fy + fz);
+      if (cl) {
+        const int c = t / 2 + 1;
+        if (c >= 0 && tid < B3CT) rc[c & 3][tid] = cr;
+      }
+    }
     const double* P0 = pl[t & 1][0];
     const double* P1 = pl[t & 1][1];
     const double* P2 = pl[t & 1][2];
@@ -278,25 +379,38 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // wait would drain them all.  Trailing steps past the column compute
   // nothing used either (their loads reload the last plane); the store wave
   // writes plane zend-1 in iteration zend+3.
-  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead];
+  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead], cas[kB3Ahead / 2], cbs[kB3Ahead / 2];
 #pragma unroll
   for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = 0.0;
+#pragma unroll
+  for (int u = 0; u < kB3Ahead / 2; u++) cas[u] = cbs[u] = 0.0;
+  // (t + u is even for odd u: t starts at -3 - kB3Ahead, odd)
   for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
 #pragma unroll
-    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u]);
+    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u], cas[u >> 1], cbs[u >> 1], (u & 1) == 1);
   }
 }
 
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
 
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st, bool push1) {
+                  const double* shift, hipStream_t st, bool push1, const LevelView* coarse, const int* ccols) {
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb3: box size must be 16");
+  const int p1 = push1 ? 1 : 0;
+  if (coarse) {
+    if (coarse->nc != B3NC || !ccols || shift)
+      throw std::runtime_error("launch_gsrb3: the correction form needs a 16^3 coarse level, its records, no shift");
+    if (op == OP_HELM)
+      k_gsrb3<OP_HELM, true><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, *coarse, ccols);
+    else
+      k_gsrb3<OP_LPL, true><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, *coarse, ccols);
+    return;
+  }
   if (op == OP_HELM)
-    k_gsrb3<OP_HELM><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, push1 ? 1 : 0);
+    k_gsrb3<OP_HELM, false><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, L, nullptr);
   else
-    k_gsrb3<OP_LPL><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, push1 ? 1 : 0);
+    k_gsrb3<OP_LPL, false><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, L, nullptr);
 }
 
 }  // namespace omg

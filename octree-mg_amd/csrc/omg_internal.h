@@ -190,6 +190,11 @@ struct Level {
   double* d_phi_buf = nullptr;
   int* d_b3 = nullptr;
   int n_b3 = 0;
+  std::vector<int> h_b3;   // (host copy, for the coarse records below)
+  // k_gsrb3's correct_children form: per column the coarse boxes around it
+  // (launch_gsrb3's ccols); null: the level's up-smoothing starts with
+  // k_prolong_smooth
+  int* d_b3c = nullptr;
   int* d_physbox = nullptr;          // boxes with a physical face (k_phys_gc after such a chain)
   int n_physbox = 0;
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
@@ -326,6 +331,7 @@ struct omg_ctx {
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
+  bool no_block3p = false;             // OMG_NO_BLOCK3P: correct_children by k_prolong_smooth, not k_gsrb3
   int b3_min_boxes = omg::kB3MinBoxes;  // smallest level for k_gsrb3 (OMG_BLOCK3_MIN_BOXES, tests)
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending

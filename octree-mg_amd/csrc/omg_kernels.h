@@ -60,8 +60,18 @@ bool gsrb3_op_ok(int op);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
 // halves are left stale: only for a pass that k_smooth_resid follows, which
 // reads colour e's and forms colour 1-e's itself)
+// coarse (k_gsrb3's correct_children form): before substep 1 the pass adds the
+// prolonged correction phi - old of the coarse level (mg_prolong_sparse of
+// correct_children, m_multigrid.f90:127-136) to the colour-(1-e) cells it
+// reads, and stores the coarse level's res = phi - old (interior and faces).
+// ccols: per workgroup kB3CRec ints, [0] = the column's y offset inside its
+// coarse boxes (0 / 8), then at 1 + 9*zc + 3*ys + xs the coarse boxes around
+// the column (zc = 0: below, 1..len/2: the column's own, then above).  The
+// column's fine boxes are the children of those (len even).
+constexpr int kB3CRec = 48;
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st, bool push1 = true);
+                  const double* shift, hipStream_t st, bool push1 = true, const LevelView* coarse = nullptr,
+                  const int* ccols = nullptr);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,

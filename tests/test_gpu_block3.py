@@ -8,7 +8,10 @@ phi into the level's second buffer.  The cases cover what changes around it:
 odd and even numbers of passes per cycle (phi left in either buffer between
 cycles and across FMG), the pending mean shift absorbed by its first substep
 (periodic Laplacian), Helmholtz, FMG with and without a guess, and the level
-with the pass switched off (OMG_NO_BLOCK3) in the same process."""
+with the pass switched off (OMG_NO_BLOCK3) in the same process.  The
+up-smoothing's first pass on the 512-box level is the correct_children form
+(its coarse level is the 64-box level below): the correction, substeps 1-3 and
+the coarse level's res in one pass; OMG_NO_BLOCK3P switches that form off."""
 import numpy as np
 import pytest
 
@@ -77,12 +80,14 @@ def test_block3_fmg_matches_oracle(have_guess):
         _assert_same(dev, orc)
 
 
-def test_block3_switch_off_same_bits(monkeypatch):
-    """OMG_NO_BLOCK3=1 (one substep per launch) and the default give the same
-    state after each cycle."""
+@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P"])
+def test_block3_switch_off_same_bits(monkeypatch, switch):
+    """OMG_NO_BLOCK3=1 (one substep per launch) / OMG_NO_BLOCK3P=1 (the
+    correction by k_prolong_smooth) and the default give the same state after
+    each cycle."""
     args = "16 128 128 128 2 v gsrb lpl 0 per sol 1 lb 0"
     dev, orc = _pair(args, 3, 2)
-    monkeypatch.setenv("OMG_NO_BLOCK3", "1")
+    monkeypatch.setenv(switch, "1")
     ref = DeviceBackend(parse(args))
     ref.mg.n_cycle_down, ref.mg.n_cycle_up = 3, 2
     ref.mg._push_methods()

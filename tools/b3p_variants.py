@@ -1,0 +1,36 @@
+"""Timing-only builds of k_gsrb3's correct_children form (not parity-correct):
+copies octree-mg_amd/csrc to /tmp, patches omg_block.hip, builds
+octree-mg_amd/_variants/libomg_b3p_<name>.so (load with OMG_LIB=...)."""
+import os, shutil, subprocess, sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VARIANTS = {
+    # coarse planes not loaded (the ring gets a register value)
+    "noload": [("a = b3_ld(C.phi, o);\n    b = b3_ld(cold, o);", "a = (double)o;\n    b = 0.0;")],
+    # no coarse res stores in the store wave
+    "nost": [("if (PRO) cflush(t + u);", "")],
+    # no coarse loads before the loop (planes -2, -1 stay zero)
+    "noprol": [("      cload(-2, a0, b0);\n      cload(-1, a1, b1);", "      a0 = b0 = a1 = b1 = 0.0;")],
+    # one coarse load per cell and no res stores (a precomputed res)
+    "half_nost": [("a = b3_ld(C.phi, o);\n    b = b3_ld(cold, o);", "a = b3_ld(C.phi, o);\n    b = 0.0;"),
+                  ("if (PRO) cflush(t + u);", "")],
+    # no correction added (its LDS reads die with it)
+    "nocorr": [("ot = ot + (f0 + fx + fy + fz);", "")],
+}
+names = sys.argv[1:] or list(VARIANTS)
+for name in names:
+    d = f"/tmp/b3pv/{name}"   # (omg_internal.h includes ../../include/omg.h: /tmp/include)
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs("/tmp/include", exist_ok=True)
+    shutil.copy(os.path.join(R, "include", "omg.h"), "/tmp/include/omg.h")
+    shutil.copytree(os.path.join(R, "octree-mg_amd", "csrc"), d)
+    p = os.path.join(d, "omg_block.hip")
+    s = open(p).read()
+    for a, b in VARIANTS[name]:
+        assert a in s, (name, a)
+        s = s.replace(a, b)
+    open(p, "w").write(s)
+    out = os.path.join(R, "octree-mg_amd", "_variants", f"libomg_b3p_{name}.so")
+    subprocess.run(["make", "-j8", "-C", d, f"OUT={out}"], check=True, stdout=subprocess.DEVNULL)
+    # the include path of omg_api.cpp (../../include/omg.h) resolves from the copy's parent
+    print("built", out)
