@@ -709,10 +709,16 @@ double* red_mean(omg_ctx* c, int ch);
 double allreduce(omg_ctx* c, double v, bool is_max);
 
 // smooth_boxes (m_multigrid.f90:404-424)
-void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0) {
+// want_res: the level above takes k_gsrb3's correct_children form next, which
+// reads this level's res = phi - old: the last three substeps run as one
+// k_gsrb3 pass that also stores it (the plain substeps first); returns whether
+// that pass ran.
+bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0,
+                  bool want_res = false) {
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps - skip_last;
-  if (!L) return;
+  bool res_done = false;
+  if (!L) return false;
   if (n_sub >= 1) rb_stale_above(c, lvl);
   // a pending phi shift is subtracted by the first tiled substep while it
   // loads (the values it reads are dead afterwards); otherwise applied now
@@ -765,7 +771,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
         launch_phys_gc(L->view(), bc, L->d_physbox, L->n_physbox, c->stream);
       }
       L->phi_gc_ok = true;
-      return;
+      return false;
     }
     for (int n = 1; n <= n_sub; n++) {
       if (L->n) {
@@ -784,7 +790,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
         fill_gc_lvl(c, lvl, 1);
       }
     }
-    return;
+    return false;
   }
   for (int n = first_substep; n <= n_sub; n++) {
     // substep n updates the cells with i+j+k+n even, i.e. colour e = n mod 2,
@@ -801,16 +807,20 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // substeps n, n+1, n+2 in one pass (k_gsrb3) into phi's other buffer: it
     // reads the neighbours' cells in their boxes, which equal its ghosts only
     // when they are consistent (phi_gc_ok), and writes every ghost face
-    if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
+    if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3 &&
+        !(want_res && (n_sub - n + 1) % 3 != 0)) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
       // the down-smoothing's last pass before k_smooth_resid (skip_last: it
       // runs the next substep, colour 0, and forms colour 0's ghosts itself
       // from colour 1, reading colour 1's only): push colour e = 1 alone
       const bool push1 = !(skip_last == 1 && n + 2 == n_sub && e == 1);
+      const bool res = want_res && n + 2 == n_sub && push1;
       {
-        Prof p(c, "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, push1);
+        Prof p(c, res ? "smoother_gsrb3r" : "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
+        launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, push1, nullptr,
+                     nullptr, 1, res);
       }
+      res_done = res;
       L->d_phi = other;
       n += 2;
       continue;
@@ -859,6 +869,7 @@ void smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     finish_halo(c, L, 1, !full_fill);
     if (full_fill) fill_gc_lvl(c, lvl, 1);
   }
+  return res_done;
 }
 
 bool tiled_level(omg_ctx* c, const Level* L) {
@@ -1158,19 +1169,24 @@ bool prolong_smooth(omg_ctx* c, int lvl) {
 // records (build_block3c), whose coarse level has consistent ghosts (the
 // reference's correction reads the parents' ghost cells; the pass reads the
 // neighbour parents' cells).
-bool correct_block3(omg_ctx* c, int l) {
+bool block3c_ok(omg_ctx* c, const Level* F) {
+  return F && F->d_b3c && !c->no_block3 && !c->no_block3p && c->smoother == OMG_SMOOTHER_GSRB &&
+         gsrb3_op_ok(c->op) && c->n_cycle_up * c->n_substeps >= 3;
+}
+// res_ready: the coarse level's last up pass stored its res = phi - old
+// (smooth_boxes' want_res), which the pass then reads instead of phi and old
+bool correct_block3(omg_ctx* c, int l, bool res_ready) {
   Level* F = level_ptr(c, l);
   Level* C = level_ptr(c, l - 1);
-  if (!F || !C || !F->d_b3c || c->no_block3 || c->no_block3p || c->smoother != OMG_SMOOTHER_GSRB ||
-      !gsrb3_op_ok(c->op) || c->n_cycle_up * c->n_substeps < 3 || !C->phi_gc_ok || C->shift_pending)
-    return false;
+  if (!block3c_ok(c, F) || !C || !C->phi_gc_ok || C->shift_pending) return false;
   if (F->shift_pending) materialize_level(c, F);
   rb_stale_above(c, l);
   double* other = F->d_phi == F->d_data ? F->d_phi_buf : F->d_data;
   {
     Prof p(c, "smoother_gsrb3p", 1.5 * F->n * F->nc * F->nc * F->nc, l);
     const LevelView cv = C->view();
-    launch_gsrb3(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, true, &cv, F->d_b3c);
+    launch_gsrb3(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, true, &cv, F->d_b3c,
+                 res_ready ? 2 : 1);
   }
   F->d_phi = other;
   F->phi_gc_ok = true;
@@ -1696,15 +1712,24 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
       if (res < c->res_rel * init_res || res < c->res_abs) break;
     }
   }
+  // res_ready: level l-1's last up pass stored its res (correct_children's
+  // phi - old) for level l's correct_children form.  A level whose level
+  // above takes that form (want_res) ends its up-smoothing with that pass, so
+  // it starts with k_prolong_smooth rather than the form itself (which leaves
+  // a plain last substep).
+  bool res_ready = false;
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
-    if (correct_block3(c, l)) {
-      smooth_boxes(c, l, c->n_cycle_up, 4);
+    const bool want_res = l < max_lvl && block3c_ok(c, level_ptr(c, l + 1)) && !c->no_block3r;
+    bool done = false;
+    if (!want_res && correct_block3(c, l, res_ready)) {
+      done = smooth_boxes(c, l, c->n_cycle_up, 4);
     } else if (prolong_smooth(c, l - 1)) {
-      smooth_boxes(c, l, c->n_cycle_up, 2);
+      done = smooth_boxes(c, l, c->n_cycle_up, 2, 0, want_res);
     } else {
       correct_and_fill(c, l - 1, c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_up >= 1);
-      smooth_boxes(c, l, c->n_cycle_up);
+      done = smooth_boxes(c, l, c->n_cycle_up, 1, 0, want_res);
     }
+    res_ready = done;
   }
   double max_res = 0.0;
   if (want_max_res) {
@@ -2880,6 +2905,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
     c->no_block3 = env_flag("OMG_NO_BLOCK3");
     c->no_block3p = env_flag("OMG_NO_BLOCK3P");
+    c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
     if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");

@@ -117,16 +117,23 @@ __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
 // prolonged correction as it is loaded (prolong_at's expression, omg_tiles.hip,
 // from the coarse tile in LDS: phi - old of the coarse level, a plane of it
 // loaded on every other step, kB3Ahead steps ahead like the fine planes);
-// colour e needs none (substep 1 overwrites it).  The store wave also stores
-// the coarse level's res = phi - old, which correct_children leaves there: the
-// column's own coarse cells, interior and the faces they are ghosts of.
-template <int OP, bool PRO>
+// colour e needs none (substep 1 overwrites it).  PRO 1: the tile is formed
+// from the coarse phi and old, and the store wave also stores the coarse
+// level's res = phi - old, which correct_children leaves there (the column's
+// own coarse cells, interior and the faces they are ghosts of); PRO 2: the
+// coarse level's last pass stored res already (RES), the tile loads it.
+// RES: the pass is the level's last up-smoothing pass and the level above
+// takes PRO 2: with the final plane the compute waves form res = phi - old
+// (old loaded with the plane kB3Ahead ahead), and the store wave stores it
+// with its ghost faces like phi.
+template <int OP, int PRO, bool RES>
 __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict__ dst,
                                                           const int* __restrict__ cols, double lambda, int e,
                                                           const double* __restrict__ shift, int push1, LevelView C,
                                                           const int* __restrict__ ccols) {
   __shared__ double pl[2][3][B3PL];
-  __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
+  // final plane: [row * B3CP + pair][colour e, 1-e (, their res)]
+  __shared__ double fin[2][B3NC * B3CP][RES ? 4 : 2];
   __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
   __shared__ double rc[PRO ? 4 : 1][PRO ? B3CT : 1];   // coarse phi - old, plane c in rc[c & 3]
   __shared__ unsigned cbo[PRO ? 36 : 1];      // the coarse record, byte offsets
@@ -160,6 +167,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // column's first coarse cell; threads past the tile load a duplicate)
   const int cyo = PRO ? cyo_s : 0, lenc = len >> 1;
   const double* __restrict__ cold = C.data + 2 * C.vstride;
+  const double* __restrict__ cres_in = C.data + 3 * C.vstride;
   const int ct = tid < B3CT ? tid : B3CT - 1;
   const int cxr = ct % B3CX - 3, cyy = cyo + ct / B3CX - 3;
   const int xsc = cxr < 0 ? 0 : (cxr < B3NC ? 1 : 2), ysc = cyy < 0 ? 0 : (cyy < B3NC ? 1 : 2);
@@ -169,8 +177,13 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     const int zsc = c < 0 ? 0 : (c >= B3NC * lenc ? lenc + 1 : (c >> 4) + 1);
     const int kc = c - B3NC * (zsc - 1) + 1;
     const unsigned o = cbo[9 * zsc + 3 * ysc + xsc] + 8u * B3HV * ((icc + jcc + kc) & 1) + cxy + PB * (kc - 1);
-    a = b3_ld(C.phi, o);
-    b = b3_ld(cold, o);
+    if (PRO == 2) {
+      a = b3_ld(cres_in, o);
+      b = 0.0;
+    } else {
+      a = b3_ld(C.phi, o);
+      b = b3_ld(cold, o);
+    }
   };
   if (PRO) {
     // coarse planes -2 and -1 (the first fine planes' parents and z taps)
@@ -192,12 +205,15 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     const int l = tid - B3NW * 64;
     double* __restrict__ dse = dst + e * B3HV;
     double* __restrict__ dso = dst + (1 - e) * B3HV;
+    double* __restrict__ rsb = L.data + 3 * L.vstride;   // RES: res, the level's own
+    double* __restrict__ rse = rsb + e * B3HV;
+    double* __restrict__ rso = rsb + (1 - e) * B3HV;
     auto flush = [&](int t) {
       const int z = t - 4;
       if (z < 0 || z >= zend) return;
       int k;
       const int r0 = kB3S * zbox(z, k);
-      const double(*F)[2] = fin[z & 1];
+      const auto* F = fin[z & 1];
       // colour e is the left cell of the pairs of row jr (0-based) at plane z
       auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
       // push1 == 0: only the colour-e cells go to the neighbours' ghosts (the
@@ -212,6 +228,10 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const double ve = F[q][0], vo = F[q][1];
         b3_st(dse, o, ve);
         b3_st(dso, o, vo);
+        if (RES) {
+          b3_st(rse, o, F[q][2]);
+          b3_st(rso, o, F[q][3]);
+        }
         if (k == 1 || k == B3NC) {
           const bool lf = leftv(jr);
           const double vl = lf ? ve : vo, vr = lf ? vo : ve;
@@ -219,6 +239,10 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
           if (push1 || lf) b3_st(dst, g + 8u * b3_gh(nb, il, j), vl);
           if (push1 || !lf) b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), vr);
+          if (RES) {
+            b3_st(rsb, g + 8u * b3_gh(nb, il, j), lf ? F[q][2] : F[q][3]);
+            b3_st(rsb, g + 8u * b3_gh(nb, il + 1, j), lf ? F[q][3] : F[q][2]);
+          }
         }
       }
       // x faces: per row the cells x = 0, 15, 16, 31 (lane: row l/4, which l%4)
@@ -227,18 +251,22 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const int pc = w == 0 ? 0 : (w == 1 ? B3H - 1 : (w == 2 ? B3H : 2 * B3H - 1));
         const int xs = 1 + pc / B3H;
         const bool lf = leftv(jr), wantl = (w & 1) == 0;   // x = 0, 16: a left cell; 15, 31: right
-        const double v = (wantl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
+        const int s = (wantl == lf) ? 0 : 1;
+        const double v = fin[z & 1][jr * B3CP + pc][s];
         const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
         if (push1 || wantl == lf) b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+        if (RES) b3_st(rsb, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), fin[z & 1][jr * B3CP + pc][2 + s]);
       }
       // y faces: the cells of rows j = 1 (lanes 0..31) and j = 16 (32..63)
       {
         const int jr = l < 32 ? 0 : B3NC - 1, x = l & 31;
         const int pc = x >> 1, xs = 1 + pc / B3H, i = x - B3NC * (xs - 1) + 1;
         const bool lf = leftv(jr), isl = (x & 1) == 0;
-        const double v = (isl == lf) ? fin[z & 1][jr * B3CP + pc][0] : fin[z & 1][jr * B3CP + pc][1];
+        const int s = (isl == lf) ? 0 : 1;
+        const double v = fin[z & 1][jr * B3CP + pc][s];
         const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
         if (push1 || isl == lf) b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+        if (RES) b3_st(rsb, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), fin[z & 1][jr * B3CP + pc][2 + s]);
       }
     };
     // PRO: res of the column's own coarse cells, plane cs in steps 2cs (rows
@@ -263,7 +291,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
 #pragma unroll
       for (int u = 0; u < kB3Ahead; u++) {
         flush(t + u);
-        if (PRO) cflush(t + u);
+        if (PRO == 1) cflush(t + u);
         __syncthreads();
       }
     }
@@ -288,16 +316,26 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   const double* __restrict__ src = L.phi + (1 - e) * B3HV;
   const double* __restrict__ rhe = L.data + L.vstride + e * B3HV;
   const double* __restrict__ rho = L.data + L.vstride + (1 - e) * B3HV;
+  const double* __restrict__ ole = L.data + 2 * L.vstride + e * B3HV;   // RES: old
+  const double* __restrict__ olo = L.data + 2 * L.vstride + (1 - e) * B3HV;
 
   // plane t: colour 1-e of phi, both colours of rhs (no branch: the waits
-  // for these loads are counted; planes past the end reload the last one)
-  auto load = [&](int t, double& q, double& fe, double& fo) {
+  // for these loads are counted; planes past the end reload the last one);
+  // RES: both colours of old at plane t-3 (final kB3Ahead steps later)
+  auto load = [&](int t, double& q, double& fe, double& fo, double& he, double& ho) {
     int k;
     const int zs = zbox(min(t, zend + 2), k);
     const unsigned o = bo[kB3S * zs + slot] + xyb + PB * (k - 1);
     q = b3_ld(src, o);
     fe = b3_ld(rhe, o);
     fo = b3_ld(rho, o);
+    if (RES) {
+      int k3;
+      const int zs3 = zbox(min(t - 3, zend + 2), k3);
+      const unsigned o3 = bo[kB3S * zs3 + slot] + xyb + PB * (k3 - 1);
+      he = b3_ld(ole, o3);
+      ho = b3_ld(olo, o3);
+    }
   };
 
   // V0: colour 1-e as loaded, planes t-2, t-1; V1: colour e after substep 1,
@@ -309,12 +347,18 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   const int ci = act ? (p + 1) + B3CX * ((y >> 1) + 3) : B3CX + 1;
   // cl (PRO): an even plane's step, which takes coarse plane t/2+1 to the
   // ring and loads plane (t+kB3Ahead)/2+1
-  auto step = [&](int t, double& q, double& fe, double& fo, double& ca, double& cb, bool cl) {
+  auto step = [&](int t, double& q, double& fe, double& fo, double& he, double& ho, double& ca, double& cb,
+                  bool cl) {
     double ot = shift ? b3_take(q) - m : b3_take(q);
     const double ret = b3_take(fe), rot = b3_take(fo);
-    double cr = 0.0;
-    if (PRO && cl) cr = b3_take(ca) - b3_take(cb);
-    load(t + kB3Ahead, q, fe, fo);
+    double cr = 0.0, hte = 0.0, hto = 0.0;
+    if (PRO == 1 && cl) cr = b3_take(ca) - b3_take(cb);
+    if (PRO == 2 && cl) cr = b3_take(ca);
+    if (RES) {
+      hte = b3_take(he);
+      hto = b3_take(ho);
+    }
+    load(t + kB3Ahead, q, fe, fo, he, ho);
     if (PRO && cl) cload(min((t + kB3Ahead) / 2 + 1, B3NC * lenc + 2), ca, cb);
     if (PRO) {
       // phi += prolong(phi - old) on the colour-(1-e) cell (prolong_at): the
@@ -359,6 +403,10 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
       double* F = fin[(t - 3) & 1][fi];
       F[0] = s3;
       F[1] = wb;
+      if (RES) {
+        F[2] = s3 - hte;
+        F[3] = wb - hto;
+      }
     }
     if (act) {
       double* W = pl[(t + 1) & 1][0];
@@ -379,38 +427,46 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // wait would drain them all.  Trailing steps past the column compute
   // nothing used either (their loads reload the last plane); the store wave
   // writes plane zend-1 in iteration zend+3.
-  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead], cas[kB3Ahead / 2], cbs[kB3Ahead / 2];
+  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead], hes[kB3Ahead], hos[kB3Ahead];
+  double cas[kB3Ahead / 2], cbs[kB3Ahead / 2];
 #pragma unroll
-  for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = 0.0;
+  for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = hes[u] = hos[u] = 0.0;
 #pragma unroll
   for (int u = 0; u < kB3Ahead / 2; u++) cas[u] = cbs[u] = 0.0;
   // (t + u is even for odd u: t starts at -3 - kB3Ahead, odd)
   for (int t = -3 - kB3Ahead; t <= zend + 3; t += kB3Ahead) {
 #pragma unroll
-    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u], cas[u >> 1], cbs[u >> 1], (u & 1) == 1);
+    for (int u = 0; u < kB3Ahead; u++)
+      step(t + u, qs[u], fes[u], fos[u], hes[u], hos[u], cas[u >> 1], cbs[u >> 1], (u & 1) == 1);
   }
 }
 
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
 
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st, bool push1, const LevelView* coarse, const int* ccols) {
+                  const double* shift, hipStream_t st, bool push1, const LevelView* coarse, const int* ccols,
+                  int coarse_mode, bool res) {
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb3: box size must be 16");
   const int p1 = push1 ? 1 : 0;
-  if (coarse) {
-    if (coarse->nc != B3NC || !ccols || shift)
-      throw std::runtime_error("launch_gsrb3: the correction form needs a 16^3 coarse level, its records, no shift");
-    if (op == OP_HELM)
-      k_gsrb3<OP_HELM, true><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, *coarse, ccols);
-    else
-      k_gsrb3<OP_LPL, true><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, *coarse, ccols);
-    return;
+  const int pm = coarse ? coarse_mode : 0;
+  if (coarse && (coarse->nc != B3NC || !ccols || shift || (pm != 1 && pm != 2)))
+    throw std::runtime_error("launch_gsrb3: the correction form needs a 16^3 coarse level, its records, no shift");
+  if (res && (pm || !push1))
+    throw std::runtime_error("launch_gsrb3: res = phi - old only on a plain pass that pushes both colours");
+  const LevelView& C = coarse ? *coarse : L;
+#define OMG_B3(OPV, PMV, RV) k_gsrb3<OPV, PMV, RV><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, C, ccols)
+  const bool helm = op == OP_HELM;
+  if (pm == 1) {
+    if (helm) OMG_B3(OP_HELM, 1, false); else OMG_B3(OP_LPL, 1, false);
+  } else if (pm == 2) {
+    if (helm) OMG_B3(OP_HELM, 2, false); else OMG_B3(OP_LPL, 2, false);
+  } else if (res) {
+    if (helm) OMG_B3(OP_HELM, 0, true); else OMG_B3(OP_LPL, 0, true);
+  } else {
+    if (helm) OMG_B3(OP_HELM, 0, false); else OMG_B3(OP_LPL, 0, false);
   }
-  if (op == OP_HELM)
-    k_gsrb3<OP_HELM, false><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, L, nullptr);
-  else
-    k_gsrb3<OP_LPL, false><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, L, nullptr);
+#undef OMG_B3
 }
 
 }  // namespace omg

@@ -67,11 +67,17 @@ bool gsrb3_op_ok(int op);
 // ccols: per workgroup kB3CRec ints, [0] = the column's y offset inside its
 // coarse boxes (0 / 8), then at 1 + 9*zc + 3*ys + xs the coarse boxes around
 // the column (zc = 0: below, 1..len/2: the column's own, then above).  The
-// column's fine boxes are the children of those (len even).
+// column's fine boxes are the children of those (len even).  coarse_mode 1:
+// the correction from the coarse phi and old, and the pass stores the coarse
+// res; 2: the coarse res is already stored (its last pass ran with `res`) and
+// is what the pass reads.
+// res: the pass also stores this level's res = phi - old (interior and faces),
+// what correct_children of the level above stores before it prolongs
+// (a plain pass only, push1).
 constexpr int kB3CRec = 48;
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, bool push1 = true, const LevelView* coarse = nullptr,
-                  const int* ccols = nullptr);
+                  const int* ccols = nullptr, int coarse_mode = 1, bool res = false);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,

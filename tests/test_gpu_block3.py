@@ -20,13 +20,17 @@ from tests.mgdriver import OPS, DeviceBackend, OracleBackend, parse, setup_probl
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _small_levels(monkeypatch):
+@pytest.fixture(autouse=True, params=["512", "64"])
+def _small_levels(monkeypatch, request):
     """The 128^3 trees here have a 512-box finest level; the pass serves
     levels of 4096 boxes and up by default (kB3MinBoxes), so lower the bound
     for these tests (read at context creation); the full-size golden
-    c3_per512_box16 runs the default bound."""
-    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", "512")
+    c3_per512_box16 runs the default bound.  At 512 the finest level's
+    correct_children form forms the coarse phi - old itself and stores the
+    coarse res; at 64 the 64-box level runs the pass too, and its last
+    up-smoothing pass stores its res for the form above it to read (C3's
+    arrangement on levels 0 and 1)."""
+    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", request.param)
 
 
 def _stored_mask(nc):
@@ -80,11 +84,11 @@ def test_block3_fmg_matches_oracle(have_guess):
         _assert_same(dev, orc)
 
 
-@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P"])
+@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P", "OMG_NO_BLOCK3R"])
 def test_block3_switch_off_same_bits(monkeypatch, switch):
     """OMG_NO_BLOCK3=1 (one substep per launch) / OMG_NO_BLOCK3P=1 (the
-    correction by k_prolong_smooth) and the default give the same state after
-    each cycle."""
+    correction by k_prolong_smooth) / OMG_NO_BLOCK3R=1 (no res from the coarse
+    level's last pass) and the default give the same state after each cycle."""
     args = "16 128 128 128 2 v gsrb lpl 0 per sol 1 lb 0"
     dev, orc = _pair(args, 3, 2)
     monkeypatch.setenv(switch, "1")

@@ -14,6 +14,10 @@ VARIANTS = {
     # one coarse load per cell and no res stores (a precomputed res)
     "half_nost": [("a = b3_ld(C.phi, o);\n    b = b3_ld(cold, o);", "a = b3_ld(C.phi, o);\n    b = 0.0;"),
                   ("if (PRO) cflush(t + u);", "")],
+    # every store of the pass non-temporal
+    "ntst": [('"global_store_dwordx2 %0, %1, %2\\n\\ts_nop 1"', '"global_store_dwordx2 %0, %1, %2 nt\\n\\ts_nop 1"')],
+    # stores with sc0 sc1 (write-through past the L2's coherence point)
+    "scst": [('"global_store_dwordx2 %0, %1, %2\\n\\ts_nop 1"', '"global_store_dwordx2 %0, %1, %2 sc0 sc1\\n\\ts_nop 1"')],
     # no correction added (its LDS reads die with it)
     "nocorr": [("ot = ot + (f0 + fx + fy + fz);", "")],
 }
