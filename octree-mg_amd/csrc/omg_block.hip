@@ -80,9 +80,11 @@ __device__ __forceinline__ double b3_take(double v) {
 // compute waves' (one kernel), and once stores and loads are both pending it
 // treats vmcnt as out of order and waits for vmcnt(0) at every load use,
 // which would drain the loads in flight.  Nothing in the kernel reads what
-// these write.  base: wave-uniform, off: bytes (< 4 GiB).
+// these write.  base: wave-uniform, off: bytes (< 4 GiB).  Non-temporal:
+// nothing re-reads the pass's output before it leaves the L2 (C3 4.49 against
+// 4.38 ms per cycle with nt, profiles/r05/s31_block3_ntst_ab.txt).
 __device__ __forceinline__ void b3_st(double* base, unsigned off, double v) {
-  asm volatile("global_store_dwordx2 %0, %1, %2\n\ts_nop 1" : : "v"(off), "v"(v), "s"(base));
+  asm volatile("global_store_dwordx2 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(v), "s"(base));
 }
 __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
