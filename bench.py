@@ -33,7 +33,9 @@ per level cell per substep (24 B per cell update), timed with
 HIP events on the library's stream in a separate profiled cycle, against
 8 TB/s HBM3E; traffic from the committed rocprofv3 PMC summary.  On C3's
 periodic finest level the kernel is k_gsrb3 (three substeps per pass,
-omg_block.hip): the same rule over its 1.5 cell updates per level cell, and
+omg_block.hip; the down-smoothing's pass, one per cycle, the up-smoothing's
+being its correct_children form): the same rule over its 1.5 cell updates per
+level cell, and
 beside it the pass's own minimum HBM bytes (phi of one colour and rhs in,
 phi and the ghost faces out: 20 B per cell + 12 KiB per box).
 cpu_baseline: the reference itself (oracle/_ref, amdflang -O2 + MPICH) on the
@@ -66,7 +68,7 @@ METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
 # also reports what these do not account for
-KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
+KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gsrb3p", "smoother_gsrb3r", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
                    "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
 COMM_FAMILIES = ("comm", "comm_overlap")
@@ -79,7 +81,7 @@ def pmc_traffic(per_gpu_cells, block3=False):
     k_gsrb3 (one workgroup per column of 2 x 4 boxes; its loads are 8 B per
     lane, for which the guide's x2 is uncalibrated)."""
     import glob
-    name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1>") if block3 else \
+    name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1, 0, false>") if block3 else \
         ("pmc_smoother.json", r"void omg::k_gsrb_tile<16, 1[,>]")
     wgs = per_gpu_cells // BOX ** 3 // (8 if block3 else 1)
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
@@ -268,7 +270,8 @@ def roofline(smoother, per_gpu_cells, boxes_hi, hi):
     traffic, tsrc = pmc_traffic(per_gpu_cells, block3)
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-           "kernel": (f"k_gsrb3<OP_LPL> (three red-black substeps per pass) on level {hi} ({boxes_hi} boxes)"
+           "kernel": (f"k_gsrb3<OP_LPL, 0, false> (three red-black substeps per pass, the down-smoothing's) "
+                      f"on level {hi} ({boxes_hi} boxes)"
                       if block3 else f"k_gsrb_tile<16,OP_LPL> on level {hi} ({boxes_hi} boxes)"),
            "launches": n, "avg_launch_us": dur * 1e6,
            "alg_bytes_per_launch": alg_bytes,
