@@ -1,10 +1,17 @@
-"""Timing-only builds of k_gsrb3's correct_children form (not parity-correct):
-copies octree-mg_amd/csrc to /tmp, patches omg_block.hip, builds
+"""Timing-only builds (not parity-correct unless noted): copies
+octree-mg_amd/csrc to /tmp, patches omg_block.hip (or FILES[name]), builds
 octree-mg_amd/_variants/libomg_b3p_<name>.so (load with OMG_LIB=...)."""
 import os, shutil, subprocess, sys
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FILES = {"subnt": "omg_tiles.hip", "subntld": "omg_tiles.hip"}   # (default: omg_block.hip)
 VARIANTS = {
+    # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
+    # of scratch), the other forms unchanged
+    "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
+    # subtract_rhs pass (k_box_sums3<SUB>) with non-temporal stores / loads too
+    "subnt": [("kSubNTLd = false, kSubNTSt = false", "kSubNTLd = false, kSubNTSt = true")],
+    "subntld": [("kSubNTLd = false, kSubNTSt = false", "kSubNTLd = true, kSubNTSt = true")],
     # coarse planes not loaded (the ring gets a register value)
     "noload": [("a = b3_ld(C.phi, o);\n    b = b3_ld(cold, o);", "a = (double)o;\n    b = 0.0;")],
     # no coarse res stores in the store wave
@@ -31,7 +38,7 @@ for name in names:
     os.makedirs("/tmp/include", exist_ok=True)
     shutil.copy(os.path.join(R, "include", "omg.h"), "/tmp/include/omg.h")
     shutil.copytree(os.path.join(R, "octree-mg_amd", "csrc"), d)
-    p = os.path.join(d, "omg_block.hip")
+    p = os.path.join(d, FILES.get(name, "omg_block.hip"))
     s = open(p).read()
     for a, b in VARIANTS[name]:
         assert a in s, (name, a)
