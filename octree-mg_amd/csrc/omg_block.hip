@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   __shared__ double fin[2][B3NC * B3CP][RES ? 4 : 2];
   __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
   __shared__ double rc[PRO ? 4 : 1][PRO ? B3CT : 1];   // coarse phi - old, plane c in rc[c & 3]
-  __shared__ unsigned cbo[PRO ? 36 : 1];      // the coarse record, byte offsets
+  __shared__ unsigned cbo[PRO ? kB3CSlots : 1];   // the coarse record, byte offsets
   __shared__ int len_s, cyo_s;
   const int tid = threadIdx.x;
   const int cq = xcd_box(blockIdx.x, gridDim.x);
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   }
   if (PRO) {
     const int q = tid - kB3Rec;
-    if (q >= 0 && q < 37) {
+    if (q >= 0 && q < 1 + kB3CSlots) {
       const int v = ccols[(long long)cq * kB3CRec + q];
       if (q == 0) cyo_s = v;
       else cbo[q - 1] = (unsigned)v * (unsigned)(C.stride * 8);

@@ -74,7 +74,8 @@ bool gsrb3_op_ok(int op);
 // res: the pass also stores this level's res = phi - old (interior and faces),
 // what correct_children of the level above stores before it prolongs
 // (a plain pass only, push1).
-constexpr int kB3CRec = 48;
+constexpr int kB3CSlots = 9 * (kB3MaxZ / 2 + 2);                // coarse boxes per record
+constexpr int kB3CRec = (1 + kB3CSlots + 15) / 16 * 16;
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, bool push1 = true, const LevelView* coarse = nullptr,
                   const int* ccols = nullptr, int coarse_mode = 1, bool res = false);

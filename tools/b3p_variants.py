@@ -4,11 +4,20 @@ octree-mg_amd/_variants/libomg_b3p_<name>.so (load with OMG_LIB=...)."""
 import os, shutil, subprocess, sys
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FILES = {"subnt": "omg_tiles.hip", "subntld": "omg_tiles.hip"}   # (default: omg_block.hip)
+FILES = {"subnt": "omg_tiles.hip", "subntld": "omg_tiles.hip", "z8": "omg_kernels.h", "z2": "omg_kernels.h"}
+# (default: omg_block.hip)
 VARIANTS = {
     # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
     # of scratch), the other forms unchanged
     "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
+    # columns of 8 / 2 boxes in z (parity-correct)
+    "z8": [("constexpr int kB3MaxZ = 4;", "constexpr int kB3MaxZ = 8;")],
+    "z2": [("constexpr int kB3MaxZ = 4;", "constexpr int kB3MaxZ = 2;")],
+    # the store wave idle (no flush at all) / interior stores only (no ghost pushes)
+    "nostw": [("        flush(t + u);\n", "")],
+    "nopush": [("        if (k == 1 || k == B3NC) {\n          const bool lf = leftv(jr);", "        if (false) {\n          const bool lf = leftv(jr);"),
+               ("      // x faces: per row the cells x = 0, 15, 16, 31 (lane: row l/4, which l%4)\n      {", "      if (false) {"),
+               ("      // y faces: the cells of rows j = 1 (lanes 0..31) and j = 16 (32..63)\n      {", "      if (false) {")],
     # subtract_rhs pass (k_box_sums3<SUB>) with non-temporal stores / loads too
     "subnt": [("kSubNTLd = false, kSubNTSt = false", "kSubNTLd = false, kSubNTSt = true")],
     "subntld": [("kSubNTLd = false, kSubNTSt = false", "kSubNTLd = true, kSubNTSt = true")],

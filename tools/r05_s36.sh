@@ -1,0 +1,14 @@
+# round 5 step 36: builds of the library with one change each
+# (tools/b3p_variants.py): k_gsrb3 with the store wave idle (nostw) / without ghost pushes (nopush); C3 ms per cycle
+O=gpurun_out/r05/s36
+mkdir -p $O
+R=$PWD
+for round in 1 2; do
+  for v in default nostw nopush; do
+    echo "== round $round $v" >> $O/ab.txt
+    if [ $v = default ]; then unset OMG_LIB; else export OMG_LIB=$R/octree-mg_amd/_variants/libomg_b3p_$v.so; fi
+    timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C3 >> $O/ab.txt 2>&1 || exit 1
+  done
+done
+unset OMG_LIB
+grep -E "^==|^C3 " $O/ab.txt
