@@ -2365,9 +2365,13 @@ void build_block3(omg_ctx* c, Level& L) {
   };
   std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
   std::vector<int> covered(n, 0);
-  // columns of kB3MaxZ boxes (on the 4096-box level of C3, two-box columns,
-  // twice the workgroups, took 110 us a pass against 102)
-  const int nzb = kB3MaxZ;
+  // columns of 8 boxes where that still leaves >= 2048 workgroups (two
+  // rounds of two per CU), else 4: C3's level 1 (32768 boxes) 873 / 773 us
+  // per pass against 898 / 789 with 4 (profiles/r05/s38_block3_z8_ab.txt);
+  // on its 4096-box level 8 gained nothing, and two-box columns, twice the
+  // workgroups, took 110 us a pass against 102
+  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 8 : 4);
+  static_assert(kB3MaxZ >= 8, "column records hold 8 boxes");
   for (int h = 0; h < n; h++) {
     if (ixd(h, 0) % kB3TX || ixd(h, 2) % nzb) continue;
     std::vector<int> zc{h};
@@ -2908,6 +2912,8 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
     if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
+    // (tests: the column length, 2 / 4 / 8 boxes; OMG_BLOCK3_COLUMN)
+    if (const char* v = getenv("OMG_BLOCK3_COLUMN")) c->b3_col = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

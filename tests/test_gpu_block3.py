@@ -20,7 +20,7 @@ from tests.mgdriver import OPS, DeviceBackend, OracleBackend, parse, setup_probl
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["512", "64"])
+@pytest.fixture(autouse=True, params=["512", "64", "64-col8"])
 def _small_levels(monkeypatch, request):
     """The 128^3 trees here have a 512-box finest level; the pass serves
     levels of 4096 boxes and up by default (kB3MinBoxes), so lower the bound
@@ -29,8 +29,12 @@ def _small_levels(monkeypatch, request):
     correct_children form forms the coarse phi - old itself and stores the
     coarse res; at 64 the 64-box level runs the pass too, and its last
     up-smoothing pass stores its res for the form above it to read (C3's
-    arrangement on levels 0 and 1)."""
-    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", request.param)
+    arrangement on levels 0 and 1).  64-col8: columns of 8 boxes (C3's level
+    1 takes them; here the 128^3 tree's 512-box level, its whole z extent)."""
+    bound, _, col = request.param.partition("-col")
+    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", bound)
+    if col:
+        monkeypatch.setenv("OMG_BLOCK3_COLUMN", col)
 
 
 def _stored_mask(nc):

@@ -4,15 +4,16 @@ octree-mg_amd/_variants/libomg_b3p_<name>.so (load with OMG_LIB=...)."""
 import os, shutil, subprocess, sys
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FILES = {"subnt": "omg_tiles.hip", "subntld": "omg_tiles.hip", "z8": "omg_kernels.h", "z2": "omg_kernels.h"}
+FILES = {"subnt": "omg_tiles.hip", "subntld": "omg_tiles.hip", "z8": "omg_api.cpp", "z2": "omg_api.cpp"}
 # (default: omg_block.hip)
 VARIANTS = {
     # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
     # of scratch), the other forms unchanged
     "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
-    # columns of 8 / 2 boxes in z (parity-correct)
-    "z8": [("constexpr int kB3MaxZ = 4;", "constexpr int kB3MaxZ = 8;")],
-    "z2": [("constexpr int kB3MaxZ = 4;", "constexpr int kB3MaxZ = 2;")],
+    # columns of 8 / 2 boxes in z on every level (parity-correct; r05/s38, when
+    # the product had 4: 8 is now its choice on levels of >= 32768 boxes)
+    "z8": [("const int nzb = L.n / (kB3TX * 8) >= 2048 ? 8 : 4;", "const int nzb = 8;")],
+    "z2": [("const int nzb = L.n / (kB3TX * 8) >= 2048 ? 8 : 4;", "const int nzb = 2;")],
     # the store wave idle (no flush at all) / interior stores only (no ghost pushes)
     "nostw": [("        flush(t + u);\n", "")],
     "nopush": [("        if (k == 1 || k == B3NC) {\n          const bool lf = leftv(jr);", "        if (false) {\n          const bool lf = leftv(jr);"),
