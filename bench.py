@@ -78,17 +78,23 @@ def pmc_traffic(per_gpu_cells, block3=False):
     """HBM bytes per launch of the finest-level smoother from the newest
     committed PMC summary (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2
     + WRITE_SIZE, the MI355X guide's gfx950 correction), or None.  block3:
-    k_gsrb3 (one workgroup per column of 2 x 4 boxes; its loads are 8 B per
-    lane, for which the guide's x2 is uncalibrated)."""
+    k_gsrb3 (one workgroup per column of 2 x 16 boxes on C3's level 1; its
+    loads are 8 B per lane, for which the guide's x2 is uncalibrated)."""
     import glob
     name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1, 0, false>") if block3 else \
         ("pmc_smoother.json", r"void omg::k_gsrb_tile<16, 1[,>]")
-    wgs = per_gpu_cells // BOX ** 3 // (8 if block3 else 1)
+    # (k_gsrb3: the finest level's launch is the one with the most workgroups,
+    # one per column of boxes, whatever the column length)
+    wgs = per_gpu_cells // BOX ** 3
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
         try:
             d = json.load(open(f))
-            for k, e in d["kernels"].items():
-                if re.match(pat, k) and "hbm_bytes_per_launch" in e and e["workgroups"] == wgs:
+            hits = [e for k, e in d["kernels"].items() if re.match(pat, k) and "hbm_bytes_per_launch" in e]
+            if block3 and hits:
+                e = max(hits, key=lambda e: e["workgroups"])
+                return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+            for e in hits:
+                if e["workgroups"] == wgs:
                     return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
         except (OSError, ValueError, KeyError):
             continue

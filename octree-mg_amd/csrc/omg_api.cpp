@@ -2365,13 +2365,13 @@ void build_block3(omg_ctx* c, Level& L) {
   };
   std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
   std::vector<int> covered(n, 0);
-  // columns of 8 boxes where that still leaves >= 2048 workgroups (two
-  // rounds of two per CU), else 4: C3's level 1 (32768 boxes) 873 / 773 us
-  // per pass against 898 / 789 with 4 (profiles/r05/s38_block3_z8_ab.txt);
-  // on its 4096-box level 8 gained nothing, and two-box columns, twice the
-  // workgroups, took 110 us a pass against 102
-  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 8 : 4);
-  static_assert(kB3MaxZ >= 8, "column records hold 8 boxes");
+  // columns of 16 boxes on levels of >= 32768 boxes, else 4: C3's level 1
+  // 857 / 759 us per pass against 875 / 772 with 8 (1024 workgroups, fewer
+  // halo planes per box; profiles/r05/s40_block3_z16_ab.txt) and 898 / 789
+  // with 4 (s38); on its 4096-box level 8 gained nothing, and two-box columns,
+  // twice the workgroups, took 110 us a pass against 102
+  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 16 : 4);
+  static_assert(kB3MaxZ >= 16, "column records hold 16 boxes");
   for (int h = 0; h < n; h++) {
     if (ixd(h, 0) % kB3TX || ixd(h, 2) % nzb) continue;
     std::vector<int> zc{h};
@@ -2912,7 +2912,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
     if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
-    // (tests: the column length, 2 / 4 / 8 boxes; OMG_BLOCK3_COLUMN)
+    // (tests: the column length, 2 .. 16 boxes, even; OMG_BLOCK3_COLUMN)
     if (const char* v = getenv("OMG_BLOCK3_COLUMN")) c->b3_col = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");

@@ -54,7 +54,7 @@ inline bool gs_tiled(int nc, int op, bool has_rb) {
 // neighbour).  Levels of 16^3 boxes whose faces are all same-GPU boxes.
 constexpr int kB3TX = 2;                         // boxes per tile in x
 constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
-constexpr int kB3MaxZ = 8;                       // boxes per column in z (at most)
+constexpr int kB3MaxZ = 16;                      // boxes per column in z (at most)
 constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
 bool gsrb3_op_ok(int op);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)

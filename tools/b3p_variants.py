@@ -10,10 +10,12 @@ VARIANTS = {
     # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
     # of scratch), the other forms unchanged
     "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
-    # columns of 8 / 2 boxes in z on every level (parity-correct; r05/s38, when
-    # the product had 4: 8 is now its choice on levels of >= 32768 boxes)
-    "z8": [("const int nzb = L.n / (kB3TX * 8) >= 2048 ? 8 : 4;", "const int nzb = 8;")],
-    "z2": [("const int nzb = L.n / (kB3TX * 8) >= 2048 ? 8 : 4;", "const int nzb = 2;")],
+    # 2 / 6 planes of loads in flight instead of 4 (parity-correct)
+    "a2": [("constexpr int kB3Ahead = 4;", "constexpr int kB3Ahead = 2;")],
+    "a6": [("constexpr int kB3Ahead = 4;", "constexpr int kB3Ahead = 6;")],
+    # (column lengths: r05/s38 measured 8 and 2 against 4, s40 16 against 8;
+    # the product now takes 16 on levels of >= 32768 boxes; OMG_BLOCK3_COLUMN
+    # sets any even length up to kB3MaxZ at run time)
     # the store wave idle (no flush at all) / interior stores only (no ghost pushes)
     "nostw": [("        flush(t + u);\n", "")],
     "nopush": [("        if (k == 1 || k == B3NC) {\n          const bool lf = leftv(jr);", "        if (false) {\n          const bool lf = leftv(jr);"),
@@ -48,12 +50,13 @@ for name in names:
     os.makedirs("/tmp/include", exist_ok=True)
     shutil.copy(os.path.join(R, "include", "omg.h"), "/tmp/include/omg.h")
     shutil.copytree(os.path.join(R, "octree-mg_amd", "csrc"), d)
-    p = os.path.join(d, FILES.get(name, "omg_block.hip"))
-    s = open(p).read()
-    for a, b in VARIANTS[name]:
+    for rep in VARIANTS[name]:
+        f, a, b = rep if len(rep) == 3 else (FILES.get(name, "omg_block.hip"),) + tuple(rep)
+        p = os.path.join(d, f)
+        s = open(p).read()
         assert a in s, (name, a)
         s = s.replace(a, b)
-    open(p, "w").write(s)
+        open(p, "w").write(s)
     out = os.path.join(R, "octree-mg_amd", "_variants", f"libomg_b3p_{name}.so")
     subprocess.run(["make", "-j8", "-C", d, f"OUT={out}"], check=True, stdout=subprocess.DEVNULL)
     # the include path of omg_api.cpp (../../include/omg.h) resolves from the copy's parent
