@@ -10,6 +10,16 @@ VARIANTS = {
     # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
     # of scratch), the other forms unchanged
     "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
+    # the periodic rhs pass writes back only the pairs whose bits change
+    # (parity-correct: the values are the same either way)
+    "subchg": [("omg_tiles.hip", """        v[r].x = v[r].x - m;
+        v[r].y = v[r].y - m;
+        if (own[r]) sums_st<kSubNTSt>(src[r] + rc, v[r]);""", """        const double2 o = v[r];
+        v[r].x = o.x - m;
+        v[r].y = o.y - m;
+        const bool chg = __double_as_longlong(v[r].x) != __double_as_longlong(o.x) ||
+                         __double_as_longlong(v[r].y) != __double_as_longlong(o.y);
+        if (own[r] && chg) sums_st<kSubNTSt>(src[r] + rc, v[r]);""")],
     # 2 / 6 planes of loads in flight instead of 4 (parity-correct)
     "a2": [("constexpr int kB3Ahead = 4;", "constexpr int kB3Ahead = 2;")],
     "a6": [("constexpr int kB3Ahead = 4;", "constexpr int kB3Ahead = 6;")],
