@@ -319,6 +319,10 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   const double* __restrict__ rhe = L.data + L.vstride + e * B3HV;
   const double* __restrict__ rho = L.data + L.vstride + (1 - e) * B3HV;
   const double* __restrict__ ole = L.data + 2 * L.vstride + e * B3HV;   // RES: old
+  // (only the box columns' old is used: the halo threads all load one cell of
+  // the tile's first box, a single line per plane)
+  const int slot3 = ctr ? slot : 1 + B3XS;
+  const unsigned xyb3 = ctr ? xyb : 0u;
   const double* __restrict__ olo = L.data + 2 * L.vstride + (1 - e) * B3HV;
 
   // plane t: colour 1-e of phi, both colours of rhs (no branch: the waits
@@ -334,7 +338,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     if (RES) {
       int k3;
       const int zs3 = zbox(min(t - 3, zend + 2), k3);
-      const unsigned o3 = bo[kB3S * zs3 + slot] + xyb + PB * (k3 - 1);
+      const unsigned o3 = bo[kB3S * zs3 + slot3] + xyb3 + PB * (k3 - 1);
       he = b3_ld(ole, o3);
       ho = b3_ld(olo, o3);
     }
