@@ -52,6 +52,9 @@ constexpr int B3XS = kB3TX + 2;                  // record slots per row
 // planes of loads in flight (2 / 3 / 4 / 5 / 6 ahead measured: 4 best, C3
 // 4.68 ms; more costs a workgroup per CU, profiles/r05/s17)
 constexpr int kB3Ahead = 4;
+// every thread loads its own cells' rhs (false: only where a substep's result
+// is used, tools/b3p_variants.py "rhsall" sets it true for the A/B)
+constexpr bool kB3HaloRhs = false;
 static_assert(kB3Ahead % 2 == 0, "coarse planes are loaded on the even planes' steps");
 // the correction form: the coarse tile of a plane, cx in [-3, kB3TX*8+2] and
 // cy in [-3, 10] around the column's coarse cells (the fine tile's parents
@@ -325,16 +328,24 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   const unsigned xyb3 = ctr ? xyb : 0u;
   const double* __restrict__ olo = L.data + 2 * L.vstride + (1 - e) * B3HV;
 
+  // rhs is used where a substep's result is: colour e (substeps 1 and 3) on
+  // the pairs within 2 cells of the tile's boxes, colour 1-e (substep 2)
+  // within 1; elsewhere the thread loads one shared line of the first box
+  // (what its substeps compute there is not used, as for the outermost halo)
+  const bool nde = kB3HaloRhs || (act && p >= 1 && p <= B3NPX - 2 && y >= -2 && y <= B3NC + 1);
+  const bool ndo = kB3HaloRhs || (nde && y >= -1 && y <= B3NC);
+  const int sle = nde ? slot : 1 + B3XS, slo = ndo ? slot : 1 + B3XS;
+  const unsigned xye = nde ? xyb : 0u, xyo = ndo ? xyb : 0u;
   // plane t: colour 1-e of phi, both colours of rhs (no branch: the waits
   // for these loads are counted; planes past the end reload the last one);
   // RES: both colours of old at plane t-3 (final kB3Ahead steps later)
   auto load = [&](int t, double& q, double& fe, double& fo, double& he, double& ho) {
     int k;
     const int zs = zbox(min(t, zend + 2), k);
-    const unsigned o = bo[kB3S * zs + slot] + xyb + PB * (k - 1);
-    q = b3_ld(src, o);
-    fe = b3_ld(rhe, o);
-    fo = b3_ld(rho, o);
+    const unsigned po = PB * (k - 1);
+    q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    fe = b3_ld(rhe, bo[kB3S * zs + sle] + xye + po);
+    fo = b3_ld(rho, bo[kB3S * zs + slo] + xyo + po);
     if (RES) {
       int k3;
       const int zs3 = zbox(min(t - 3, zend + 2), k3);
