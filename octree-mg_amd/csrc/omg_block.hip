@@ -56,11 +56,14 @@ constexpr int kB3Ahead = 4;
 // is used, tools/b3p_variants.py "rhsall" sets it true for the A/B)
 constexpr bool kB3HaloRhs = false;
 static_assert(kB3Ahead % 2 == 0, "coarse planes are loaded on the even planes' steps");
-// the correction form: the coarse tile of a plane, cx in [-3, kB3TX*8+2] and
-// cy in [-3, 10] around the column's coarse cells (the fine tile's parents
-// and their x / y taps), in a ring of four coarse planes
+// the correction form: the coarse tile of a plane, cx in [-2, kB3TX*8+1] and
+// cy in [-2, 9] around the column's coarse cells: the parents and x / y taps
+// of the fine cells the pass uses (within 3 cells of the boxes; the pairs'
+// outer cells at 4 read a neighbouring tile entry instead, unused), in a
+// ring of four coarse planes
 static_assert(kB3TX == 2, "a column spans one coarse box in x");
-constexpr int B3CX = kB3TX * B3H + 6, B3CY = B3H + 6, B3CT = B3CX * B3CY;
+constexpr int B3CO = 2;                                  // tile offset of cx, cy = 0
+constexpr int B3CX = kB3TX * B3H + 2 * B3CO, B3CY = B3H + 2 * B3CO, B3CT = B3CX * B3CY;
 
 // ghost slot of face nb (1..6) at tangential (a, c) (omg_device.h off_gh)
 __device__ __forceinline__ int b3_gh(int nb, int a, int c) {
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   const double* __restrict__ cold = C.data + 2 * C.vstride;
   const double* __restrict__ cres_in = C.data + 3 * C.vstride;
   const int ct = tid < B3CT ? tid : B3CT - 1;
-  const int cxr = ct % B3CX - 3, cyy = cyo + ct / B3CX - 3;
+  const int cxr = ct % B3CX - B3CO, cyy = cyo + ct / B3CX - B3CO;
   const int xsc = cxr < 0 ? 0 : (cxr < B3NC ? 1 : 2), ysc = cyy < 0 ? 0 : (cyy < B3NC ? 1 : 2);
   const int icc = cxr - B3NC * (xsc - 1) + 1, jcc = cyy - B3NC * (ysc - 1) + 1;
   const unsigned cxy = 8u * (((icc - 1) >> 1) + B3H * (jcc - 1));
@@ -280,7 +283,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     auto cflush = [&](int t) {
       if (t < 0 || t >= zend) return;
       const int cs = t >> 1, q = l + 64 * (t & 1), cxq = q & 15, cyq = q >> 4;
-      const double v = rc[cs & 3][(cxq + 3) + B3CX * (cyq + 3)];
+      const double v = rc[cs & 3][(cxq + B3CO) + B3CX * (cyq + B3CO)];
       const int ic = cxq + 1, jc = cyo + cyq + 1, zsc = (cs >> 4) + 1, kc = (cs & 15) + 1;
       const unsigned* cb = cbo + 9 * zsc;
       const unsigned o = 8u * (((ic + jc + kc) & 1) * B3HV + ((ic - 1) >> 1) + B3H * (jc - 1) + B3FH * (kc - 1));
@@ -361,7 +364,9 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   double oa = 0.0, ob = 0.0, ea = 0.0, eb = 0.0, wa = 0.0, wb = 0.0;
   double re1 = 0.0, re2 = 0.0, re3 = 0.0, ro1 = 0.0, ro2 = 0.0;
   // PRO: this thread's coarse cell (the parent of its pair) in the tile
-  const int ci = act ? (p + 1) + B3CX * ((y >> 1) + 3) : B3CX + 1;
+  // (p - 2 is the pair's cx; the outer cells of pairs 0 and B3NPX-1 tap one
+  // entry past the tile's edge, in the ring's bounds: their values are unused)
+  const int ci = act ? (p - 2 + B3CO) + B3CX * ((y >> 1) + B3CO) : B3CX + 1;
   // cl (PRO): an even plane's step, which takes coarse plane t/2+1 to the
   // ring and loads plane (t+kB3Ahead)/2+1
   auto step = [&](int t, double& q, double& fe, double& fo, double& he, double& ho, double& ca, double& cb,

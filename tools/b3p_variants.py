@@ -10,6 +10,8 @@ VARIANTS = {
     # the plain pass at 6 waves per SIMD (3 workgroups per CU; 79 VGPRs, 20 B
     # of scratch), the other forms unchanged
     "occ6": [("__global__ void __launch_bounds__(B3BS) k_gsrb3", "__global__ void __launch_bounds__(B3BS, (PRO == 0 && !RES) ? 6 : 1) k_gsrb3")],
+    # the coarse tile with a 3-cell rim (22 x 14), as before r05/s47
+    "ct22": [("constexpr int B3CO = 2; ", "constexpr int B3CO = 3; ")],
     # every thread loads its own cells' rhs, as before r05/s46
     "rhsall": [("constexpr bool kB3HaloRhs = false;", "constexpr bool kB3HaloRhs = true;")],
     # the periodic rhs pass writes back only the pairs whose bits change
