@@ -32,12 +32,12 @@ roofline: the red-black smoother kernel on the finest level, algorithmic 12 B
 per level cell per substep (24 B per cell update), timed with
 HIP events on the library's stream in a separate profiled cycle, against
 8 TB/s HBM3E; traffic from the committed rocprofv3 PMC summary.  On C3's
-periodic finest level the kernel is k_gsrb3 (three substeps per pass,
-omg_block.hip; the down-smoothing's pass, one per cycle, the up-smoothing's
-being its correct_children form): the same rule over its 1.5 cell updates per
-level cell, and
+periodic finest level the kernel is k_gsrb3 in its correct_children form
+(omg_block.hip: the up-smoothing's correction + three substeps per pass, one
+per cycle, the level's longest kernel; the down-smoothing is one k_gsrb4 pass
+of four substeps): the same rule over its 1.5 cell updates per level cell, and
 beside it the pass's own minimum HBM bytes (phi of one colour and rhs in,
-phi and the ghost faces out: 20 B per cell + 12 KiB per box).
+phi and the ghost faces out, the coarse res in: 21 B per cell + 12 KiB per box).
 cpu_baseline: the reference itself (oracle/_ref, amdflang -O2 + MPICH) on the
 host cores of this box at P = 1, 8 and the job's CPU share (rank 0, N = 1).
 """
@@ -68,7 +68,7 @@ METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
 # also reports what these do not account for
-KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gsrb3p", "smoother_gsrb3r", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
+KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gsrb3p", "smoother_gsrb3r", "smoother_gsrb4", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
                    "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
 COMM_FAMILIES = ("comm", "comm_overlap")
@@ -81,7 +81,7 @@ def pmc_traffic(per_gpu_cells, block3=False):
     k_gsrb3 (one workgroup per column of 2 x 16 boxes on C3's level 1; its
     loads are 8 B per lane, for which the guide's x2 is uncalibrated)."""
     import glob
-    name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1, 0, false>") if block3 else \
+    name, pat = ("pmc_block3.json", r"void omg::k_gsrb3<1, 2, false>") if block3 else \
         ("pmc_smoother.json", r"void omg::k_gsrb_tile<16, 1[,>]")
     # (k_gsrb3: the finest level's launch is the one with the most workgroups,
     # one per column of boxes, whatever the column length)
@@ -261,7 +261,9 @@ def profile_cycle(omg, mg, timer, cycle):
     kern["unaccounted_ms"] = round(tp * 1e3 - total - comm.get("comm", {}).get("ms", 0.0), 4)
     # the finest level's red-black smoother: k_gsrb3 where it runs (three
     # substeps per pass), else the one-substep kernel
-    smoother = mg.ctx.kernel_stats(f"smoother_gsrb3@{hi}")
+    # (C3: the up-smoothing's k_gsrb3 pass in its correct_children form, the
+    # level's longest kernel; the down-smoothing's is k_gsrb4, four substeps)
+    smoother = mg.ctx.kernel_stats(f"smoother_gsrb3p@{hi}")
     smoother = (True,) + tuple(smoother) if smoother[0] else (False,) + tuple(mg.ctx.kernel_stats(f"smoother_gsrb@{hi}"))
     return kern, comm, smoother
 
@@ -276,7 +278,8 @@ def roofline(smoother, per_gpu_cells, boxes_hi, hi):
     traffic, tsrc = pmc_traffic(per_gpu_cells, block3)
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-           "kernel": (f"k_gsrb3<OP_LPL, 0, false> (three red-black substeps per pass, the down-smoothing's) "
+           "kernel": (f"k_gsrb3<OP_LPL, 2, false> (the up-smoothing's correction + three red-black substeps "
+                      f"per pass) "
                       f"on level {hi} ({boxes_hi} boxes)"
                       if block3 else f"k_gsrb_tile<16,OP_LPL> on level {hi} ({boxes_hi} boxes)"),
            "launches": n, "avg_launch_us": dur * 1e6,
@@ -286,7 +289,9 @@ def roofline(smoother, per_gpu_cells, boxes_hi, hi):
            "traffic_source": tsrc}
     if block3:
         cells = upd / n / 1.5
-        own = 20.0 * cells + 6 * BOX * BOX * 8 * boxes_hi
+        # phi of one colour and rhs in, phi out, the ghost faces, the coarse
+        # res read for the correction (1 B per fine cell)
+        own = 21.0 * cells + 6 * BOX * BOX * 8 * boxes_hi
         out["pass_min_bytes_per_launch"] = own
         out["pass_min_frac"] = own / dur / 1e9 / HBM_PEAK_GBS
     return out

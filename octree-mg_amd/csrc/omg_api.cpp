@@ -713,8 +713,10 @@ double allreduce(omg_ctx* c, double v, bool is_max);
 // reads this level's res = phi - old: the last three substeps run as one
 // k_gsrb3 pass that also stores it (the plain substeps first); returns whether
 // that pass ran.
+// four: runs of four substeps as one k_gsrb4 pass (the down-smoothing when
+// the residual + restriction run unfused after it, OMG_BLOCK4)
 bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0,
-                  bool want_res = false) {
+                  bool want_res = false, bool four = false) {
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps - skip_last;
   bool res_done = false;
@@ -807,6 +809,16 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // substeps n, n+1, n+2 in one pass (k_gsrb3) into phi's other buffer: it
     // reads the neighbours' cells in their boxes, which equal its ghosts only
     // when they are consistent (phi_gc_ok), and writes every ghost face
+    if (four && (n_sub - n + 1) % 4 == 0 && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
+      double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
+      {
+        Prof p(c, "smoother_gsrb4", 2.0 * L->n * L->nc * L->nc * L->nc, lvl);
+        launch_gsrb4(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
+      }
+      L->d_phi = other;
+      n += 3;
+      continue;
+    }
     if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3 &&
         !(want_res && (n_sub - n + 1) % 3 != 0)) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
@@ -1686,8 +1698,14 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   const bool tail_crhs = tail && max_lvl > top && tail_crhs_ok(c, top);
   for (int l = max_lvl; l >= min_lvl + 1; l--) {
     if (tail && l <= top) break;
-    const bool fused = smooth_resid_ok(c, l);
-    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0);
+    // four substeps per pass, then the unfused residual (k_resid_restrict):
+    // C3 4.06 -> 3.97 ms against k_gsrb3 + k_smooth_resid (level 1 775 + 592
+    // us; level 0 even, profiles/r05/s50_block4_ab.txt); OMG_NO_BLOCK4: the latter
+    const bool four = c->block4 && !c->no_block3 && c->smoother == OMG_SMOOTHER_GSRB && gsrb3_op_ok(c->op) &&
+                      level_ptr(c, l) && level_ptr(c, l)->d_b3 && level_ptr(c, l)->phi_gc_ok &&
+                      (c->n_cycle_down * c->n_substeps) % 4 == 0;
+    const bool fused = !four && smooth_resid_ok(c, l);
+    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0, false, four);
     update_coarse(c, l, fused, tail_crhs && l == top + 1);
   }
   if (tail) {
@@ -2910,6 +2928,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_block3 = env_flag("OMG_NO_BLOCK3");
     c->no_block3p = env_flag("OMG_NO_BLOCK3P");
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
+    c->block4 = !env_flag("OMG_NO_BLOCK4");
     // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
     if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
     // (tests: the column length, 2 .. 16 boxes, even; OMG_BLOCK3_COLUMN)

@@ -463,6 +463,194 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   }
 }
 
+// Four red-black substeps (colours e, 1-e, e, 1-e) in one pass (k_gsrb4): the
+// plain form of k_gsrb3 with a fourth stage at plane t-4 and a 4-row y halo
+// (rows -4 .. 19; the x tile already reaches 4 cells), for the down-smoothing
+// of a level whose residual + restriction then runs as k_resid_restrict (the
+// alternative to k_gsrb3 + k_smooth_resid, the default; OMG_NO_BLOCK4).  Every
+// ghost face of both colours is pushed.
+constexpr int B4NY = B3NC + 8, B4NT = B3NPX * B4NY, B4NW = (B4NT + 63) / 64, B4BS = 64 * (B4NW + 1);
+constexpr int B4PL = B3LP * (B4NY + 2);
+
+template <int OP>
+__global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict__ dst,
+                                               const int* __restrict__ cols, double lambda, int e,
+                                               const double* __restrict__ shift) {
+  __shared__ double pl[2][4][B4PL];
+  __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
+  __shared__ unsigned bo[kB3Rec];
+  __shared__ int len_s;
+  const int tid = threadIdx.x;
+  const int cq = xcd_box(blockIdx.x, gridDim.x);
+  for (int q = tid; q < kB3Rec; q += B4BS) {
+    const int v = cols[(long long)cq * kB3Rec + q];
+    if (q == 0) len_s = v;
+    else bo[q - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+  }
+  for (int q = tid; q < 2 * 4 * B4PL; q += B4BS) (&pl[0][0][0])[q] = 0.0;
+  __syncthreads();
+  const int len = len_s, zend = B3NC * len;
+  constexpr unsigned PB = 8u * B3H * B3NC;
+  auto zbox = [&](int t, int& k) {
+    const int zs = t < 0 ? 0 : (t >= zend ? len + 1 : (t >> 4) + 1);
+    k = t - B3NC * (zs - 1) + 1;
+    return zs;
+  };
+
+  if (tid >= B4NW * 64) {
+    // ---- the store wave: plane t-5 (written to fin by iteration t-1) ------
+    const int l = tid - B4NW * 64;
+    double* __restrict__ dse = dst + e * B3HV;
+    double* __restrict__ dso = dst + (1 - e) * B3HV;
+    auto flush = [&](int t) {
+      const int z = t - 5;
+      if (z < 0 || z >= zend) return;
+      int k;
+      const int r0 = kB3S * zbox(z, k);
+      const auto* F = fin[z & 1];
+      auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
+#pragma unroll
+      for (int r = 0; r < B3NC * B3CP / 64; r++) {
+        const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
+        const int xs = 1 + pc / B3H, ih = pc % B3H, j = jr + 1;
+        const unsigned o = bo[r0 + xs + B3XS] + 8u * (ih + B3H * (j - 1)) + PB * (k - 1);
+        const double ve = F[q][0], vo = F[q][1];
+        b3_st(dse, o, ve);
+        b3_st(dso, o, vo);
+        if (k == 1 || k == B3NC) {
+          const bool lf = leftv(jr);
+          const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
+          const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
+          b3_st(dst, g + 8u * b3_gh(nb, il, j), lf ? ve : vo);
+          b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), lf ? vo : ve);
+        }
+      }
+      {
+        const int jr = l >> 2, w = l & 3, j = jr + 1;
+        const int pc = w == 0 ? 0 : (w == 1 ? B3H - 1 : (w == 2 ? B3H : 2 * B3H - 1));
+        const int xs = 1 + pc / B3H;
+        const bool lf = leftv(jr), wantl = (w & 1) == 0;
+        const double v = fin[z & 1][jr * B3CP + pc][(wantl == lf) ? 0 : 1];
+        const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
+        b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+      }
+      {
+        const int jr = l < 32 ? 0 : B3NC - 1, x = l & 31;
+        const int pc = x >> 1, xs = 1 + pc / B3H, i = x - B3NC * (xs - 1) + 1;
+        const bool lf = leftv(jr), isl = (x & 1) == 0;
+        const double v = fin[z & 1][jr * B3CP + pc][(isl == lf) ? 0 : 1];
+        const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
+        b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+      }
+    };
+    for (int t = -4 - kB3Ahead; t <= zend + 4; t += kB3Ahead) {
+#pragma unroll
+      for (int u = 0; u < kB3Ahead; u++) {
+        flush(t + u);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  // ---- the compute waves ---------------------------------------------------
+  const bool act = tid < B4NT;
+  const int p = tid % B3NPX, y = tid / B3NPX - 4;
+  const int x0 = 2 * p - 4;
+  const int xs = x0 < 0 ? 0 : (x0 < kB3TX * B3NC ? 1 + x0 / B3NC : kB3TX + 1);
+  const int ys = y < 0 ? 0 : (y < B3NC ? 1 : 2);
+  const int ih = (x0 - B3NC * (xs - 1)) >> 1, j = y - B3NC * (ys - 1) + 1;
+  const int slot = xs + B3XS * ys;
+  const unsigned xyb = 8u * (ih + B3H * (j - 1));
+  const int li = act ? (p + 1) + B3LP * (y + 5) : B3LP + 1;
+  const bool ctr = act && xs >= 1 && xs <= kB3TX && ys == 1;
+  const int fi = ctr ? (j - 1) * B3CP + (xs - 1) * B3H + ih : 0;
+  const double m = shift ? *shift : 0.0;
+  const OpCoef<OP> K(L, lambda);
+  const double* __restrict__ src = L.phi + (1 - e) * B3HV;
+  const double* __restrict__ rhe = L.data + L.vstride + e * B3HV;
+  const double* __restrict__ rho = L.data + L.vstride + (1 - e) * B3HV;
+  // rhs where a substep's result is used: colour e (substeps 1, 3) within 3
+  // cells of the boxes, colour 1-e (substeps 2, 4) within 2
+  const bool nde = act && y >= -3 && y <= B3NC + 2;
+  const bool ndo = act && p >= 1 && p <= B3NPX - 2 && y >= -2 && y <= B3NC + 1;
+  const int sle = nde ? slot : 1 + B3XS, slo = ndo ? slot : 1 + B3XS;
+  const unsigned xye = nde ? xyb : 0u, xyo = ndo ? xyb : 0u;
+  auto load = [&](int t, double& q, double& fe, double& fo) {
+    int k;
+    const int zs = zbox(min(t, zend + 3), k);
+    const unsigned po = PB * (k - 1);
+    q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    fe = b3_ld(rhe, bo[kB3S * zs + sle] + xye + po);
+    fo = b3_ld(rho, bo[kB3S * zs + slo] + xyo + po);
+  };
+  // V0 stage 0 (planes t-2, t-1), V1 stage 1 (t-3, t-2), V2 stage 2 (t-4,
+  // t-3), V3 stage 3 (t-5, t-4); rhs colour e at t-1 .. t-3, 1-e at t-1 .. t-4
+  double oa = 0.0, ob = 0.0, ea = 0.0, eb = 0.0, wa = 0.0, wb = 0.0, xa = 0.0, xb = 0.0;
+  double re1 = 0.0, re2 = 0.0, re3 = 0.0, ro1 = 0.0, ro2 = 0.0, ro3 = 0.0, ro4 = 0.0;
+  auto step = [&](int t, double& q, double& fe, double& fo) {
+    const double ot = shift ? b3_take(q) - m : b3_take(q);
+    const double ret = b3_take(fe), rot = b3_take(fo);
+    load(t + kB3Ahead, q, fe, fo);
+    const double* P0 = pl[t & 1][0];
+    const double* P1 = pl[t & 1][1];
+    const double* P2 = pl[t & 1][2];
+    const double* P3 = pl[t & 1][3];
+    const int far = ((y + t) & 1) == e ? li - 1 : li + 1;
+    Nbr7 n;
+    n.c = 0.0;
+    n.xm = P0[far]; n.xp = ob;
+    n.ym = P0[li - B3LP]; n.yp = P0[li + B3LP]; n.zm = oa; n.zp = ot;
+    const double s1 = gs_value<OP>(K, n, re1);
+    n.xm = P1[far]; n.xp = eb;
+    n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
+    const double s2 = gs_value<OP>(K, n, ro2);
+    n.xm = P2[far]; n.xp = wb;
+    n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
+    const double s3 = gs_value<OP>(K, n, re3);
+    n.xm = P3[far]; n.xp = xb;
+    n.ym = P3[li - B3LP]; n.yp = P3[li + B3LP]; n.zm = xa; n.zp = s3;
+    const double s4 = gs_value<OP>(K, n, ro4);
+    // plane t-4 is final (colour e = stage 3 of the last iteration, 1-e = s4)
+    if (ctr) {
+      double* F = fin[(t - 4) & 1][fi];
+      F[0] = xb;
+      F[1] = s4;
+    }
+    if (act) {
+      double* W = pl[(t + 1) & 1][0];
+      W[li] = ot;
+      W[B4PL + li] = s1;
+      W[2 * B4PL + li] = s2;
+      W[3 * B4PL + li] = s3;
+    }
+    __syncthreads();
+    oa = ob; ob = ot;
+    ea = eb; eb = s1;
+    wa = wb; wb = s2;
+    xa = xb; xb = s3;
+    re3 = re2; re2 = re1; re1 = ret;
+    ro4 = ro3; ro3 = ro2; ro2 = ro1; ro1 = rot;
+  };
+  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead];
+#pragma unroll
+  for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = 0.0;
+  for (int t = -4 - kB3Ahead; t <= zend + 4; t += kB3Ahead) {
+#pragma unroll
+    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u]);
+  }
+}
+
+void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
+                  const double* shift, hipStream_t st) {
+  if (n_cols <= 0) return;
+  if (L.nc != B3NC) throw std::runtime_error("launch_gsrb4: box size must be 16");
+  if (op == OP_HELM)
+    k_gsrb4<OP_HELM><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+  else
+    k_gsrb4<OP_LPL><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+}
+
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
 
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,

@@ -57,6 +57,11 @@ constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
 constexpr int kB3MaxZ = 16;                      // boxes per column in z (at most)
 constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
 bool gsrb3_op_ok(int op);
+// four substeps (colours e, 1-e, e, 1-e) per pass, same columns (k_gsrb4,
+// omg_block.hip): the down-smoothing of a level whose residual + restriction
+// then runs unfused (the default; OMG_NO_BLOCK4)
+void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
+                  const double* shift, hipStream_t st);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
 // halves are left stale: only for a pass that k_smooth_resid follows, which
 // reads colour e's and forms colour 1-e's itself)

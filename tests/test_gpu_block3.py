@@ -103,3 +103,20 @@ def test_block3_switch_off_same_bits(monkeypatch, switch):
     for _ in range(2):
         assert dev.vcycle(True) == ref.vcycle(True) == orc.vcycle(True)
         _assert_same(dev, ref)
+
+
+# The down-smoothing's four substeps as one k_gsrb4 pass, then the unfused
+# residual + restriction (k_resid_restrict; the default where the substep count
+# is a multiple of 4), and with OMG_NO_BLOCK4 k_gsrb3 + k_smooth_resid: every
+# variable bitwise
+@pytest.mark.parametrize("switch", [None, "OMG_NO_BLOCK4"])
+@pytest.mark.parametrize("down,up", [(2, 2), (4, 1)])
+@pytest.mark.parametrize("args", ["16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0",
+                                  "16 128 128 128 3 v gsrb helm 2 per sol 1 lb 0"])
+def test_block4_vcycles_match_oracle(monkeypatch, args, down, up, switch):
+    if switch:
+        monkeypatch.setenv(switch, "1")
+    dev, orc = _pair(args, down, up)
+    for _ in range(3):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc)
