@@ -40,6 +40,12 @@ beside it the pass's own minimum HBM bytes (phi of one colour and rhs in,
 phi and the ghost faces out, the coarse res in: 21 B per cell + 12 KiB per box).
 cpu_baseline: the reference itself (oracle/_ref, amdflang -O2 + MPICH) on the
 host cores of this box at P = 1, 8 and the job's CPU share (rank 0, N = 1).
+parity: before anything is timed, the N ranks run C3 itself (512^3 in total,
+the strong tree, with the timed run's coarse replication) for the 3 V-cycles
+the reference ran at the same rank count (tests/golden/golden.json
+c3_per512_box16, runs 1/2/4/8) and compare the printed history (max |phi - u|,
+max |res| over the leaves, reduced over ranks) bit for bit; a mismatch prints
+the line with "parity": {"ok": false} and no value, and exits 3.
 """
 from __future__ import annotations
 
@@ -86,6 +92,57 @@ PASSES = {
     "smoother_gsrb3": ("k_gsrb3<OP_LPL, 0, false> (three red-black substeps per pass)", 1.5,
                        r"void omg::k_gsrb3<1, 0, false>", 20.0),
 }
+
+
+PARITY_CONFIG = "c3_per512_box16"
+PARITY_EXIT = 3
+
+
+def parity_verdict(history, golden_history):
+    """Bitwise comparison of a run's history with the reference's: ok, and the
+    first differing iteration (or None)."""
+    first = next((i for i, (a, b) in enumerate(zip(history, golden_history)) if a != b), None)
+    if first is None and len(history) != len(golden_history):
+        first = min(len(history), len(golden_history))
+    return {"ok": first is None, "first_mismatch": first}
+
+
+def c3_parity(dist, world):
+    """C3 (512^3 in total over the N ranks, the strong tree) for the reference's
+    3 V-cycles on this rank's GPU, its history against the reference's own run
+    at N MPI ranks (golden c3_per512_box16).  The history is omg_golden's
+    print_state (tests/mgdriver.py measure: max |phi - u| and max |res| over the
+    leaves, each reduced by max over ranks, m_multigrid.f90:150-243's cycle in
+    between).  No golden at this N: ok None."""
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["configs"][PARITY_CONFIG]
+    run = golden["runs"].get(str(world))
+    if run is None:
+        return {"ok": None, "config": PARITY_CONFIG, "reason": f"no reference run at {world} ranks"}
+    from tests import mgdriver as D   # the golden driver's problem set-up and print_state (device backend)
+    import torch
+
+    def reduce(e, r):
+        if not dist:
+            return e, r
+        t = torch.tensor([e, r], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]), float(t[1])
+
+    t0 = time.time()
+    cfg = D.parse(golden["args"])
+    be = D.DeviceBackend(cfg, None, REPLICATE_CELLS)
+    D.setup_problem(be)
+    hist = D._cycles(be, cfg, reduce)
+    be.mg.ctx.call("synchronize")
+    omg_pkg = __graft_entry__.load_package()
+    omg_pkg.mg_deallocate_storage(be.mg)
+    if os.environ.get("OMG_BENCH_PARITY_CORRUPT"):   # (tests: the mismatch path)
+        hist[-1] = dict(hist[-1], res="%016X" % (int(hist[-1]["res"], 16) ^ 1))
+    out = parity_verdict(hist, run["history"])
+    out.update({"config": PARITY_CONFIG, "ranks": world, "vcycles": cfg["n_its"], "seconds": round(time.time() - t0, 1),
+                "checked": "history (max |phi-u|, max |res|, per V-cycle) bit for bit vs the reference's run at "
+                           f"{world} MPI ranks"})
+    return out
 
 
 def pmc_traffic(per_gpu_cells, block3_pat=None):
@@ -539,6 +596,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the c3_strong / c4_refined sub-benchmarks")
+    ap.add_argument("--no-parity", action="store_true", help="skip the C3 parity check before the timed runs")
     ap.add_argument("--plan-only", action="store_true",
                     help="CPU only: launch the ranks, build each rank's communication plan, check they pair up")
     a = ap.parse_args()
@@ -564,6 +622,15 @@ def main():
         # transport, octree-mg_amd/mg.py _use_host_transport)
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
 
+    parity = None if a.no_parity else c3_parity(dist, world)
+    if parity and parity["ok"] is False:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": world,
+                              "parity": parity, "error": "C3 history differs from the reference's"}), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        sys.exit(PARITY_EXIT)
     domain = domain_for(a.mode, world)
     main_run = run_c3(omg, domain, dist, rank, world, local_rank, a.steps, a.warmup,
                       profile=not a.no_profile_pass)
@@ -606,6 +673,7 @@ def main():
                        "parallelism": f"domain-decomposition x{world} (RCCL halos)"},
             "roofline": main_run.get("roofline"),
             "cpu_baseline": cpu,
+            "parity": parity,
             "comm": main_run["comm"],
             "ref_unknowns_per_us": main_run["ref_unknowns_per_us"],
             "kernels_one_cycle": main_run.get("kernels_one_cycle"),

@@ -702,11 +702,44 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   finish_halo(c, L, iv);
 }
 
+// Deep halo of a split level (plan_deep) around a k_gsrb3 / k_gsrb4 pass:
+// before it, the proxies get phi of the colour the pass reads (as stored: a
+// pending mean shift is subtracted by the pass from proxies and own boxes
+// alike) and, when the level's rhs changed since the last fill, rhs; after
+// it, the ghosts of this rank's faces toward other GPUs (nobody pushed them)
+// by the level's halo plan.  Both rounds are collective: the rhs refill is
+// decided by flags every rank changes alike (every rhs writer is a
+// collective call, include/omg.h), checked under OMG_CHECK_COLLECTIVE.
+double allreduce(omg_ctx* c, double v, bool is_max);
+void deep_before(omg_ctx* c, Level* L, int colour) {
+  if (!L->deep) return;
+  const LevelView V = L->view();
+  if (c->check_collective && (allreduce(c, L->prox_rhs_ok ? 1.0 : 0.0, true) > 0.5) != L->prox_rhs_ok)
+    throw OmgError("deep halo: the rhs refill decision differs across ranks (an rhs write was not collective)");
+  if (!L->prox_rhs_ok) {
+    Prof p(c, "deep_rhs", (double)L->deep_rhs.n_recv * 64, L->lvl);
+    launch_deep_copy(V, 2, 0, 64, L->deep_rhs.d_send_items, L->deep_rhs.n_send, L->d_sendbuf, false, c->stream);
+    exchange(c, L->deep_rhs, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+    launch_deep_copy(V, 2, 0, 64, L->deep_rhs.d_recv_items, L->deep_rhs.n_recv, L->d_recvbuf, true, c->stream);
+    L->prox_rhs_ok = true;
+  }
+  Prof p(c, "deep_phi", (double)L->deep_phi.n_recv * 32, L->lvl);
+  launch_deep_copy(V, 1, colour, 32, L->deep_phi.d_send_items, L->deep_phi.n_send, L->d_sendbuf, false, c->stream);
+  exchange(c, L->deep_phi, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+  launch_deep_copy(V, 1, colour, 32, L->deep_phi.d_recv_items, L->deep_phi.n_recv, L->d_recvbuf, true, c->stream);
+}
+void deep_after(omg_ctx* c, Level* L) {
+  if (!L->deep) return;
+  Prof p(c, "deep_faces", (double)L->halo.n_recv * L->nc * L->nc, L->lvl);
+  launch_face_pack(L->view(), L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, c->stream);
+  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+  launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+}
+
 void materialize_level(omg_ctx* c, Level* L);
 void drop_rhs_lex(omg_ctx* c);
 void phi_mean_ready(omg_ctx* c);
 double* red_mean(omg_ctx* c, int ch);
-double allreduce(omg_ctx* c, double v, bool is_max);
 
 // smooth_boxes (m_multigrid.f90:404-424)
 // want_res: the level above takes k_gsrb3's correct_children form next, which
@@ -811,11 +844,13 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // when they are consistent (phi_gc_ok), and writes every ghost face
     if (four && (n_sub - n + 1) % 4 == 0 && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
+      deep_before(c, L, 1 - e);
       {
         Prof p(c, "smoother_gsrb4", 2.0 * L->n * L->nc * L->nc * L->nc, lvl);
         launch_gsrb4(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
       }
       L->d_phi = other;
+      deep_after(c, L);
       n += 3;
       continue;
     }
@@ -825,8 +860,10 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       // the down-smoothing's last pass before k_smooth_resid (skip_last: it
       // runs the next substep, colour 0, and forms colour 0's ghosts itself
       // from colour 1, reading colour 1's only): push colour e = 1 alone
-      const bool push1 = !(skip_last == 1 && n + 2 == n_sub && e == 1);
+      // (a split level: both colours, its remote faces' ghosts arrive whole)
+      const bool push1 = L->deep || !(skip_last == 1 && n + 2 == n_sub && e == 1);
       const bool res = want_res && n + 2 == n_sub && push1;
+      deep_before(c, L, 1 - e);
       {
         Prof p(c, res ? "smoother_gsrb3r" : "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
         launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, push1, nullptr,
@@ -834,6 +871,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       }
       res_done = res;
       L->d_phi = other;
+      deep_after(c, L);
       n += 2;
       continue;
     }
@@ -1006,7 +1044,7 @@ bool smooth_resid_ok(omg_ctx* c, int lvl) {
 void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = false) {
   Level* F = level_ptr(c, lvl);
   if (Level* Cl = level_ptr(c, lvl - 1)) {
-    Cl->rhs_lex_ok = false;   // its rhs is rewritten below
+    Cl->rhs_lex_ok = Cl->prox_rhs_ok = false;   // its rhs is rewritten below
     // restriction overwrites every box of an all-parents level (interior), and
     // the fill below every ghost face: a pending shift there is dead
     if (Cl->all_parents) Cl->shift_pending = false;
@@ -1393,7 +1431,7 @@ void materialize_phi(omg_ctx* c) {
 }
 // the ring-order rhs copies: every write of a level's rhs drops its copy
 void drop_rhs_lex(omg_ctx* c) {
-  for (auto& kv : c->levels) kv.second.rhs_lex_ok = false;
+  for (auto& kv : c->levels) kv.second.rhs_lex_ok = kv.second.prox_rhs_ok = false;
 }
 // ring-order rhs buffers for the levels the register-ring lexicographic
 // kernel serves (allocated outside any graph capture: tree setup, smoother
@@ -1465,6 +1503,11 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       leaf_sum_device(c, 2, kChRhs);
     }
     c->rhs_cache_valid = false;
+    // (split levels: proxies whose rhs was the owners' take the same
+    // subtraction, bit for bit the owners' rhs - mean, and stay valid)
+    std::vector<int> prox_kept;
+    for (auto& kv : c->levels)
+      if (kv.second.prox_rhs_ok) prox_kept.push_back(kv.first);
     drop_rhs_lex(c);
     mean_device(c, kChRhs);
     bool all_fused = true;
@@ -1472,6 +1515,14 @@ void subtract_mean(omg_ctx* c, int iv, int ghosts, int mode = kPlain) {
       Level* L = level_ptr(c, l);
       if (!L || !L->n) continue;
       if (mode == kInCycle && L->all_parents) continue;
+      if (L->n_prox && std::count(prox_kept.begin(), prox_kept.end(), l)) {
+        LevelView P = L->view();   // the proxies as boxes 0 .. n_prox-1
+        P.data += (long long)L->n * L->stride;
+        P.phi += (long long)L->n * L->stride;
+        P.n = L->n_prox;
+        launch_subtract(P, 2, red_mean(c, kChRhs), 0, c->stream);
+        L->prox_rhs_ok = true;
+      }
       Prof p(c, "subtract_rhs", (double)L->n * L->nc * L->nc * L->nc, l);
       if (l >= 1 && (int)L->leaves.size() == L->n && subtract_sums_nc(L->nc))
         launch_subtract_sums(L->sweep_view(), 2, L->d_leaves, L->n, red_mean(c, kChRhs), L->d_scratch_rhs, c->stream);
@@ -1585,7 +1636,7 @@ void run_tail(omg_ctx* c, int top, bool top_crhs) {
       if (L->all_parents && l < top) L->shift_pending = false;   // overwritten by the restriction
       else materialize_level(c, L);
     }
-    L->rhs_lex_ok = false;   // the tail writes the rhs of the levels below its top
+    L->rhs_lex_ok = L->prox_rhs_ok = false;   // the tail writes the rhs of the levels below its top
     TailLevel& T = A.lv[l - c->lowest];
     T.L = L->view();
     T.bc = bc_for(c, l, 1);
@@ -1826,8 +1877,11 @@ bool graph_ok(omg_ctx* c) {
 // matches anything), the graph of this key is dropped, and every level's phi
 // ghost faces count as stale (the next cycle fills them).  (The graph path
 // runs without subtract_mean, so no mean / shift state is involved.)
-void graph_rollback(omg_ctx* c, int key) {
+void graph_rollback(omg_ctx* c, int key, const std::map<int, double*>& phi_at_start) {
   c->capturing = false;
+  // the multi-substep passes swap a level's phi buffer on the host as they are
+  // recorded: a graph that never ran leaves phi where it was
+  for (auto& kv : phi_at_start) c->levels[kv.first].d_phi = kv.second;
   c->max_deferred = false;
   std::memset(c->h_tail, 0xff, sizeof(TailArgs));
   auto it = c->graphs.find(key);
@@ -1845,6 +1899,8 @@ void graph_rollback(omg_ctx* c, int key) {
 template <typename F>
 double run_cycle(omg_ctx* c, int key, F&& body) {
   if (!graph_ok(c)) return body();
+  std::map<int, double*> phi_at_start;
+  for (auto& kv : c->levels) phi_at_start[kv.first] = kv.second.d_phi;
   c->capturing = true;
   c->max_deferred = false;
   HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
@@ -1858,7 +1914,7 @@ double run_cycle(omg_ctx* c, int key, F&& body) {
   } catch (...) {
     (void)hipStreamEndCapture(c->stream, &g);
     if (g) (void)hipGraphDestroy(g);
-    graph_rollback(c, key);
+    graph_rollback(c, key, phi_at_start);
     throw;
   }
   c->capturing = false;
@@ -1886,7 +1942,7 @@ double run_cycle(omg_ctx* c, int key, F&& body) {
     }
   } catch (...) {
     if (g) (void)hipGraphDestroy(g);
-    graph_rollback(c, key);
+    graph_rollback(c, key, phi_at_start);
     throw;
   }
   HIPCHK(hipGraphDestroy(g));
@@ -2344,7 +2400,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_phi_buf); dfree(L.d_b3); dfree(L.d_b3c); L.n_b3 = 0; L.h_b3.clear();
     dfree(L.d_physbox);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0); dfree(L.d_bndface);
-    for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl}) {
+    for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl, &L.deep_phi, &L.deep_rhs}) {
       dfree(T->d_send_items);
       dfree(T->d_recv_items);
     }
@@ -2361,6 +2417,11 @@ void free_levels(omg_ctx* c) {
   }
 }
 
+// whether k_gsrb3's 32-bit byte offsets reach every box of a variable
+bool block3_addressable(long long n_boxes, long long stride) {
+  return (unsigned long long)n_boxes * (unsigned long long)stride * 8ull <= 0xFFFFFFFFull;
+}
+
 // k_gsrb3's columns (launch_gsrb3): a level of at least kB3MinBoxes boxes of
 // 16^3 whose faces are all same-GPU boxes of the level (a periodic uniform
 // level on one GPU) is tiled by columns of kB3TX boxes in x and up to kB3MaxZ
@@ -2369,7 +2430,10 @@ void free_levels(omg_ctx* c) {
 // each XCD's run of workgroups (xcd_box) is one compact patch whose halo
 // columns its own L2 holds.  Any face or tiling that does not fit: no records.
 void build_block3(omg_ctx* c, Level& L) {
-  if (g_host_only || c->host_only || L.nc != 16 || L.n < c->b3_min_boxes || L.replicated) return;
+  if (g_host_only || c->host_only || L.nc != 16 || L.n < c->b3_min_boxes || L.replicated || L.deep) return;
+  // k_gsrb3 / k_gsrb4 address a variable with 32-bit byte offsets
+  // (omg_block.hip b3_ld / b3_st): 95,325 boxes of 16^3 at most
+  if (!block3_addressable(L.n + L.n_prox, L.stride)) return;
   for (int8_t k : L.h_nbk)
     if (k != NB_LOCAL) return;
   const int n = L.n;
@@ -2441,7 +2505,8 @@ void build_block3(omg_ctx* c, Level& L) {
 // coarse level of 16^3 boxes whose faces are all same-GPU boxes.
 void build_block3c(omg_ctx* c, Level& F, const Level& C) {
   (void)c;
-  if (!F.d_b3 || F.h_b3.empty() || C.nc != 16 || C.replicated || C.n == 0 || F.n != 8 * C.n) return;
+  if (!F.d_b3 || F.h_b3.empty() || C.nc != 16 || C.replicated || C.n == 0 || F.n != 8 * C.n || F.deep || C.deep) return;
+  if (!block3_addressable(C.n + C.n_prox, C.stride)) return;
   for (int8_t k : C.h_nbk)
     if (k != NB_LOCAL) return;
   for (int b = 0; b < F.n; b++)
@@ -2489,6 +2554,214 @@ void build_block3c(omg_ctx* c, Level& F, const Level& C) {
   for (int b = 0; b < C.n; b++)
     if (own[b] != 2) return;
   F.d_b3c = to_device(out);
+}
+
+// ---------------------------------------------------------------------------
+// Deep halo: k_gsrb3 / k_gsrb4 on a level split over GPUs.
+// The reference fills the ghost layer after every substep
+// (m_multigrid.f90:404-424, mg_fill_ghost_cells_lvl, m_ghost_cells.f90:131-175,
+// whose remote part is one sort_and_transfer_buffers round,
+// m_communication.f90:37-66).  A multi-substep pass instead reads the
+// neighbours' cells up to 4 deep, so on a split level the remote boxes its
+// columns read become proxy boxes of this rank (after its own boxes, in every
+// variable), filled once per pass: phi of the colour the pass reads, rhs when
+// it changed.  The pass then runs exactly as on one GPU; its store wave's
+// pushes into proxies are dropped, and the remote faces' ghosts of this rank's
+// boxes arrive by the level's halo plan after it.
+//
+// What travels: a proxy B is read by the columns of this rank's boxes A in
+// its 26-neighbourhood; per dimension, B lies below A (its top 4 layers are
+// read), above (its bottom 4) or level with A (all 16): a product of ranges,
+// whose union over those A is sent as 4^3-cell bricks (launch_deep_copy).  Every rank derives the same regions from the global
+// tree, so the brick lists pair up key for key (key 64*id + brick).
+//
+// Where: 16^3 levels whose every box is a leaf (rhs then changes only by the
+// periodic mean, which the proxies follow, not by update_coarse every cycle),
+// every face a box of the level (uniform, periodic or interior), x pairs of
+// boxes (even ix and its x+ neighbour) on one rank, at least b3_min_boxes
+// boxes on every rank holding some, and byte offsets of every rank's boxes
+// + proxies under 4 GiB; decided alike on every rank.
+// the box at offset o (components -1..1) from id, walking x, y, z in turn
+// (zyx: the reverse order); 0 when the walk leaves the level's boxes
+int deep_walk(const Tree& T, int id, const int o[3], bool zyx = false) {
+  for (int s = 0; s < 3; s++) {
+    const int d = zyx ? 2 - s : s;
+    if (!o[d]) continue;
+    id = T.nbr(id, 2 * d + (o[d] > 0 ? 2 : 1));
+    if (id <= 0) return 0;
+  }
+  return id;
+}
+
+template <typename F>
+void deep_offsets(F&& f) {
+  for (int z = -1; z <= 1; z++)
+    for (int y = -1; y <= 1; y++)
+      for (int x = -1; x <= 1; x++)
+        if (x || y || z) {
+          const int o[3] = {x, y, z};
+          f(o);
+        }
+}
+
+// the bricks box B shows a box A at offset o from B (A reads B's 4 layers
+// toward it, all 16 across): bit bx + 4 by + 16 bz
+unsigned long long deep_bricks(const int o[3]) {
+  unsigned long long m = 0;
+  for (int bz = 0; bz < 4; bz++)
+    for (int by = 0; by < 4; by++)
+      for (int bx = 0; bx < 4; bx++) {
+        const int b[3] = {bx, by, bz};
+        bool in = true;
+        for (int d = 0; d < 3; d++) in &= o[d] == 0 || b[d] == (o[d] > 0 ? 3 : 0);
+        if (in) m |= 1ull << (bx + 4 * by + 16 * bz);
+      }
+  return m;
+}
+
+// (before the level's arena is allocated: sets n_prox, which sizes it)
+void plan_deep(omg_ctx* c, Level& L) {
+  const int l = L.lvl, me = c->rank;
+  L.deep = false;
+  L.n_prox = 0;
+  L.prox_ids.clear();
+  if (c->n_ranks == 1 || L.replicated || L.nc != 16 || c->no_block3 || c->no_deep) return;
+  Tree T{c};
+  const auto& ids = c->ids[l];
+  if (ids.empty() || c->leaves[l].size() != ids.size()) return;
+  std::map<int, std::vector<int>> by_rank;
+  bool split = false;
+  for (int id : ids) {
+    by_rank[T.rank(id)].push_back(id);
+    for (int nb = 1; nb <= 6; nb++) {
+      const int nid = T.nbr(id, nb);
+      if (nid <= 0 || T.lvl(nid) != l) return;   // physical or refinement-boundary face
+      split |= T.rank(nid) != T.rank(id);
+    }
+  }
+  if (!split) return;
+  auto ixd = [&](int id, int d) { return c->ix[(size_t)(id - 1) * 3 + d] - 1; };
+  for (int id : ids) {
+    const int odd = ixd(id, 0) & 1, pr = T.nbr(id, odd ? 1 : 2);
+    if (T.rank(pr) != T.rank(id) || T.nbr(pr, odd ? 2 : 1) != id || (ixd(pr, 0) & 1) == odd) return;
+    bool grid = true;
+    deep_offsets([&](const int* o) { grid &= deep_walk(T, id, o) == deep_walk(T, id, o, true); });
+    if (!grid) return;
+  }
+  // every rank: enough boxes, and its boxes + proxies addressable by k_gsrb3's
+  // 32-bit byte offsets
+  std::vector<int> stamp((size_t)c->n_boxes + 1, -1);
+  const unsigned long long box_bytes = 8ull * (unsigned long long)(((stored_cells(16) + 63) / 64) * 64);
+  for (auto& kv : by_rank) {
+    if ((int)kv.second.size() < c->b3_min_boxes) return;
+    long long np = 0;
+    for (int id : kv.second)
+      deep_offsets([&](const int* o) {
+        const int b = deep_walk(T, id, o);
+        if (T.rank(b) != kv.first && stamp[b] != kv.first) {
+          stamp[b] = kv.first;
+          np++;
+        }
+      });
+    if ((unsigned long long)(kv.second.size() + np) * box_bytes > 0xFFFFFFFFull) return;
+  }
+  L.deep = true;
+  // proxies (this rank reads them) and what the peers read of this rank's boxes
+  // (box B at offset o from my box A: A reads B's bricks at -o from B; and
+  // the peer's box B reads my A's bricks at o from A)
+  std::map<int, unsigned long long> need;
+  std::map<std::pair<int, int>, unsigned long long> give;
+  for (int id : L.ids) {
+    if (T.rank(id) != me) continue;
+    deep_offsets([&](const int* o) {
+      const int b = deep_walk(T, id, o), q = T.rank(b);
+      if (q == me) return;
+      const int mo[3] = {-o[0], -o[1], -o[2]};
+      need[b] |= deep_bricks(mo);
+      give[{q, id}] |= deep_bricks(o);
+    });
+  }
+  std::map<int, int> pidx;
+  for (auto& kv : need) {
+    pidx[kv.first] = L.n + (int)L.prox_ids.size();
+    L.prox_ids.push_back(kv.first);
+  }
+  L.n_prox = (int)L.prox_ids.size();
+  std::vector<Rec> rs, rr;
+  for (auto& kv : need)
+    for (int br = 0; br < 64; br++)
+      if ((kv.second >> br) & 1) rr.push_back({T.rank(kv.first), 64LL * kv.first + br, pidx[kv.first], br});
+  for (auto& kv : give)
+    for (int br = 0; br < 64; br++)
+      if ((kv.second >> br) & 1)
+        rs.push_back({kv.first.first, 64LL * kv.first.second + br, c->local_index[kv.first.second], br});
+  for (Transfer* X : {&L.deep_phi, &L.deep_rhs}) {
+    X->send = group(rs, 2);
+    X->recv = group(rr, 2);
+    X->send_ints = X->recv_ints = 2;
+    X->item_doubles = X == &L.deep_phi ? 32 : 64;
+    finalize_transfer(*X);
+  }
+  L.prox_rhs_ok = false;
+  // the columns (build_block3's, over global ids: a column's boxes are this
+  // rank's, the boxes around it this rank's or proxies)
+  auto mine = [&](int id) { return id > 0 && T.rank(id) == me; };
+  auto slot = [&](int id) {
+    if (mine(id)) return c->local_index[id];
+    auto it = pidx.find(id);
+    if (it == pidx.end()) throw OmgError("plan_deep: a column reads a box outside the proxies");
+    return it->second;
+  };
+  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 16 : 4);
+  std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
+  std::vector<int> covered(L.n, 0);
+  auto spread = [](unsigned v) {
+    unsigned long long r = 0;
+    for (int q = 0; q < 20; q++) r |= (unsigned long long)((v >> q) & 1u) << (2 * q);
+    return r;
+  };
+  for (int h : L.ids) {
+    if (!mine(h) || ixd(h, 0) % kB3TX || !(ixd(h, 2) % nzb == 0 || !mine(T.nbr(h, 5)))) continue;
+    std::vector<int> zc{h};
+    while ((int)zc.size() < nzb) {
+      const int up = T.nbr(zc.back(), 6);
+      if (!mine(up) || ixd(up, 2) % nzb == 0) break;
+      zc.push_back(up);
+    }
+    const int len = (int)zc.size();
+    std::vector<int> r(kB3Rec, 0);
+    r[0] = len;
+    for (int zs = 0; zs <= len + 1; zs++) {
+      const int cb = zs == 0 ? T.nbr(zc[0], 5) : (zs == len + 1 ? T.nbr(zc[len - 1], 6) : zc[zs - 1]);
+      int g[3][kB3TX + 2];
+      g[1][0] = T.nbr(cb, 1);
+      for (int xs = 1; xs <= kB3TX + 1; xs++) g[1][xs] = xs == 1 ? cb : T.nbr(g[1][xs - 1], 2);
+      for (int xs = 0; xs < kB3TX + 2; xs++) {
+        g[0][xs] = T.nbr(g[1][xs], 3);
+        g[2][xs] = T.nbr(g[1][xs], 4);
+      }
+      for (int ys = 0; ys < 3; ys++)
+        for (int xs = 0; xs < kB3TX + 2; xs++) {
+          if (zs >= 1 && zs <= len && ys == 1 && xs >= 1 && xs <= kB3TX) {
+            if (!mine(g[ys][xs])) throw OmgError("plan_deep: a column box on another rank");
+            covered[c->local_index[g[ys][xs]]]++;
+          }
+          r[1 + kB3S * zs + (kB3TX + 2) * ys + xs] = slot(g[ys][xs]);
+        }
+    }
+    const unsigned long long key = ((unsigned long long)(ixd(h, 2) / nzb) << 40) |
+                                   (spread((unsigned)(ixd(h, 0) / kB3TX)) | (spread((unsigned)ixd(h, 1)) << 1));
+    cols.emplace_back(key, std::move(r));
+  }
+  for (int b = 0; b < L.n; b++)
+    if (covered[b] != 1) throw OmgError("plan_deep: the columns do not cover the level once");
+  std::sort(cols.begin(), cols.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<int> flat;
+  flat.reserve(cols.size() * kB3Rec);
+  for (auto& cr : cols) flat.insert(flat.end(), cr.second.begin(), cr.second.end());
+  L.n_b3 = (int)cols.size();
+  L.d_b3 = to_device(flat);
+  L.h_b3 = std::move(flat);
 }
 
 void build_plan(omg_ctx* c) {
@@ -2546,11 +2819,15 @@ void build_plan(omg_ctx* c) {
   for (int l = c->lowest; l <= c->highest; l++) {
     Level& L = c->levels[l];
     const int nc = L.nc;
+    // deep halo on a split level (k_gsrb3 / k_gsrb4 there): the proxies
+    // extend every variable of the arena
+    plan_deep(c, L);
     // arena
     if (L.n) {
-      const size_t bytes = sizeof(double) * (size_t)c->n_vars * L.n * L.stride;
+      const size_t bytes = sizeof(double) * (size_t)c->n_vars * (L.n + L.n_prox) * L.stride;
       dmalloc(&L.d_data, bytes, true);
       L.d_phi = L.d_data;
+      if (L.deep && L.n_b3) dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)(L.n + L.n_prox) * L.stride, true);
       if (c->debug && !g_host_only) {   // (L.view() needs only the arena fields here)
         launch_poison_ghosts(L.view(), c->n_vars, snan_value(), nullptr);
         HIPCHK(hipDeviceSynchronize());
@@ -2822,6 +3099,8 @@ void build_plan(omg_ctx* c) {
       upd(recvn, l, (size_t)L.halo.n_recv * L.halo.item_doubles);
       upd(sendn, l, (size_t)L.repl.n_send * L.repl.item_doubles);
       upd(recvn, l, (size_t)L.repl.n_recv * L.repl.item_doubles);
+      upd(sendn, l, (size_t)L.deep_rhs.n_send * L.deep_rhs.item_doubles);
+      upd(recvn, l, (size_t)L.deep_rhs.n_recv * L.deep_rhs.item_doubles);
       if (l > c->lowest) {
         upd(sendn, l, (size_t)L.restr.n_send * L.restr.item_doubles);      // fine side packs
         upd(recvn, l - 1, (size_t)L.restr.n_recv * L.restr.item_doubles);  // coarse side receives
@@ -2892,12 +3171,23 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw OmgError("bad rank / n_ranks");
     if (n_ranks > 1 && !unique_id && device != OMG_DEVICE_NONE)
       throw OmgError("unique_id required for n_ranks > 1");
+    // the switches the communication plan depends on (read by plan-only
+    // contexts too, whose plans the CPU tests pair up)
+    auto plan_switches = [](omg_ctx* c) {
+      c->no_block3 = env_flag("OMG_NO_BLOCK3");
+      c->no_deep = env_flag("OMG_NO_DEEP");
+      // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
+      if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
+      // (tests: the column length, 2 .. 16 boxes, even; OMG_BLOCK3_COLUMN)
+      if (const char* v = getenv("OMG_BLOCK3_COLUMN")) c->b3_col = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
+    };
     if (device == OMG_DEVICE_NONE) {   // plan-only context: no HIP, no RCCL
       omg_ctx* c = new omg_ctx();
       c->device = device;
       c->rank = rank;
       c->n_ranks = n_ranks;
       c->host_only = true;
+      plan_switches(c);
       *out = c;
       return;
     }
@@ -2925,14 +3215,10 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_gs_plane = env_flag("OMG_NO_GS_PLANE");
     c->no_fill_xl = env_flag("OMG_NO_FILL_XL");
     c->no_gs_dbl = env_flag("OMG_NO_GS_DBL");
-    c->no_block3 = env_flag("OMG_NO_BLOCK3");
+    plan_switches(c);
     c->no_block3p = env_flag("OMG_NO_BLOCK3P");
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     c->block4 = !env_flag("OMG_NO_BLOCK4");
-    // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
-    if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
-    // (tests: the column length, 2 .. 16 boxes, even; OMG_BLOCK3_COLUMN)
-    if (const char* v = getenv("OMG_BLOCK3_COLUMN")) c->b3_col = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");
@@ -3100,8 +3386,8 @@ int omg_plan_transfer(omg_ctx* c, int lvl, int which, int dir, int cap, int* pee
   return guarded([&] {
     Level* L = level_ptr(c, lvl);
     if (!L) throw OmgError("no such level");
-    if (which < 0 || which > 4) throw OmgError("omg_plan_transfer: bad transfer");
-    const Transfer* T[5] = {&L->halo, &L->restr, &L->prol, &L->rbx, &L->repl};
+    if (which < 0 || which > 5) throw OmgError("omg_plan_transfer: bad transfer");
+    const Transfer* T[6] = {&L->halo, &L->restr, &L->prol, &L->rbx, &L->repl, &L->deep_phi};
     const auto& lists = dir ? T[which]->recv : T[which]->send;
     int n = 0;
     for (auto& p : lists)

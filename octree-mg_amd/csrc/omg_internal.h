@@ -50,7 +50,7 @@ struct LevelView {
   double* data;          // [n_vars][n][stride]
   double* phi;           // phi (= var 1 of data)
   long long stride;      // doubles per box and variable
-  long long vstride;     // doubles per variable = n * stride
+  long long vstride;     // doubles per variable = (n + proxies) * stride
   int n;                 // local boxes
   int nc;                // box size (cells per dim)
   int h, hf;             // ceil(nc/2): cells of one colour per row / per face row
@@ -195,6 +195,18 @@ struct Level {
   // (launch_gsrb3's ccols); null: the level's up-smoothing starts with
   // k_prolong_smooth
   int* d_b3c = nullptr;
+  // Deep halo (k_gsrb3 / k_gsrb4 on a level split over GPUs, plan_deep in
+  // omg_api.cpp): the remote boxes the columns read are proxy boxes
+  // n .. n+n_prox-1 of every variable (vstride covers them); before a pass the
+  // cells the columns read travel as 4^3-cell bricks, phi of the colour the
+  // pass reads (deep, 32 doubles per brick) and rhs when it changed since
+  // (deep_rhs, 64: both colours); after it the remote faces' ghosts by the
+  // halo plan.  Decided alike on every rank from the global tree.
+  bool deep = false;
+  int n_prox = 0;
+  std::vector<int> prox_ids;     // global ids of the proxies, ascending
+  Transfer deep_phi, deep_rhs;   // items: (box or n + proxy, brick)
+  bool prox_rhs_ok = false;      // the proxies' rhs equals the owners' rhs
   int* d_physbox = nullptr;          // boxes with a physical face (k_phys_gc after such a chain)
   int n_physbox = 0;
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
@@ -221,7 +233,7 @@ struct Level {
     v.data = d_data;
     v.phi = d_phi;
     v.stride = stride;
-    v.vstride = stride * n;
+    v.vstride = stride * (n + n_prox);
     v.n = n;
     v.nc = nc;
     v.h = v.hf = (nc + 1) / 2;
@@ -331,6 +343,7 @@ struct omg_ctx {
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
+  bool no_deep = false;                // OMG_NO_DEEP: split levels keep one substep per launch (no deep halo)
   bool no_block3p = false;             // OMG_NO_BLOCK3P: correct_children by k_prolong_smooth, not k_gsrb3
   bool block4 = true;                  // the down-smoothing as k_gsrb4 + the unfused residual (OMG_NO_BLOCK4: off)
   bool no_block3r = false;             // OMG_NO_BLOCK3R: no res from the coarse level's last pass (k_gsrb3 forms phi - old)

@@ -53,6 +53,61 @@ __global__ void __launch_bounds__(256) k_unpack_faces(LevelView L, int iv, const
   }
 }
 
+// Deep halo of a level split over GPUs (k_gsrb3 / k_gsrb4 on split levels,
+// omg_api.cpp plan_deep): a remote box that some column here reads is held
+// as a proxy box after this rank's boxes in every variable, and the cells the
+// columns read (4 layers toward this rank's boxes, whole across) travel as
+// 4 x 4 x 4 bricks, brick = bx + 4 by + 16 bz.  per = 32: one colour c of
+// the brick; 64: both colours.  A brick row of 4 cells is two consecutive
+// slots of each colour (omg_device.h off_int), so a brick of one colour is 16
+// slot pairs: slot 2 bx + w of row (4 by + jj, 4 bz + kk).  items: (box, brick)
+// pairs, box = a local box (pack) or n + proxy (unpack); the same order on
+// both sides (sort_and_transfer_buffers' keys, m_communication.f90:37-66).
+__global__ void __launch_bounds__(256) k_deep_copy(LevelView L, int iv, int c, int per, const int* items,
+                                                   int n_items, double* buf, int unpack) {
+  GRID_STRIDE(t, (long long)n_items * per) {
+    const int q = (int)(t / per);
+    int r = (int)(t % per);
+    const int cc = per == 64 ? r >> 5 : c;
+    r &= 31;
+    const int b = items[2 * q], br = items[2 * q + 1];
+    const int w = r & 1, jj = (r >> 1) & 3, kk = r >> 3;
+    const int bx = br & 3, by = (br >> 2) & 3, bz = br >> 4;
+    double* p = boxp(L, iv, b) + cc * L.hv + 2 * bx + w + L.h * ((4 * by + jj) + L.nc * (4 * bz + kk));
+    if (unpack)
+      *p = buf[t];
+    else
+      buf[t] = *p;
+  }
+}
+
+void launch_deep_copy(const LevelView& L, int iv, int c, int per, const int* items, int n, double* buf, bool unpack,
+                      hipStream_t st) {
+  if (L.nc != 16 || (per != 32 && per != 64)) throw std::runtime_error("launch_deep_copy: 16^3 boxes, 32 or 64");
+  const long long work = (long long)n * per;
+  if (work == 0) return;
+  k_deep_copy<<<grid_for(work), 256, 0, st>>>(L, iv, c, per, items, n, buf, unpack ? 1 : 0);
+}
+
+// the boundary layer of phi at the listed faces (items b*6+nb-1) into the
+// halo send buffer, nc*nc doubles per face in the order k_unpack_faces
+// writes the peer's ghosts: after a pass that does not pack (k_gsrb3 /
+// k_gsrb4 on split levels)
+__global__ void __launch_bounds__(256) k_face_pack(LevelView L, const int* items, int n_items, double* buf) {
+  const int nc = L.nc, nc2 = nc * nc;
+  GRID_STRIDE(t, (long long)n_items * nc2) {
+    const int q = (int)(t / nc2), cell = (int)(t % nc2);
+    const int f = items[q], b = f / 6, nb = f % 6 + 1;
+    buf[t] = boxp(L, 1, b)[off_face_cell(L, nb, (nb & 1) ? 1 : nc, cell % nc + 1, cell / nc + 1)];
+  }
+}
+
+void launch_face_pack(const LevelView& L, const int* items, int n, double* buf, hipStream_t st) {
+  const long long work = (long long)n * L.nc * L.nc;
+  if (work == 0) return;
+  k_face_pack<<<grid_for(work), 256, 0, st>>>(L, items, n, buf);
+}
+
 // buffer_for_fine_nb (m_ghost_cells.f90:385-422) on the coarse rank: the
 // coarse face next to a fine neighbour on another rank, interpolated by
 // box_gc_for_fine_neighbor (:500-577).  Item = (coarse box, coarse-side nb,

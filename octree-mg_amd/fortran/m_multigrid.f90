@@ -401,19 +401,67 @@ contains
     end subroutine put_list
   end subroutine tree_key
 
-  !> Whether the device context was built for this tree (tree_key).
+  !> Whether the device context was built for this tree (tree_key), compared
+  !> in place against the stored key: no key is built (about 20 ints per box,
+  !> 25 MB at 262k boxes, on every call in resident mode, ADVICE r05), and the
+  !> first difference ends the walk.
   logical function same_tree(mg)
-    type(mg_t), intent(in)      :: mg
-    integer(c_int), allocatable :: key(:)
-    real(c_double), allocatable :: dr(:)
+    type(mg_t), intent(in) :: mg
+    integer                :: n, nlev, n_lists, lvl, t, o, id, p
     same_tree = .false.
     if (.not. c_associated(ctx) .or. .not. allocated(ctx_key)) return
-    call tree_key(mg, key, dr)
-    if (size(key) /= size(ctx_key)) return
-    if (any(key /= ctx_key)) return
+    n = mg%n_boxes
+    nlev = mg%highest_lvl - mg%lowest_lvl + 1
+    if (size(ctx_key) < key_head) return
+    n_lists = 0
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       n_lists = n_lists + size(mg%lvls(lvl)%ids) + size(mg%lvls(lvl)%leaves) + &
+            size(mg%lvls(lvl)%parents) + size(mg%lvls(lvl)%ref_bnds)
+    end do
+    if (size(ctx_key) /= key_head + 20*n + nlev + 4*nlev+1 + max(n_lists, 1)) return
+    if (any(ctx_key(1:key_head) /= [n, mg_num_vars + mg%n_extra_vars, mg%lowest_lvl, mg%highest_lvl, &
+         mg%first_normal_lvl, mg%box_size, mg%n_cpu, mg%my_rank, n_lists])) return
+    o = key_head
+    do id = 1, n
+       if (ctx_key(o + id) /= mg%boxes(id)%lvl .or. ctx_key(o + n + id) /= mg%boxes(id)%parent .or. &
+            ctx_key(o + 19*n + id) /= mg%boxes(id)%rank) return
+       if (any(ctx_key(o + 2*n + 8*(id-1) + 1 : o + 2*n + 8*id) /= mg%boxes(id)%children)) return
+       if (any(ctx_key(o + 10*n + 6*(id-1) + 1 : o + 10*n + 6*id) /= &
+            merge(mg_physical_boundary, mg%boxes(id)%neighbors, mg%boxes(id)%neighbors < mg_no_box))) return
+       if (any(ctx_key(o + 16*n + 3*(id-1) + 1 : o + 16*n + 3*id) /= mg%boxes(id)%ix)) return
+    end do
+    o = o + 20*n
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       if (ctx_key(o + lvl - mg%lowest_lvl + 1) /= mg%box_size_lvl(lvl)) return
+    end do
+    o = o + nlev
+    p = o + 4*nlev+1
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       t = lvl - mg%lowest_lvl
+       if (.not. same_list(mg%lvls(lvl)%ids, 4*t+2)) return
+       if (.not. same_list(mg%lvls(lvl)%leaves, 4*t+3)) return
+       if (.not. same_list(mg%lvls(lvl)%parents, 4*t+4)) return
+       if (.not. same_list(mg%lvls(lvl)%ref_bnds, 4*t+5)) return
+    end do
     ! the level spacings, compared bit for bit
-    same_tree = all(transfer(dr, 0_c_int64_t, size(dr)) == &
-         transfer(ctx_key_dr, 0_c_int64_t, size(ctx_key_dr)))
+    do lvl = mg%lowest_lvl, mg%highest_lvl
+       t = lvl - mg%lowest_lvl
+       if (any(transfer(mg%dr(:, lvl), 0_c_int64_t, NDIM) /= &
+            transfer(ctx_key_dr(NDIM*t+1 : NDIM*t+NDIM), 0_c_int64_t, NDIM))) return
+    end do
+    same_tree = .true.
+
+  contains
+
+    logical function same_list(ids, slot)
+      integer, intent(in) :: ids(:)
+      integer, intent(in) :: slot
+      integer             :: m
+      m = size(ids)
+      same_list = ctx_key(o + slot) == ctx_key(o + slot - 1) + m
+      if (same_list .and. m > 0) same_list = all(ctx_key(p + 1 : p + m) == ids)
+      p = p + m
+    end function same_list
   end function same_tree
 
   !> Build (or rebuild) the device context for the current tree.
@@ -651,17 +699,22 @@ contains
   !> transport (sort_and_transfer_buffers, m_communication.f90:37-66;
   !> mpi_allreduce, m_multigrid.f90:232,255), when ranks share a GPU (RCCL
   !> refuses two ranks on one device) or when OMG_TRANSPORT=host is set.
-  !> Decided alike on every rank.
+  !> Decided alike on every rank.  The GPUs a rank sees are its node's, so
+  !> they are compared with the ranks on the same node (MPI_COMM_TYPE_SHARED),
+  !> not with mg%n_cpu: 2 nodes x 8 GPUs run 16 ranks on RCCL.
   logical function use_host_transport(mg)
     type(mg_t), intent(in) :: mg
     integer(c_int)         :: nd
-    integer                :: mine, lowest, ierr, ln, st
+    integer                :: mine, lowest, ierr, ln, st, node_comm, n_node
     character(len=16)      :: env
     call get_environment_variable("OMG_TRANSPORT", env, ln, st)
     mine = 0
     if (st == 0 .and. trim(env) == "host") mine = 1
     call omg_ok(omg_device_count(nd), "device_count")
-    if (nd < mg%n_cpu) mine = 1
+    call mpi_comm_split_type(mg%comm, MPI_COMM_TYPE_SHARED, mg%my_rank, MPI_INFO_NULL, node_comm, ierr)
+    call mpi_comm_size(node_comm, n_node, ierr)
+    call mpi_comm_free(node_comm, ierr)
+    if (nd < n_node) mine = 1
     call mpi_allreduce(mine, lowest, 1, MPI_INTEGER, MPI_MAX, mg%comm, ierr)
     use_host_transport = lowest == 1
   end function use_host_transport

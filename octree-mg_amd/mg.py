@@ -311,11 +311,14 @@ def mg_allocate_storage(mg: MG, device_index=None):
 
 
 def _use_host_transport(mg: MG) -> bool:
-    """The host transport when the ranks outnumber the visible GPUs or
-    OMG_TRANSPORT=host; agreed over the group (as the Fortran drop-in does)."""
+    """The host transport when this node's ranks outnumber its visible GPUs
+    or OMG_TRANSPORT=host; agreed over the group (as the Fortran drop-in
+    does).  The node's ranks: LOCAL_WORLD_SIZE (torchrun, bench.py's own
+    launcher), else every rank of the group (one node)."""
     import torch
     import torch.distributed as dist
-    want = os.environ.get("OMG_TRANSPORT") == "host" or device.device_count() < mg.n_cpu
+    n_node = int(os.environ.get("LOCAL_WORLD_SIZE", mg.n_cpu))
+    want = os.environ.get("OMG_TRANSPORT") == "host" or device.device_count() < n_node
     t = torch.tensor([1 if want else 0], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=mg.comm)
     return bool(t[0])

@@ -519,24 +519,33 @@ def run_loopback(args: str, n_ranks: int, body, n_its=None, timeout=600, rep_cel
     return out
 
 
-def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0):
+def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_cells=0, stats=(), cycles=None):
     """The same configuration on n_ranks device contexts of this process,
     exchanging through the loopback transport (run_loopback): the multi-rank
     path of libomg.so (plans, packing, MPICH-order reductions) on a single
     GPU.  Returns the history with err / res reduced by max over ranks, as
     omg_golden's MPI_Reduce(MAX), and the sha256 of the final phi of every box
     gathered from its owner, in the order phi_digest uses for a one-rank run
-    (ids per level, lowest first)."""
+    (ids per level, lowest first).  stats: kernel-family names (omg_kernel_stats)
+    whose launch counts every rank returns under "stats" (the cycles then run
+    with profiling on); cycles = (n_cycle_down, n_cycle_up) other than the
+    reference's 2, 2."""
     cfg = parse(args)
     if n_its is not None:
         cfg["n_its"] = n_its
 
     def body(be, rank, reduce):
+        if cycles:
+            be.mg.n_cycle_down, be.mg.n_cycle_up = cycles
+            be.mg._push_methods()
+        if stats:
+            be.mg.ctx.call("set_profiling", 1)
         hist = _cycles(be, cfg, reduce)
         be.mg.ctx.call("synchronize")
+        st = {name: be.mg.ctx.kernel_stats(name)[0] for name in stats}
         t = be.tree   # (copied: run_loopback frees the storage, which empties the level lists)
         order = [(lvl, [int(i) for i in t.lvls[lvl].ids]) for lvl in range(t.lowest_lvl, t.highest_lvl + 1)]
-        return hist, _owned_phi(be), (order, t.rank.copy())
+        return hist, _owned_phi(be), (order, t.rank.copy()), st
 
     res = run_loopback(args, n_ranks, body, n_its, timeout, rep_cells)
     out = [r[0] for r in res]
@@ -549,4 +558,4 @@ def run_problem_loopback(args: str, n_ranks: int, n_its=None, timeout=600, rep_c
             key = (lvl, id_)
             owner = int(owners[id_])
             h.update(phis[owner][key] if key in phis[owner] else phis[0][key])
-    return {"history": out[0], "phi_sha256": h.hexdigest()}
+    return {"history": out[0], "phi_sha256": h.hexdigest(), "stats": [r[3] for r in res]}

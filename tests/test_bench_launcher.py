@@ -14,12 +14,13 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(*args):
+def _run(*args, env_extra=None, rc=0):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
                        timeout=600, env=env, cwd=ROOT)
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == rc, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]   # rank 0 only
     return json.loads(lines[0])
@@ -87,6 +88,31 @@ def test_bench_two_ranks_on_one_gpu():
     share the GPU, so the library takes the host transport over the gloo
     group (RCCL refuses two ranks on one device); the line must report two
     GPUs, the host transport and the weak-scaling workload."""
-    out = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--mode", "weak256", "--no-cpu-baseline")
+    out = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--mode", "weak256", "--no-cpu-baseline",
+               "--no-extra")
     assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["value"] > 0
     assert out["comm"]["transport"] == "host", out["comm"]
+    # the self-check before the timed run: C3 at 2 ranks against the
+    # reference's own 2-rank history
+    assert out["parity"]["ok"] is True and out["parity"]["ranks"] == 2, out["parity"]
+
+
+@pytest.mark.gpu
+def test_bench_parity_mismatch_exits_nonzero():
+    """A history that differs from the reference's (one bit flipped by the
+    test hook OMG_BENCH_PARITY_CORRUPT) stops the bench before anything is
+    timed: exit 3, a line with parity false and no value."""
+    out = _run("--gpus", "2", "--mode", "weak256", "--no-cpu-baseline", "--no-extra",
+               env_extra={"OMG_BENCH_PARITY_CORRUPT": "1"}, rc=3)
+    assert out["parity"]["ok"] is False and out["parity"]["first_mismatch"] == 3 and out["value"] is None
+
+
+def test_parity_verdict():
+    sys.path.insert(0, ROOT)
+    import bench
+    h = [{"it": i, "err": "%016X" % i, "res": "0", "max_res": "0"} for i in range(4)]
+    assert bench.parity_verdict(h, [dict(x) for x in h]) == {"ok": True, "first_mismatch": None}
+    g = [dict(x) for x in h]
+    g[2]["res"] = "1"
+    assert bench.parity_verdict(h, g) == {"ok": False, "first_mismatch": 2}
+    assert bench.parity_verdict(h[:3], h) == {"ok": False, "first_mismatch": 3}

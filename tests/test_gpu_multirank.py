@@ -9,7 +9,8 @@ import os
 
 import pytest
 
-from tests.mgdriver import omg, run_loopback, run_problem, run_problem_loopback
+from tests.mgdriver import OPS, OracleBackend, _cycles, omg, parse, phi_digest, run_loopback, run_problem, \
+    run_problem_loopback, setup_problem
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"]
 MULTI = [(n, int(r)) for n, e in sorted(GOLDEN.items()) if not e.get("big") for r in e["runs"] if int(r) > 1]
@@ -134,3 +135,59 @@ def test_multirank_vcycle_makes_no_host_wait(args, ranks, monkeypatch):
         assert no_max == 0
         assert with_max == 1
         assert prio < 0   # the highest priority HIP offers (lower is higher)
+
+
+# Round 6: the multi-substep passes on levels split over ranks (the deep halo,
+# omg_api.cpp plan_deep): the remote boxes the columns read are proxies,
+# filled once per pass (phi of the colour read; rhs when it changed, the
+# periodic mean subtracted on them like on their owners), and the remote
+# faces' ghosts exchanged after it.  The 128^3 tree's 512-box finest level
+# takes it with the level bound lowered to one box; every rank must run the
+# k_gsrb4 / k_gsrb3 passes there and the deep rounds, and the history and
+# every box's final phi must be the reference's at the same rank count.  (C3
+# itself at 2/4/8 ranks, test_c3_512_multirank_matches_reference_golden, takes
+# it at the default bound: 16384 / 8192 / 4096 boxes per rank on level 1.)
+DEEP_STATS = ("smoother_gsrb4@1", "smoother_gsrb3@1", "deep_phi@1", "deep_rhs@1", "deep_faces@1")
+
+
+@pytest.mark.parametrize("name,ranks", [("per128_box16_gsrb_v", 2), ("per128_box16_gsrb_v", 8)])
+def test_deep_halo_multirank_matches_reference(name, ranks, monkeypatch):
+    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", "1")
+    e = GOLDEN[name]
+    out = run_problem_loopback(e["args"], ranks, stats=DEEP_STATS)
+    _check(out, e["runs"][str(ranks)])
+    n_it = parse(e["args"])["n_its"]
+    for st in out["stats"]:
+        # per cycle: the down pass (k_gsrb4), the up pass after k_prolong_smooth
+        # (k_gsrb3), one phi round each; rhs once (the proxies follow the mean)
+        assert st["smoother_gsrb4@1"] == n_it and st["smoother_gsrb3@1"] == n_it, st
+        assert st["deep_phi@1"] == 2 * n_it and st["deep_rhs@1"] == 1 and st["deep_faces@1"] == 2 * n_it, st
+
+
+# Against the oracle at the same rank count: other smoothing counts (the down
+# pass as k_gsrb3 + one-substep launches + the split fused last substep, the
+# up passes after k_prolong_smooth), Helmholtz, FMG (rhs rewritten below the
+# finest level every cycle), and OMG_NO_DEEP in the same process.
+@pytest.mark.parametrize("args,ranks,cycles", [
+    ("16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0", 4, (3, 1)),
+    ("16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0", 2, (1, 3)),
+    ("16 128 128 128 3 v gsrb helm 2 per sol 1 lb 0", 4, (2, 2)),
+    ("16 128 128 128 3 v gsrb helm 2 per sol 1 lb 0", 8, (4, 4)),
+    ("16 128 128 128 2 f gsrb lpl 0 per sol 1 lb 0", 2, (2, 2)),
+])
+@pytest.mark.parametrize("switch", [None, "OMG_NO_DEEP"])
+def test_deep_halo_multirank_matches_oracle(args, ranks, cycles, switch, monkeypatch):
+    monkeypatch.setenv("OMG_BLOCK3_MIN_BOXES", "1")
+    if switch:
+        monkeypatch.setenv(switch, "1")
+    out = run_problem_loopback(args, ranks, cycles=cycles, stats=DEEP_STATS)
+    cfg = parse(args)
+    orc = OracleBackend(cfg, ranks)
+    import pyoracle  # on sys.path once OracleBackend exists (checker only)
+    orc.o.configure(op=OPS[cfg["op"]], lam=cfg["lam"], smoother=pyoracle.GSRB, n_cycle_down=cycles[0],
+                    n_cycle_up=cycles[1], subtract_mean=True)
+    setup_problem(orc)
+    assert out["history"] == _cycles(orc, cfg)
+    assert out["phi_sha256"] == phi_digest(orc)
+    deep = sum(st["deep_phi@1"] for st in out["stats"])
+    assert (deep == 0) == (switch == "OMG_NO_DEEP"), out["stats"]

@@ -34,7 +34,7 @@ CASES = [
     ("8 64 64 64 1 v gsrb lpl 0 per sol 1 lb 0", 2, 4096),
     ("8 32 32 32 1 v gs lpl 0 sol sol 2 lb 0", 3, 1 << 40),  # + refinement boundaries
 ]
-WHICH = {0: "halo", 1: "restrict", 2: "prolong", 3: "refinement-boundary", 4: "replica"}
+WHICH = {0: "halo", 1: "restrict", 2: "prolong", 3: "refinement-boundary", 4: "replica", 5: "deep"}
 
 
 def _free_port():
@@ -88,8 +88,48 @@ def _expected_remote(args, rank, world, rep_lvl):
     return halo, rb
 
 
-def _worker(rank, world, port, args, rep, q):
+def _expected_deep(args, rank, world):
+    """The deep halo of the finest level from box coordinates alone: whether
+    the level takes it (16^3 leaves, every rank's x pairs of boxes on one rank,
+    split over ranks) and the bricks (64*id + brick) this rank's k_gsrb3 /
+    k_gsrb4 columns read of other ranks' boxes: a box B at periodic offset
+    (dx, dy, dz) in -1..1 from one of my boxes shows it its 4 layers toward
+    it (brick index 3 where B is below, 0 where above) and all 16 across."""
+    cfg = parse(args)
+    t = build_tree(cfg, T.MGTree(), world, rank)
+    lvl = t.highest_lvl
+    ids = [int(i) for i in t.lvls[lvl].ids]
+    ix = {i: [int(v) for v in t.ix[i]] for i in ids}
+    n = [max(ix[i][d] for i in ids) for d in range(3)]
+    own = {i: int(t.rank[i]) for i in ids}
+    at = {tuple(ix[i]): i for i in ids}
+    pairs_ok = all(own[i] == own[at[((ix[i][0] - 1) ^ 1) + 1, ix[i][1], ix[i][2]]] for i in ids)
+    split = len(set(own.values())) > 1
+    deep = cfg["box"] == 16 and cfg["n_levels"] == 1 and cfg["bc"] == "per" and pairs_ok and split
+    want = set()
+    for a in ids:
+        if own[a] != rank:
+            continue
+        for dz in (-1, 0, 1):
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    o = (dx, dy, dz)
+                    if o == (0, 0, 0):
+                        continue
+                    b = at[tuple((ix[a][d] - 1 + o[d]) % n[d] + 1 for d in range(3))]
+                    if own[b] == rank:
+                        continue
+                    for br in range(64):
+                        bb = (br & 3, (br >> 2) & 3, br >> 4)
+                        # B at offset o from A: A at -o from B reads the bricks toward it
+                        if all(o[d] == 0 or bb[d] == (0 if o[d] > 0 else 3) for d in range(3)):
+                            want.add(64 * b + br)
+    return lvl, deep, want
+
+
+def _worker(rank, world, port, args, rep, q, env=None):
     try:
+        os.environ.update(env or {})
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
         mine, rep_lvl = _plans(args, rank, world, rep)
@@ -134,6 +174,15 @@ def _worker(rank, world, port, args, rep, q):
                 problems.append(f"lvl {lvl}: halo receives {len(got_h)} faces, tree needs {len(halo[lvl])}")
             if sorted(got_r) != sorted(rb[lvl]):
                 problems.append(f"lvl {lvl}: rb receives {len(got_r)} faces, tree needs {len(rb[lvl])}")
+        if env:
+            lvl, deep, want = _expected_deep(args, rank, world)
+            got = [k for _, k in mine[(lvl, 5, 1)][0]]
+            if bool(got) != deep:
+                problems.append(f"lvl {lvl}: deep halo {'on' if got else 'off'}, expected {'on' if deep else 'off'}")
+            if deep and (sorted(got) != sorted(want) or len(set(got)) != len(got)):
+                problems.append(f"lvl {lvl}: deep halo receives {len(got)} bricks, the columns read {len(want)}")
+            if deep and mine[(lvl, 5, 1)][1] != 32:
+                problems.append(f"lvl {lvl}: deep item of {mine[(lvl, 5, 1)][1]} doubles")
         n_rb = sum(len(v) for v in rb.values())
         dist.barrier()
         dist.destroy_process_group()
@@ -142,12 +191,11 @@ def _worker(rank, world, port, args, rep, q):
         q.put((rank, [f"{type(e).__name__}: {e}"], 0))
 
 
-@pytest.mark.parametrize("args,world,rep", CASES)
-def test_plans_pair_up_across_ranks(args, world, rep):
+def _run(args, world, rep, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, args, rep, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, rep, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -155,5 +203,28 @@ def test_plans_pair_up_across_ranks(args, world, rep):
         p.join(60)
     problems = [f"rank {r}: {m}" for r, ms, _ in res for m in ms]
     assert not problems, "\n".join(problems)
+    return res
+
+
+@pytest.mark.parametrize("args,world,rep", CASES)
+def test_plans_pair_up_across_ranks(args, world, rep):
+    res = _run(args, world, rep)
     if world == 3 and " 2 lb" in args and not rep:
         assert sum(n for _, _, n in res) > 0, "case meant to cross refinement boundaries has none"
+
+
+# The deep halo of k_gsrb3 / k_gsrb4 on a split level (omg_api.cpp plan_deep),
+# with the pass's level bound lowered to one box (OMG_BLOCK3_MIN_BOXES): the
+# brick lists pair up key for key, every rank receives exactly the bricks its
+# columns read (from box coordinates, _expected_deep), and a level whose x
+# pairs of boxes straddle ranks (128^3 at 3 ranks: 171 boxes on the first)
+# is declined on every rank alike.
+DEEP = [("16 64 64 64 1 v gsrb lpl 0 per sol 1 lb 0", 2),
+        ("16 128 64 64 1 v gsrb lpl 0 per sol 1 lb 0", 4),
+        ("16 128 128 128 1 v gsrb lpl 0 per sol 1 lb 0", 3),
+        ("16 128 128 128 1 v gsrb helm 1 per sol 1 lb 0", 8)]
+
+
+@pytest.mark.parametrize("args,world", DEEP)
+def test_deep_halo_plans_pair_up(args, world):
+    _run(args, world, 0, {"OMG_BLOCK3_MIN_BOXES": "1"})

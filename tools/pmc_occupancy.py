@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per kernel and grid size, from the PMC passes of tools/r04_c4_pmc.sh:
+"""Per kernel and grid size, from the PMC passes of tools/archive/r04_c4_pmc.sh:
 waves, the GPU-busy clock (GRBM_GUI_ACTIVE, summed over the 8 XCDs),
 SQ_BUSY_CYCLES, the mean resident waves (SQ_WAVE_CYCLES, quad-cycles, x4
 / GRBM_GUI_ACTIVE per XCD), the share of wave time waiting (SQ_WAIT_ANY /

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction) and kernel-
 trace duration of the level-1 red-black substep (32768 workgroups, 512^3)
-for the builds of tools/r04_pmc_yz.sh: base, yz1 (no y/z ghost pushes), yz3
+for the builds of tools/archive/r04_pmc_yz.sh: base, yz1 (no y/z ghost pushes), yz3
 (no y/z pushes and no y/z ghost loads).  usage: pmc_yz_summary.py <dir>"""
 import csv
 import glob

@@ -1,0 +1,27 @@
+#!/bin/bash
+# round 6 GPU session: tag, then steps (smoke deep block3 c3multi loop bench suite), each
+# under its own limit; stops at the first crash / abort / time-out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r06
+tag=$1; shift
+O=gpurun_out/r06/${tag}
+PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for s in "$@"; do
+  echo "=== $s $(date +%T)"
+  case $s in
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1; rc=$? ;;
+    deep) timeout -k 10 900 $PT tests/test_gpu_multirank.py -k deep > ${O}_deep.log 2>&1; rc=$? ;;
+    block3) timeout -k 10 900 $PT tests/test_gpu_block3.py > ${O}_block3.log 2>&1; rc=$? ;;
+    c3multi) timeout -k 10 900 $PT tests/test_gpu_multirank.py -k c3_512 > ${O}_c3multi.log 2>&1; rc=$? ;;
+    loop) { timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && \
+            timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5; } > ${O}_loop.log 2>&1; rc=$? ;;
+    bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
+    suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
+    *) echo "unknown step $s"; rc=2 ;;
+  esac
+  echo "=== $s rc=$rc $(date +%T)"
+  tail -3 ${O}_${s}*.log 2>/dev/null
+  if [ $rc -ne 0 ]; then echo "stopping after $s (rc=$rc)"; exit $rc; fi
+done
+exit 0
