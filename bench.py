@@ -149,8 +149,9 @@ def pmc_traffic(per_gpu_cells, block3_pat=None):
     """HBM bytes per launch of the finest-level smoother from the newest
     committed PMC summary (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2
     + WRITE_SIZE, the MI355X guide's gfx950 correction), or None.  block3:
-    k_gsrb3 (one workgroup per column of 2 x 16 boxes on C3's level 1; its
-    loads are 8 B per lane, for which the guide's x2 is uncalibrated)."""
+    k_gsrb3 / k_gsrb4 (one workgroup per column of 2 x 16 boxes on C3's level
+    1; their loads are 8 B per lane, for which the x2 holds exactly as for the
+    guide's 16-B loads: profiles/r06/fetch_calib.txt)."""
     import glob
     block3 = block3_pat is not None
     name, pat = ("pmc_block3.json", block3_pat) if block3 else \

@@ -728,12 +728,28 @@ void deep_before(omg_ctx* c, Level* L, int colour) {
   exchange(c, L->deep_phi, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
   launch_deep_copy(V, 1, colour, 32, L->deep_phi.d_recv_items, L->deep_phi.n_recv, L->d_recvbuf, true, c->stream);
 }
-void deep_after(omg_ctx* c, Level* L) {
+// defer: on the comm stream, joined by the caller (faces_pending: only the
+// boxes with a face on another GPU wait for it, update_coarse's residual)
+void deep_after(omg_ctx* c, Level* L, bool defer = false) {
   if (!L->deep) return;
-  Prof p(c, "deep_faces", (double)L->halo.n_recv * L->nc * L->nc, L->lvl);
-  launch_face_pack(L->view(), L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, c->stream);
-  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
-  launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+  hipStream_t st = c->stream;
+  if (defer && L->n_bnd && L->n_int) {
+    HIPCHK(hipEventRecord(c->ev_bnd, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->stream_comm, c->ev_bnd, 0));
+    st = c->stream_comm;
+    L->faces_pending = true;
+  }
+  Prof p(c, "deep_faces", (double)L->halo.n_recv * L->nc * L->nc, L->lvl, st);
+  launch_face_pack(L->view(), L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, st);
+  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, st, L->lvl);
+  launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, st);
+  if (L->faces_pending) HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
+}
+// the deferred faces of deep_after have arrived (the main stream waits)
+void faces_join(omg_ctx* c, Level* L) {
+  if (!L || !L->faces_pending) return;
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+  L->faces_pending = false;
 }
 
 void materialize_level(omg_ctx* c, Level* L);
@@ -748,8 +764,10 @@ double* red_mean(omg_ctx* c, int ch);
 // that pass ran.
 // four: runs of four substeps as one k_gsrb4 pass (the down-smoothing when
 // the residual + restriction run unfused after it, OMG_BLOCK4)
+// defer_faces: a k_gsrb4 pass that ends the smoothing leaves its remote faces'
+// exchange in flight on the comm stream (deep_after), for update_coarse
 bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0,
-                  bool want_res = false, bool four = false) {
+                  bool want_res = false, bool four = false, bool defer_faces = false) {
   Level* L = level_ptr(c, lvl);
   const int n_sub = n_cycle * c->n_substeps - skip_last;
   bool res_done = false;
@@ -850,7 +868,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
         launch_gsrb4(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
       }
       L->d_phi = other;
-      deep_after(c, L);
+      deep_after(c, L, defer_faces && n + 3 == n_sub);
       n += 3;
       continue;
     }
@@ -1107,6 +1125,20 @@ void update_coarse(omg_ctx* c, int lvl, bool fused = false, bool tail_crhs = fal
                                F->d_dix, c->stream, nullptr, 0, bc_for(c, lvl, 1), F->has_rb, F->has_phys,
                                rbgv ? F->d_rbgv : nullptr))
         throw OmgError("smooth_resid: not available for this level");
+    } else if (F->faces_pending) {
+      // a split level's k_gsrb4 pass left its remote faces' ghosts in flight
+      // (deep_after): the boxes without such a face first
+      {
+        Prof p(c, "resid_restrict", (double)F->n_int * F->nc * F->nc * F->nc, lvl);
+        launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+                              F->d_dix, c->stream, F->d_int, F->n_int);
+      }
+      faces_join(c, F);
+      {
+        Prof p(c, "resid_restrict", (double)F->n_bnd * F->nc * F->nc * F->nc, lvl);
+        launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
+                              F->d_dix, c->stream, F->d_bnd, F->n_bnd);
+      }
     } else {
       Prof p(c, "resid_restrict", (double)F->n * F->nc * F->nc * F->nc, lvl);
       launch_resid_restrict(F->sweep_view(), view_of(c, lvl - 1), c->op, c->lambda, nullptr, 1, F->d_parent_local,
@@ -1756,8 +1788,9 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
                       level_ptr(c, l) && level_ptr(c, l)->d_b3 && level_ptr(c, l)->phi_gc_ok &&
                       (c->n_cycle_down * c->n_substeps) % 4 == 0;
     const bool fused = !four && smooth_resid_ok(c, l);
-    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0, false, four);
+    smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0, false, four, four);
     update_coarse(c, l, fused, tail_crhs && l == top + 1);
+    faces_join(c, level_ptr(c, l));   // (update_coarse joined them; defensive)
   }
   if (tail) {
     run_tail(c, top, tail_crhs);

@@ -207,6 +207,7 @@ struct Level {
   std::vector<int> prox_ids;     // global ids of the proxies, ascending
   Transfer deep_phi, deep_rhs;   // items: (box or n + proxy, brick)
   bool prox_rhs_ok = false;      // the proxies' rhs equals the owners' rhs
+  bool faces_pending = false;    // deep_after's remote faces still in flight on the comm stream
   int* d_physbox = nullptr;          // boxes with a physical face (k_phys_gc after such a chain)
   int n_physbox = 0;
   int* d_bnd = nullptr;              // boxes with a face on another GPU / the others
