@@ -74,10 +74,14 @@ METRIC = "V-cycle cell-updates/s + smoother HBM GB/s vs roofline, 3D Poisson 512
 
 # every Prof name the library records (omg_api.cpp); the per-cycle breakdown
 # also reports what these do not account for
-KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gsrb3p", "smoother_gsrb3r", "smoother_gsrb4", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
+KERNEL_FAMILIES = ("smoother_gsrb", "smoother_gsrb3", "smoother_gsrb3p", "smoother_gsrb3r", "smoother_gsrb4",
+                   "smoother_gsrb4p", "smoother_gs", "smooth_resid", "prolong_smooth", "coarse_tail",
                    "fill_gc", "resid_restrict", "residual", "restrict", "prolong_fill", "prolong",
                    "sub_parents", "coarse_rhs", "box_sums", "seq_sum", "subtract", "subtract_rhs")
 COMM_FAMILIES = ("comm", "comm_overlap")
+# the deep-halo rounds of split levels (pack + exchange + unpack, omg_api.cpp
+# deep_before / deep_after): reported beside the exchanges, not summed
+DEEP_FAMILIES = ("deep_phi", "deep_rhs", "deep_faces")
 
 
 # the multi-substep passes (omg_block.hip) by Prof name: kernel, cell updates
@@ -85,8 +89,10 @@ COMM_FAMILIES = ("comm", "comm_overlap")
 # one colour and rhs in, phi out; + the coarse res for the correction form),
 # beside 12 KiB of ghost faces per box
 PASSES = {
-    "smoother_gsrb4": ("k_gsrb4<OP_LPL> (the down-smoothing: four red-black substeps per pass)", 2.0,
-                       r"void omg::k_gsrb4<1>", 20.0),
+    "smoother_gsrb4": ("k_gsrb4<OP_LPL, 0> (the down-smoothing: four red-black substeps per pass)", 2.0,
+                       r"void omg::k_gsrb4<1(, 0)?>", 20.0),
+    "smoother_gsrb4p": ("k_gsrb4<OP_LPL, 2> (the up-smoothing: correction + four substeps per pass)", 2.0,
+                        r"void omg::k_gsrb4<1, 2>", 21.0),
     "smoother_gsrb3p": ("k_gsrb3<OP_LPL, 2, false> (the up-smoothing: correction + three substeps per pass)", 1.5,
                         r"void omg::k_gsrb3<1, 2, false>", 21.0),
     "smoother_gsrb3": ("k_gsrb3<OP_LPL, 0, false> (three red-black substeps per pass)", 1.5,
@@ -323,7 +329,7 @@ def profile_cycle(omg, mg, timer, cycle):
             n1, ms1, _ = mg.ctx.kernel_stats(f"{name}@{hi}")
             kern[name] = {"launches": n, "ms": round(ms, 4), f"launches_lvl{hi}": n1, f"ms_lvl{hi}": round(ms1, 4)}
     comm = {}
-    for name in COMM_FAMILIES:
+    for name in COMM_FAMILIES + DEEP_FAMILIES:
         n, ms, doubles = mg.ctx.kernel_stats(name)
         if n:
             comm[name] = {"rounds": n, "ms": round(ms, 4), "MB_received": round(8e-6 * doubles, 3)}

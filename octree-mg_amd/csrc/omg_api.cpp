@@ -1256,23 +1256,32 @@ bool block3c_ok(omg_ctx* c, const Level* F) {
          gsrb3_op_ok(c->op) && c->n_cycle_up * c->n_substeps >= 3;
 }
 // res_ready: the coarse level's last up pass stored its res = phi - old
-// (smooth_boxes' want_res), which the pass then reads instead of phi and old
-bool correct_block3(omg_ctx* c, int l, bool res_ready) {
+// (smooth_boxes' want_res), which the pass then reads instead of phi and old;
+// then, where the up-smoothing has four substeps or more, the pass is
+// k_gsrb4's correction form, substeps 1-4 (round 6: level 1 of C3 815 + 308
+// us for k_gsrb3's form + the one-substep launch before; OMG_NO_BLOCK4P: those)
+// Returns the substeps run (0: none, the caller corrects otherwise).
+int correct_block3(omg_ctx* c, int l, bool res_ready) {
   Level* F = level_ptr(c, l);
   Level* C = level_ptr(c, l - 1);
-  if (!block3c_ok(c, F) || !C || !C->phi_gc_ok || C->shift_pending) return false;
+  if (!block3c_ok(c, F) || !C || !C->phi_gc_ok || C->shift_pending) return 0;
   if (F->shift_pending) materialize_level(c, F);
   rb_stale_above(c, l);
   double* other = F->d_phi == F->d_data ? F->d_phi_buf : F->d_data;
-  {
+  const LevelView cv = C->view();
+  int done = 3;
+  if (res_ready && c->block4 && !c->no_block4p && c->n_cycle_up * c->n_substeps >= 4) {
+    Prof p(c, "smoother_gsrb4p", 2.0 * F->n * F->nc * F->nc * F->nc, l);
+    launch_gsrb4(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, &cv, F->d_b3c);
+    done = 4;
+  } else {
     Prof p(c, "smoother_gsrb3p", 1.5 * F->n * F->nc * F->nc * F->nc, l);
-    const LevelView cv = C->view();
     launch_gsrb3(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, true, &cv, F->d_b3c,
                  res_ready ? 2 : 1);
   }
   F->d_phi = other;
   F->phi_gc_ok = true;
-  return true;
+  return done;
 }
 
 // correct_children(lvl) followed by mg_fill_ghost_cells_lvl(lvl+1, phi), as the
@@ -1823,8 +1832,9 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
   for (int l = (tail ? top : min_lvl) + 1; l <= max_lvl; l++) {
     const bool want_res = l < max_lvl && block3c_ok(c, level_ptr(c, l + 1)) && !c->no_block3r;
     bool done = false;
-    if (!want_res && correct_block3(c, l, res_ready)) {
-      done = smooth_boxes(c, l, c->n_cycle_up, 4);
+    int pro = 0;
+    if (!want_res && (pro = correct_block3(c, l, res_ready)) > 0) {
+      done = smooth_boxes(c, l, c->n_cycle_up, pro + 1);
     } else if (prolong_smooth(c, l - 1)) {
       done = smooth_boxes(c, l, c->n_cycle_up, 2, 0, want_res);
     } else {
@@ -3252,6 +3262,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_block3p = env_flag("OMG_NO_BLOCK3P");
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     c->block4 = !env_flag("OMG_NO_BLOCK4");
+    c->no_block4p = env_flag("OMG_NO_BLOCK4P");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

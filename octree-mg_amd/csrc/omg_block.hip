@@ -469,25 +469,62 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
 // of a level whose residual + restriction then runs as k_resid_restrict (the
 // alternative to k_gsrb3 + k_smooth_resid, the default; OMG_NO_BLOCK4).  Every
 // ghost face of both colours is pushed.
+// PRO 2 (round 6): the up-smoothing's correct_children form with all four
+// substeps (k_gsrb3's PRO 2 reaches three, the fourth was a one-substep
+// launch): the colour 1-e it reads gets the prolonged correction from the
+// coarse res the coarse level's last pass stored, as in k_gsrb3.  The cells
+// used now reach 4 from the boxes (stage 1 at distance 3 reads them), so the
+// coarse tile has a 3-cell rim (cx in [-3, 18], cy in [-3, 10]) and the ring
+// starts at coarse plane -3.  The compute waves of k_gsrb4 are at 94 VGPRs,
+// two workgroups per CU allow 96, so in this form a wave of its own loads the
+// coarse planes into the ring (a wave's VGPR count is the most its own path
+// needs: 10 waves, two workgroups per CU at 5 waves per SIMD), and the
+// compute waves keep 2 planes of loads in flight instead of 4, which makes
+// room for the correction: 86 VGPRs.  On C3's level 1 it takes 881 us
+// against 819 + 307 for k_gsrb3's form and the last substep
+// (profiles/r06/s5_block4p_ab.txt; 4 ahead with rhs of colour 1-e in an LDS
+// ring and 2 VGPRs spilled took 1027 us, the correction formed by the loader
+// wave alone 1451 us: one wave's issue share of its SIMD).
 constexpr int B4NY = B3NC + 8, B4NT = B3NPX * B4NY, B4NW = (B4NT + 63) / 64, B4BS = 64 * (B4NW + 1);
 constexpr int B4PL = B3LP * (B4NY + 2);
+constexpr int B4CO = 3;
+constexpr int B4CX = kB3TX * B3H + 2 * B4CO, B4CY = B3H + 2 * B4CO, B4CT = B4CX * B4CY;
+constexpr int B4CL = (B4CT + 63) / 64;   // coarse cells per lane of the loader wave
+constexpr int b4_threads(int pro) { return pro ? B4BS + 64 : B4BS; }
 
-template <int OP>
-__global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict__ dst,
+template <int OP, int PRO>
+__global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* __restrict__ dst,
                                                const int* __restrict__ cols, double lambda, int e,
-                                               const double* __restrict__ shift) {
+                                               const double* __restrict__ shift, LevelView C,
+                                               const int* __restrict__ ccols, double fac) {
+  static_assert(PRO == 0 || PRO == 2, "k_gsrb4: plain or the correction from a stored coarse res");
   __shared__ double pl[2][4][B4PL];
   __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
   __shared__ unsigned bo[kB3Rec];
-  __shared__ int len_s;
+  __shared__ double rc[PRO ? 4 : 1][PRO ? B4CT : 1];   // coarse res, plane c in rc[c & 3]
+  __shared__ unsigned cbo[PRO ? kB3CSlots : 1];        // the coarse record, byte offsets
+  __shared__ int len_s, cyo_s;
   const int tid = threadIdx.x;
   const int cq = xcd_box(blockIdx.x, gridDim.x);
-  for (int q = tid; q < kB3Rec; q += B4BS) {
+  constexpr int BS = b4_threads(PRO);
+  // planes of loads in flight: the correction form 2 (its registers)
+  constexpr int AH = PRO ? 2 : kB3Ahead;
+  // steps of every wave's loop: planes -4-AH .. zend+4 in blocks of AH
+  const int t0 = -4 - AH;
+  for (int q = tid; q < kB3Rec; q += BS) {
     const int v = cols[(long long)cq * kB3Rec + q];
     if (q == 0) len_s = v;
     else bo[q - 1] = (unsigned)v * (unsigned)(L.stride * 8);
   }
-  for (int q = tid; q < 2 * 4 * B4PL; q += B4BS) (&pl[0][0][0])[q] = 0.0;
+  if (PRO) {
+    for (int q = tid; q < 1 + kB3CSlots; q += BS) {
+      const int v = ccols[(long long)cq * kB3CRec + q];
+      if (q == 0) cyo_s = v;
+      else cbo[q - 1] = (unsigned)v * (unsigned)(C.stride * 8);
+    }
+    for (int q2 = tid; q2 < 4 * B4CT; q2 += BS) (&rc[0][0])[q2] = 0.0;
+  }
+  for (int q = tid; q < 2 * 4 * B4PL; q += BS) (&pl[0][0][0])[q] = 0.0;
   __syncthreads();
   const int len = len_s, zend = B3NC * len;
   constexpr unsigned PB = 8u * B3H * B3NC;
@@ -496,6 +533,58 @@ __global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict_
     k = t - B3NC * (zs - 1) + 1;
     return zs;
   };
+  if (PRO && tid >= B4BS) {
+    // ---- the coarse loader wave: at the even step t it writes coarse plane
+    // t/2+1 to the ring (loaded 4 steps before) and loads plane t/2+3, the
+    // cells of the tile, B4CL per lane.  The compute threads read plane p at
+    // steps 2p-1 .. 2p+2 (the parent of planes 2p, 2p+1, the z tap of 2p-1
+    // and 2p+2); it is written at step 2p-2 and its slot next at 2p+6.
+    const int l = tid - B4BS, cyo = cyo_s, lenc = len >> 1;
+    const double* __restrict__ cres_in = C.data + 3 * C.vstride;
+    auto cload = [&](int c, double* v) {
+      const int zsc = c < 0 ? 0 : (c >= B3NC * lenc ? lenc + 1 : (c >> 4) + 1);
+      const int kc = c - B3NC * (zsc - 1) + 1;
+#pragma unroll
+      for (int r = 0; r < B4CL; r++) {
+        const int ct = min(l + 64 * r, B4CT - 1);
+        const int cxr = ct % B4CX - B4CO, cyy = cyo + ct / B4CX - B4CO;
+        const int xsc = cxr < 0 ? 0 : (cxr < B3NC ? 1 : 2), ysc = cyy < 0 ? 0 : (cyy < B3NC ? 1 : 2);
+        const int icc = cxr - B3NC * (xsc - 1) + 1, jcc = cyy - B3NC * (ysc - 1) + 1;
+        v[r] = b3_ld(cres_in, cbo[9 * zsc + 3 * ysc + xsc] + 8u * B3HV * ((icc + jcc + kc) & 1) +
+                                  8u * (((icc - 1) >> 1) + B3H * (jcc - 1)) + PB * (kc - 1));
+      }
+    };
+    double va[B4CL], vb[B4CL];
+    const int cmax = B3NC * lenc + 2;
+    auto cput = [&](int c, double* v) {
+#pragma unroll
+      for (int r = 0; r < B4CL; r++)
+        if (l + 64 * r < B4CT) rc[c & 3][l + 64 * r] = b3_take(v[r]);
+    };
+    auto cstep = [&](int t, double* v) {
+      const int c = t / 2 + 1;
+      cput(c, v);
+      cload(min(c + 2, cmax), v);
+    };
+    // the first step is t0 = -6 (even): planes -2 and -1 come from the loop,
+    // plane -3 (read from step -4 on) is written before it
+    static_assert(!PRO || AH == 2, "the loader's steps start at plane -6");
+    cload(-3, va);
+    cput(-3, va);
+    cload(-2, va);
+    cload(-1, vb);
+    // (the steps of the compute loop: AH * ceil((zend + 5 - t0) / AH), a multiple of 4)
+    const int n_steps = AH * ((zend + 5 - t0 + AH - 1) / AH);
+    for (int t = t0; t < t0 + n_steps; t += 4) {
+      cstep(t, va);
+      __syncthreads();
+      __syncthreads();
+      cstep(t + 2, vb);
+      __syncthreads();
+      __syncthreads();
+    }
+    return;
+  }
 
   if (tid >= B4NW * 64) {
     // ---- the store wave: plane t-5 (written to fin by iteration t-1) ------
@@ -543,9 +632,9 @@ __global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict_
         b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
       }
     };
-    for (int t = -4 - kB3Ahead; t <= zend + 4; t += kB3Ahead) {
+    for (int t = t0; t <= zend + 4; t += AH) {
 #pragma unroll
-      for (int u = 0; u < kB3Ahead; u++) {
+      for (int u = 0; u < AH; u++) {
         flush(t + u);
         __syncthreads();
       }
@@ -565,8 +654,11 @@ __global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict_
   const int li = act ? (p + 1) + B3LP * (y + 5) : B3LP + 1;
   const bool ctr = act && xs >= 1 && xs <= kB3TX && ys == 1;
   const int fi = ctr ? (j - 1) * B3CP + (xs - 1) * B3H + ih : 0;
-  const double m = shift ? *shift : 0.0;
-  const OpCoef<OP> K(L, lambda);
+  const double m = (!PRO && shift) ? *shift : 0.0;
+  // fac from the host (op_fac: the same expression, so the same bits): the
+  // division on the device would hold it in VGPRs
+  OpCoef<OP> K(L, lambda);
+  K.fac = fac;
   const double* __restrict__ src = L.phi + (1 - e) * B3HV;
   const double* __restrict__ rhe = L.data + L.vstride + e * B3HV;
   const double* __restrict__ rho = L.data + L.vstride + (1 - e) * B3HV;
@@ -588,10 +680,24 @@ __global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict_
   // t-3), V3 stage 3 (t-5, t-4); rhs colour e at t-1 .. t-3, 1-e at t-1 .. t-4
   double oa = 0.0, ob = 0.0, ea = 0.0, eb = 0.0, wa = 0.0, wb = 0.0, xa = 0.0, xb = 0.0;
   double re1 = 0.0, re2 = 0.0, re3 = 0.0, ro1 = 0.0, ro2 = 0.0, ro3 = 0.0, ro4 = 0.0;
+  // PRO: this thread's coarse cell (the parent of its pair) in the tile
+  const int ci = act ? (p - 2 + B4CO) + B4CX * ((y >> 1) + B4CO) : B4CX + 1;
   auto step = [&](int t, double& q, double& fe, double& fo) {
-    const double ot = shift ? b3_take(q) - m : b3_take(q);
+    double ot = (!PRO && shift) ? b3_take(q) - m : b3_take(q);
     const double ret = b3_take(fe), rot = b3_take(fo);
-    load(t + kB3Ahead, q, fe, fo);
+    load(t + AH, q, fe, fo);
+    if (PRO) {
+      // phi += prolong(res) on the colour-(1-e) cell (prolong_at, as k_gsrb3)
+      const int cz0 = t >> 1;
+      const double* R0 = rc[cz0 & 3];
+      const double* Rz = rc[((t & 1) ? cz0 + 1 : cz0 - 1) & 3];
+      const bool lft = ((y + t) & 1) == e;
+      const double f0 = 0.25 * R0[ci];
+      const double fx = 0.25 * R0[lft ? ci - 1 : ci + 1];
+      const double fy = 0.25 * R0[(y & 1) ? ci + B4CX : ci - B4CX];
+      const double fz = 0.25 * Rz[ci];
+      ot = ot + (f0 + fx + fy + fz);
+    }
     const double* P0 = pl[t & 1][0];
     const double* P1 = pl[t & 1][1];
     const double* P2 = pl[t & 1][2];
@@ -632,23 +738,38 @@ __global__ void __launch_bounds__(B4BS) k_gsrb4(LevelView L, double* __restrict_
     re3 = re2; re2 = re1; re1 = ret;
     ro4 = ro3; ro3 = ro2; ro2 = ro1; ro1 = rot;
   };
-  double qs[kB3Ahead], fes[kB3Ahead], fos[kB3Ahead];
+  double qs[AH], fes[AH], fos[AH];
 #pragma unroll
-  for (int u = 0; u < kB3Ahead; u++) qs[u] = fes[u] = fos[u] = 0.0;
-  for (int t = -4 - kB3Ahead; t <= zend + 4; t += kB3Ahead) {
+  for (int u = 0; u < AH; u++) qs[u] = fes[u] = fos[u] = 0.0;
+  for (int t = t0; t <= zend + 4; t += AH) {
 #pragma unroll
-    for (int u = 0; u < kB3Ahead; u++) step(t + u, qs[u], fes[u], fos[u]);
+    for (int u = 0; u < AH; u++) step(t + u, qs[u], fes[u], fos[u]);
   }
 }
 
+// OpCoef's fac on the host: box_gs_lpl's 0.5/sum(idr2) (m_laplacian.f90:64-65),
+// box_gs_helmh's 1/(2*sum(idr2)+lambda) (m_helmholtz.f90:58-59), the same
+// operations in the same order as the device's (IEEE division both sides)
+static double op_fac(const LevelView& L, int op, double lambda) {
+  const double ix = L.idr2[0], iy = L.idr2[1], iz = L.idr2[2];
+  return op == OP_HELM ? 1.0 / (2 * ((ix + iy) + iz) + lambda) : 0.5 / ((ix + iy) + iz);
+}
+
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st) {
+                  const double* shift, hipStream_t st, const LevelView* coarse, const int* ccols) {
+  const double fac = op_fac(L, op, lambda);
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb4: box size must be 16");
-  if (op == OP_HELM)
-    k_gsrb4<OP_HELM><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift);
-  else
-    k_gsrb4<OP_LPL><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift);
+  if (coarse && (coarse->nc != B3NC || !ccols || shift))
+    throw std::runtime_error("launch_gsrb4: the correction form needs a 16^3 coarse level, its records, no shift");
+  const LevelView& C = coarse ? *coarse : L;
+  if (op == OP_HELM) {
+    if (coarse) k_gsrb4<OP_HELM, 2><<<n_cols, b4_threads(2), 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+    else k_gsrb4<OP_HELM, 0><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+  } else {
+    if (coarse) k_gsrb4<OP_LPL, 2><<<n_cols, b4_threads(2), 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+    else k_gsrb4<OP_LPL, 0><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+  }
 }
 
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }

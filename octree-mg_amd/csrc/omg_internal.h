@@ -347,6 +347,7 @@ struct omg_ctx {
   bool no_deep = false;                // OMG_NO_DEEP: split levels keep one substep per launch (no deep halo)
   bool no_block3p = false;             // OMG_NO_BLOCK3P: correct_children by k_prolong_smooth, not k_gsrb3
   bool block4 = true;                  // the down-smoothing as k_gsrb4 + the unfused residual (OMG_NO_BLOCK4: off)
+  bool no_block4p = false;             // OMG_NO_BLOCK4P: the up-smoothing's correction form with three substeps (k_gsrb3)
   bool no_block3r = false;             // OMG_NO_BLOCK3R: no res from the coarse level's last pass (k_gsrb3 forms phi - old)
   int b3_min_boxes = omg::kB3MinBoxes;  // smallest level for k_gsrb3 (OMG_BLOCK3_MIN_BOXES, tests)
   int b3_col = 0;                      // k_gsrb3 column length (0: by level size; OMG_BLOCK3_COLUMN, tests)

@@ -60,8 +60,12 @@ bool gsrb3_op_ok(int op);
 // four substeps (colours e, 1-e, e, 1-e) per pass, same columns (k_gsrb4,
 // omg_block.hip): the down-smoothing of a level whose residual + restriction
 // then runs unfused (the default; OMG_NO_BLOCK4)
+// coarse (PRO 2, round 6): the up-smoothing's correct_children form with all
+// four substeps, the correction from the coarse res its last pass stored
+// (k_gsrb3's coarse_mode 2; ccols as for launch_gsrb3)
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st);
+                  const double* shift, hipStream_t st, const LevelView* coarse = nullptr,
+                  const int* ccols = nullptr);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
 // halves are left stale: only for a pass that k_smooth_resid follows, which
 // reads colour e's and forms colour 1-e's itself)

@@ -54,15 +54,17 @@ def _assert_same(dev, orc, ivs=(1, 2, 3, 4)):
             assert np.array_equal(a[:, m].view(np.uint64), b[:, m].view(np.uint64)), (lvl, iv)
 
 
-def _pair(args, down, up):
+def _pair(args, down, up, subtract_mean=None):
     cfg = parse(args)
     dev, orc = DeviceBackend(cfg), OracleBackend(cfg)
     import pyoracle  # on sys.path once OracleBackend exists (checker only)
+    sub = cfg["bc"] == "per" if subtract_mean is None else subtract_mean
     dev.mg.n_cycle_down, dev.mg.n_cycle_up = down, up
+    dev.mg.subtract_mean = sub
     dev.mg._push_methods()
     op = OPS[cfg["op"]]
     orc.o.configure(op=op, lam=cfg["lam"], smoother=pyoracle.GSRB, n_cycle_down=down, n_cycle_up=up,
-                    subtract_mean=cfg["bc"] == "per")
+                    subtract_mean=sub)
     for be in (dev, orc):
         setup_problem(be)
     return dev, orc
@@ -88,11 +90,13 @@ def test_block3_fmg_matches_oracle(have_guess):
         _assert_same(dev, orc)
 
 
-@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P", "OMG_NO_BLOCK3R"])
+@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P", "OMG_NO_BLOCK3R", "OMG_NO_BLOCK4P"])
 def test_block3_switch_off_same_bits(monkeypatch, switch):
     """OMG_NO_BLOCK3=1 (one substep per launch) / OMG_NO_BLOCK3P=1 (the
     correction by k_prolong_smooth) / OMG_NO_BLOCK3R=1 (no res from the coarse
-    level's last pass) and the default give the same state after each cycle."""
+    level's last pass) / OMG_NO_BLOCK4P=1 (the correction form with three
+    substeps, k_gsrb3, instead of k_gsrb4's four) and the default give the
+    same state after each cycle."""
     args = "16 128 128 128 2 v gsrb lpl 0 per sol 1 lb 0"
     dev, orc = _pair(args, 3, 2)
     monkeypatch.setenv(switch, "1")
@@ -117,6 +121,25 @@ def test_block4_vcycles_match_oracle(monkeypatch, args, down, up, switch):
     if switch:
         monkeypatch.setenv(switch, "1")
     dev, orc = _pair(args, down, up)
+    for _ in range(3):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc)
+
+
+# the passes swap a level's phi buffer on the host as a captured
+# cycle is recorded; a capture (1) or an instantiation / launch (2) that fails
+# leaves phi where it was (graph_rollback restores the buffers).  The graph
+# path needs a cycle that never waits for the host: no subtract_mean here (on
+# both sides), so periodic Helmholtz with the level bound lowered.
+@pytest.mark.parametrize("fail_at", [1, 2])
+def test_block3_graph_failure_keeps_phi(monkeypatch, fail_at):
+    from tests.mgdriver import omg
+    monkeypatch.setenv("OMG_GRAPH", "1")
+    monkeypatch.setenv("OMG_GRAPH_FAIL", str(fail_at))
+    dev, orc = _pair("16 128 128 128 3 v gsrb helm 2 per sol 1 lb 0", 2, 2, subtract_mean=False)
+    with pytest.raises(omg.device.OmgError, match="injected failure"):
+        dev.vcycle(True)
+    _assert_same(dev, orc)
     for _ in range(3):
         assert dev.vcycle(True) == orc.vcycle(True)
         _assert_same(dev, orc)
