@@ -18,6 +18,9 @@ for s in "$@"; do
             timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5; } > ${O}_loop.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
+    benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
+    prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/${O}_prof" -o run --output-format csv \
+             -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-parity) > ${O}_prof.log 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   echo "=== $s rc=$rc $(date +%T)"

@@ -12,6 +12,19 @@ import sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # name -> [(file, old, new), ...]
 VARIANTS = {
+    # plain k_gsrb4 with a tenth, idle wave (as the correction form's loader)
+    "b4w10": [("omg_block.hip", "constexpr int b4_threads(int pro) { return pro ? B4BS + 64 : B4BS; }",
+               "constexpr int b4_threads(int pro) { return B4BS + 64; }"),
+              ("omg_block.hip", "  if (PRO && tid >= B4BS) {",
+               "  if (!PRO && tid >= B4BS) {\n    for (int t = -4 - AH; t <= zend + 4; t += AH)\n      for (int u = 0; u < AH; u++) __syncthreads();\n    return;\n  }\n  if (PRO && tid >= B4BS) {"),
+              ("omg_block.hip", "else k_gsrb4<OP_HELM, 0><<<n_cols, B4BS, 0, st>>>", "else k_gsrb4<OP_HELM, 0><<<n_cols, B4BS + 64, 0, st>>>"),
+              ("omg_block.hip", "else k_gsrb4<OP_LPL, 0><<<n_cols, B4BS, 0, st>>>", "else k_gsrb4<OP_LPL, 0><<<n_cols, B4BS + 64, 0, st>>>")],
+    # k_gsrb4's plain form (the down-smoothing) with 2 planes of loads in
+    # flight, as its correction form (r06)
+    "b4ah2": [("omg_block.hip", "constexpr int AH = PRO ? 2 : kB3Ahead;", "constexpr int AH = 2;")],
+    # k_gsrb3 (every form) with 2 planes ahead
+    "b3ah2": [("omg_block.hip", "constexpr int kB3Ahead = 4;", "constexpr int kB3Ahead = 2;"),
+              ("omg_block.hip", "constexpr int AH = PRO ? 2 : kB3Ahead;", "constexpr int AH = PRO ? 2 : 4;")],
     # the periodic rhs pass (k_box_sums3<SUB>): 16 leaves per wave (2048
     # waves, two per SIMD on C3's level 1) / chunks of 8 rows / both
     "sumslpw16": [("omg_tiles.hip", "constexpr int kSumsLPW = 32, kSumsR = 4;", "constexpr int kSumsLPW = 16, kSumsR = 4;")],
