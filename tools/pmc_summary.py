@@ -3,9 +3,10 @@
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are reported in KiB; on gfx950 FETCH_SIZE counts
-exactly half the bytes of a 16-B-per-lane streaming read, so it is doubled
-(every load of the measured kernels is a 16-B-per-lane double2 stream except
-the neighbour-kind tables, a few KB).  WRITE_SIZE is taken as is.
+exactly half the bytes of a 16-B-per-lane streaming read, so it is doubled;
+the same holds for 8-B-per-lane loads (the block passes', calibrated in
+profiles/r06/fetch_calib.txt).  WRITE_SIZE is taken as is (exact for 8-B and
+16-B stores, temporal or nt).
 usage: pmc_summary.py gpurun_out/pmc_<op> > profiles/<round>/pmc_<op>.json
 """
 import collections
@@ -40,7 +41,7 @@ def main():
         out[f"{k}@{wg}"] = e
     tl = os.path.join(d, "time.log")
     json.dump({"source": d, "time_log": open(tl).read().strip().splitlines()[-1] if os.path.exists(tl) else None,
-               "correction": "FETCH_SIZE x2 (gfx950, 16-B/lane streaming reads), KiB -> bytes",
+               "correction": "FETCH_SIZE x2 (gfx950 streaming reads, 16-B and 8-B per lane: profiles/r06/fetch_calib.txt), KiB -> bytes",
                "kernels": out}, sys.stdout, indent=1)
 
 
