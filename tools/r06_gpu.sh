@@ -13,6 +13,7 @@ for s in "$@"; do
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1; rc=$? ;;
     deep) timeout -k 10 900 $PT tests/test_gpu_multirank.py -k deep > ${O}_deep.log 2>&1; rc=$? ;;
     block3) timeout -k 10 900 $PT tests/test_gpu_block3.py > ${O}_block3.log 2>&1; rc=$? ;;
+    golden) timeout -k 10 900 $PT tests/test_gpu_parity.py -k "test_device_matches_reference_golden and (c3_ or per256 or c2_256 or c5_)" > ${O}_golden.log 2>&1; rc=$? ;;
     c3multi) timeout -k 10 900 $PT tests/test_gpu_multirank.py -k c3_512 > ${O}_c3multi.log 2>&1; rc=$? ;;
     loop) { timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && \
             timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5; } > ${O}_loop.log 2>&1; rc=$? ;;
