@@ -740,11 +740,28 @@ void deep_after(omg_ctx* c, Level* L, bool defer = false) {
     L->faces_pending = true;
   }
   Prof p(c, "deep_faces", (double)L->halo.n_recv * L->nc * L->nc, L->lvl, st);
-  launch_face_pack(L->view(), L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, st);
+  launch_face_pack(L->view(), 1, L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, st);
   exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, st, L->lvl);
   launch_unpack_faces(L->view(), 1, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, st);
   if (L->faces_pending) HIPCHK(hipEventRecord(c->ev_comm, c->stream_comm));
 }
+// after a deep level's RES pass (res = phi - old, stored for the correction
+// form above): the proxies get res where the level above's columns read it
+// (the bricks of the deep halo, both colours), and this rank's faces toward
+// other GPUs get their res ghosts (the halo plan), as the pass gave the
+// same-GPU ones
+void deep_res(omg_ctx* c, Level* L) {
+  if (!L->deep) return;
+  const LevelView V = L->view();
+  Prof p(c, "deep_res", (double)L->deep_rhs.n_recv * 64, L->lvl);
+  launch_deep_copy(V, 4, 0, 64, L->deep_rhs.d_send_items, L->deep_rhs.n_send, L->d_sendbuf, false, c->stream);
+  exchange(c, L->deep_rhs, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+  launch_deep_copy(V, 4, 0, 64, L->deep_rhs.d_recv_items, L->deep_rhs.n_recv, L->d_recvbuf, true, c->stream);
+  launch_face_pack(V, 4, L->halo.d_send_items, L->halo.n_send, L->d_sendbuf, c->stream);
+  exchange(c, L->halo, L->d_sendbuf, L->d_recvbuf, nullptr, L->lvl);
+  launch_unpack_faces(V, 4, L->halo.d_recv_items, L->halo.n_recv, L->d_recvbuf, c->stream);
+}
+
 // the deferred faces of deep_after have arrived (the main stream waits)
 void faces_join(omg_ctx* c, Level* L) {
   if (!L || !L->faces_pending) return;
@@ -890,6 +907,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       res_done = res;
       L->d_phi = other;
       deep_after(c, L);
+      if (res) deep_res(c, L);
       n += 2;
       continue;
     }
@@ -1265,11 +1283,14 @@ int correct_block3(omg_ctx* c, int l, bool res_ready) {
   Level* F = level_ptr(c, l);
   Level* C = level_ptr(c, l - 1);
   if (!block3c_ok(c, F) || !C || !C->phi_gc_ok || C->shift_pending) return 0;
+  // (a split level: only from the coarse res, whose proxies deep_res filled)
+  if (F->deep && !res_ready) return 0;
   if (F->shift_pending) materialize_level(c, F);
   rb_stale_above(c, l);
   double* other = F->d_phi == F->d_data ? F->d_phi_buf : F->d_data;
   const LevelView cv = C->view();
   int done = 3;
+  deep_before(c, F, 0);   // (the pass reads colour 0, before the correction)
   if (res_ready && c->block4 && !c->no_block4p && c->n_cycle_up * c->n_substeps >= 4) {
     Prof p(c, "smoother_gsrb4p", 2.0 * F->n * F->nc * F->nc * F->nc, l);
     launch_gsrb4(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, &cv, F->d_b3c);
@@ -1280,6 +1301,7 @@ int correct_block3(omg_ctx* c, int l, bool res_ready) {
                  res_ready ? 2 : 1);
   }
   F->d_phi = other;
+  deep_after(c, F);
   F->phi_gc_ok = true;
   return done;
 }
@@ -2547,14 +2569,28 @@ void build_block3(omg_ctx* c, Level& L) {
 // box is the own box of exactly two columns (its two halves in y), on a
 // coarse level of 16^3 boxes whose faces are all same-GPU boxes.
 void build_block3c(omg_ctx* c, Level& F, const Level& C) {
-  (void)c;
-  if (!F.d_b3 || F.h_b3.empty() || C.nc != 16 || C.replicated || C.n == 0 || F.n != 8 * C.n || F.deep || C.deep) return;
+  if (F.h_b3.empty() || C.nc != 16 || C.replicated || C.n == 0 || F.n != 8 * C.n || F.deep != C.deep) return;
   if (!block3_addressable(C.n + C.n_prox, C.stride)) return;
-  for (int8_t k : C.h_nbk)
-    if (k != NB_LOCAL) return;
+  if (!F.deep)
+    for (int8_t k : C.h_nbk)
+      if (k != NB_LOCAL) return;
   for (int b = 0; b < F.n; b++)
     if (F.parent_local[b] < 0) return;
-  auto nbc = [&](int b, int f) { return C.h_nba[(size_t)b * 6 + f]; };
+  // the coarse boxes by their neighbours: C's own table on one GPU; on a
+  // split level (deep halo on both levels) the global tree, a box on another
+  // rank standing for its proxy in C's arena (deep_res fills its res)
+  Tree T{c};
+  auto cslot = [&](int id) {
+    if (id > 0 && T.rank(id) == c->rank) return c->local_index[id];
+    auto it = std::lower_bound(C.prox_ids.begin(), C.prox_ids.end(), id);
+    return it != C.prox_ids.end() && *it == id ? C.n + (int)(it - C.prox_ids.begin()) : -1;
+  };
+  auto cid = [&](int x) { return x < C.n ? C.ids[x] : C.prox_ids[x - C.n]; };
+  auto nbc = [&](int b, int f) {
+    if (!F.deep) return C.h_nba[(size_t)b * 6 + f];
+    const int id = T.nbr(cid(b), f + 1);
+    return id > 0 ? cslot(id) : -1;
+  };
   auto dix = [&](int b, int q) { return (F.dix_packed[b] >> (10 * q)) & 1023; };
   std::vector<int> out((size_t)F.n_b3 * kB3CRec, 0);
   std::vector<int> own(C.n, 0);
@@ -2570,6 +2606,9 @@ void build_block3c(omg_ctx* c, Level& F, const Level& C) {
     int zc[kB3MaxZ / 2 + 2];
     zc[1] = F.parent_local[b0];
     for (int z = 2; z <= lenc; z++) zc[z] = nbc(zc[z - 1], 5);
+    if (F.deep)
+      for (int z = 2; z <= lenc; z++)
+        if (zc[z] < 0 || zc[z] >= C.n) return;   // (a column's coarse boxes are this rank's)
     zc[0] = nbc(zc[1], 4);
     zc[lenc + 1] = nbc(zc[lenc], 5);
     for (int z = 0; z <= lenc + 1; z++) {
@@ -2581,6 +2620,8 @@ void build_block3c(omg_ctx* c, Level& F, const Level& C) {
         row[xs] = nbc(row[3 + xs], 2);
         row[6 + xs] = nbc(row[3 + xs], 3);
       }
+      for (int q2 = 0; q2 < 9; q2++)
+        if (row[q2] < 0) return;
       for (int ys = 0; ys < 3; ys += 2)
         for (int xs = 0; xs < 2; xs++)
           if (nbc(row[3 * ys + xs], 1) != row[3 * ys + xs + 1]) return;
@@ -2618,12 +2659,15 @@ void build_block3c(omg_ctx* c, Level& F, const Level& C) {
 // whose union over those A is sent as 4^3-cell bricks (launch_deep_copy).  Every rank derives the same regions from the global
 // tree, so the brick lists pair up key for key (key 64*id + brick).
 //
-// Where: 16^3 levels whose every box is a leaf (rhs then changes only by the
-// periodic mean, which the proxies follow, not by update_coarse every cycle),
-// every face a box of the level (uniform, periodic or interior), x pairs of
-// boxes (even ix and its x+ neighbour) on one rank, at least b3_min_boxes
-// boxes on every rank holding some, and byte offsets of every rank's boxes
-// + proxies under 4 GiB; decided alike on every rank.
+// Where: 16^3 levels, every face a box of the level (uniform, periodic or
+// interior), x pairs of boxes (even ix and its x+ neighbour) on one rank, at
+// least b3_min_boxes boxes on every rank holding some, and byte offsets of
+// every rank's boxes + proxies under 4 GiB; decided alike on every rank.  On
+// a level of leaves rhs changes only by the periodic mean, which the proxies
+// follow; a level with parents gets its rhs from update_coarse every cycle,
+// so its proxies' rhs travels once per cycle.  Such a level (C3's level 0 at
+// N > 1) also stores res for the correction form above it (the RES pass), and
+// its proxies get that res too (deep_res).
 // the box at offset o (components -1..1) from id, walking x, y, z in turn
 // (zyx: the reverse order); 0 when the walk leaves the level's boxes
 int deep_walk(const Tree& T, int id, const int o[3], bool zyx = false) {
@@ -2671,7 +2715,7 @@ void plan_deep(omg_ctx* c, Level& L) {
   if (c->n_ranks == 1 || L.replicated || L.nc != 16 || c->no_block3 || c->no_deep) return;
   Tree T{c};
   const auto& ids = c->ids[l];
-  if (ids.empty() || c->leaves[l].size() != ids.size()) return;
+  if (ids.empty()) return;
   std::map<int, std::vector<int>> by_rank;
   bool split = false;
   for (int id : ids) {
@@ -3161,6 +3205,18 @@ void build_plan(omg_ctx* c) {
       dmalloc(&L.d_rbrecv, sizeof(double) * (size_t)L.rbx.n_recv * L.rbx.item_doubles);
     }
   }
+  // k_gsrb3 / k_gsrb4's correction form on split levels: which path the
+  // up-smoothing takes decides collective rounds (the deep halo of both
+  // levels, deep_res), and whether the coarse records could be built depends
+  // on each rank's boxes, so the ranks agree: every rank holding boxes of the
+  // level must have them, else none uses them
+  if (c->n_ranks > 1 && !c->host_only)
+    for (int l = c->lowest + 1; l <= c->highest; l++) {
+      Level& F = c->levels[l];
+      if (!F.deep) continue;
+      const bool fail = F.n > 0 && !F.d_b3c;
+      if (allreduce(c, fail ? 1.0 : 0.0, true) > 0.5) dfree(F.d_b3c);
+    }
   ensure_rhs_lex(c);
   rbh_build(c);
 }

@@ -140,8 +140,8 @@ void launch_unpack_faces(const LevelView& L, int iv, const int* items, int n, co
 // colour c (per 32) or both (per 64) between boxes / proxies and a buffer
 void launch_deep_copy(const LevelView& L, int iv, int c, int per, const int* items, int n, double* buf, bool unpack,
                       hipStream_t st);
-// the boundary layer of phi at the listed faces (b*6+nb-1) into the halo send buffer
-void launch_face_pack(const LevelView& L, const int* items, int n, double* buf, hipStream_t st);
+// the boundary layer of variable iv at the listed faces (b*6+nb-1) into the halo send buffer
+void launch_face_pack(const LevelView& L, int iv, const int* items, int n, double* buf, hipStream_t st);
 void launch_rb_pack(const LevelView& C, int iv, const int* items, int n, int nc, double* buf, hipStream_t st);
 void launch_rb_unpack(const LevelView& L, int iv, const int* items, int n, const double* recv, hipStream_t st);
 void launch_restrict(const LevelView& F, const LevelView& C, int iv, const int* pairs, int n_pairs,

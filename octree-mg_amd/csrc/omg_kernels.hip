@@ -89,23 +89,24 @@ void launch_deep_copy(const LevelView& L, int iv, int c, int per, const int* ite
   k_deep_copy<<<grid_for(work), 256, 0, st>>>(L, iv, c, per, items, n, buf, unpack ? 1 : 0);
 }
 
-// the boundary layer of phi at the listed faces (items b*6+nb-1) into the
-// halo send buffer, nc*nc doubles per face in the order k_unpack_faces
+// the boundary layer of variable iv at the listed faces (items b*6+nb-1) into
+// the halo send buffer, nc*nc doubles per face in the order k_unpack_faces
 // writes the peer's ghosts: after a pass that does not pack (k_gsrb3 /
-// k_gsrb4 on split levels)
-__global__ void __launch_bounds__(256) k_face_pack(LevelView L, const int* items, int n_items, double* buf) {
+// k_gsrb4 on split levels; iv 4: the res its RES form stores)
+__global__ void __launch_bounds__(256) k_face_pack(LevelView L, int iv, const int* items, int n_items,
+                                                   double* buf) {
   const int nc = L.nc, nc2 = nc * nc;
   GRID_STRIDE(t, (long long)n_items * nc2) {
     const int q = (int)(t / nc2), cell = (int)(t % nc2);
     const int f = items[q], b = f / 6, nb = f % 6 + 1;
-    buf[t] = boxp(L, 1, b)[off_face_cell(L, nb, (nb & 1) ? 1 : nc, cell % nc + 1, cell / nc + 1)];
+    buf[t] = boxp(L, iv, b)[off_face_cell(L, nb, (nb & 1) ? 1 : nc, cell % nc + 1, cell / nc + 1)];
   }
 }
 
-void launch_face_pack(const LevelView& L, const int* items, int n, double* buf, hipStream_t st) {
+void launch_face_pack(const LevelView& L, int iv, const int* items, int n, double* buf, hipStream_t st) {
   const long long work = (long long)n * L.nc * L.nc;
   if (work == 0) return;
-  k_face_pack<<<grid_for(work), 256, 0, st>>>(L, items, n, buf);
+  k_face_pack<<<grid_for(work), 256, 0, st>>>(L, iv, items, n, buf);
 }
 
 // buffer_for_fine_nb (m_ghost_cells.f90:385-422) on the coarse rank: the

@@ -147,7 +147,8 @@ def test_multirank_vcycle_makes_no_host_wait(args, ranks, monkeypatch):
 # every box's final phi must be the reference's at the same rank count.  (C3
 # itself at 2/4/8 ranks, test_c3_512_multirank_matches_reference_golden, takes
 # it at the default bound: 16384 / 8192 / 4096 boxes per rank on level 1.)
-DEEP_STATS = ("smoother_gsrb4@1", "smoother_gsrb3@1", "deep_phi@1", "deep_rhs@1", "deep_faces@1")
+DEEP_STATS = ("smoother_gsrb4@1", "smoother_gsrb3@1", "smoother_gsrb4p@1", "deep_phi@1", "deep_rhs@1",
+              "deep_faces@1", "deep_res@0")
 
 
 @pytest.mark.parametrize("name,ranks", [("per128_box16_gsrb_v", 2), ("per128_box16_gsrb_v", 8)])
@@ -158,9 +159,13 @@ def test_deep_halo_multirank_matches_reference(name, ranks, monkeypatch):
     _check(out, e["runs"][str(ranks)])
     n_it = parse(e["args"])["n_its"]
     for st in out["stats"]:
-        # per cycle: the down pass (k_gsrb4), the up pass after k_prolong_smooth
-        # (k_gsrb3), one phi round each; rhs once (the proxies follow the mean)
-        assert st["smoother_gsrb4@1"] == n_it and st["smoother_gsrb3@1"] == n_it, st
+        # per cycle: the down pass (k_gsrb4) and the up pass, one phi round
+        # each; rhs once (the proxies follow the mean).  The up pass is the
+        # correction form (k_gsrb4<PRO 2>) from level 0's res, which level 0
+        # (64 boxes, split too) stores with its last pass and sends to its
+        # proxies (deep_res)
+        assert st["smoother_gsrb4@1"] == n_it and st["smoother_gsrb4p@1"] == n_it, st
+        assert st["smoother_gsrb3@1"] == 0 and st["deep_res@0"] == n_it, st
         assert st["deep_phi@1"] == 2 * n_it and st["deep_rhs@1"] == 1 and st["deep_faces@1"] == 2 * n_it, st
 
 
