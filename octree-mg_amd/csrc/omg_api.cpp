@@ -783,6 +783,7 @@ double* red_mean(omg_ctx* c, int ch);
 // the residual + restriction run unfused after it, OMG_BLOCK4)
 // defer_faces: a k_gsrb4 pass that ends the smoothing leaves its remote faces'
 // exchange in flight on the comm stream (deep_after), for update_coarse
+bool b3_usable(omg_ctx* c, int lvl, B3Phys& P, const B3Phys*& ph);
 bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int skip_last = 0,
                   bool want_res = false, bool four = false, bool defer_faces = false) {
   Level* L = level_ptr(c, lvl);
@@ -792,9 +793,10 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
   if (n_sub >= 1) rb_stale_above(c, lvl);
   // a pending phi shift is subtracted by the first tiled substep while it
   // loads (the values it reads are dead afterwards); otherwise applied now
-  // (not next to refinement boundaries: their ghosts read the coarse level)
+  // (not next to refinement boundaries: their ghosts read the coarse level;
+  // nor before a block pass with physical faces, whose ghosts take no shift)
   const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 1 && L->phi_gc_ok &&
-                      !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb);
+                      !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb) && !(L->d_b3 && L->b3_phys);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
     // the register-ring kernel reads rhs from its ring-order copy, rebuilt
@@ -877,20 +879,24 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
     // substeps n, n+1, n+2 in one pass (k_gsrb3) into phi's other buffer: it
     // reads the neighbours' cells in their boxes, which equal its ghosts only
     // when they are consistent (phi_gc_ok), and writes every ghost face
-    if (four && (n_sub - n + 1) % 4 == 0 && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3) {
+    // (ph: the ghosts across physical faces, formed in the pass)
+    B3Phys P3;
+    const B3Phys* ph = nullptr;
+    const bool b3 = b3_usable(c, lvl, P3, ph);
+    if (four && (n_sub - n + 1) % 4 == 0 && b3 && (!ph || c->block4_phys)) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
       deep_before(c, L, 1 - e);
       {
         Prof p(c, "smoother_gsrb4", 2.0 * L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gsrb4(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream);
+        launch_gsrb4(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, nullptr, nullptr,
+                     ph);
       }
       L->d_phi = other;
       deep_after(c, L, defer_faces && n + 3 == n_sub);
       n += 3;
       continue;
     }
-    if (n + 2 <= n_sub && L->d_b3 && L->phi_gc_ok && gsrb3_op_ok(c->op) && !c->no_block3 &&
-        !(want_res && (n_sub - n + 1) % 3 != 0)) {
+    if (n + 2 <= n_sub && b3 && !(want_res && (n_sub - n + 1) % 3 != 0)) {
       double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
       // the down-smoothing's last pass before k_smooth_resid (skip_last: it
       // runs the next substep, colour 0, and forms colour 0's ghosts itself
@@ -902,7 +908,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       {
         Prof p(c, res ? "smoother_gsrb3r" : "smoother_gsrb3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
         launch_gsrb3(L->view(), other, L->d_b3, L->n_b3, c->op, c->lambda, e, shift, c->stream, push1, nullptr,
-                     nullptr, 1, res);
+                     nullptr, 1, res, ph);
       }
       res_done = res;
       L->d_phi = other;
@@ -1815,9 +1821,12 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     // four substeps per pass, then the unfused residual (k_resid_restrict):
     // C3 4.06 -> 3.97 ms against k_gsrb3 + k_smooth_resid (level 1 775 + 592
     // us; level 0 even, profiles/r05/s50_block4_ab.txt); OMG_NO_BLOCK4: the latter
-    const bool four = c->block4 && !c->no_block3 && c->smoother == OMG_SMOOTHER_GSRB && gsrb3_op_ok(c->op) &&
-                      level_ptr(c, l) && level_ptr(c, l)->d_b3 && level_ptr(c, l)->phi_gc_ok &&
-                      (c->n_cycle_down * c->n_substeps) % 4 == 0;
+    // (a level with physical faces: k_gsrb3 + k_smooth_resid, whose k_gsrb4
+    // takes a workgroup per CU, 114 VGPRs; OMG_BLOCK4_PHYS: k_gsrb4 there too)
+    B3Phys P3;
+    const B3Phys* ph = nullptr;
+    const bool four = c->block4 && c->smoother == OMG_SMOOTHER_GSRB && b3_usable(c, l, P3, ph) &&
+                      (!ph || c->block4_phys) && (c->n_cycle_down * c->n_substeps) % 4 == 0;
     const bool fused = !four && smooth_resid_ok(c, l);
     smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0, false, four, four);
     update_coarse(c, l, fused, tail_crhs && l == top + 1);
@@ -2487,23 +2496,34 @@ bool block3_addressable(long long n_boxes, long long stride) {
   return (unsigned long long)n_boxes * (unsigned long long)stride * 8ull <= 0xFFFFFFFFull;
 }
 
+// boxes per column in z: 16 on levels of >= 32768 boxes, 4 down to 4096, below
+// that (levels that take the passes with OMG_BLOCK3_MIN_BOXES lowered) 2, for
+// more workgroups (OMG_BLOCK3_SMALL_COL); OMG_BLOCK3_COLUMN: all levels
+int b3_column(const omg_ctx* c, int n) {
+  if (c->b3_col) return c->b3_col;
+  return n / (kB3TX * 8) >= 2048 ? 16 : (n >= kB3MinBoxes ? 4 : c->b3_col_small);
+}
+
 // k_gsrb3's columns (launch_gsrb3): a level of at least kB3MinBoxes boxes of
-// 16^3 whose faces are all same-GPU boxes of the level (a periodic uniform
+// 16^3 whose faces are all same-GPU boxes of the level or physical (a uniform
 // level on one GPU) is tiled by columns of kB3TX boxes in x and up to kB3MaxZ
 // in z, each with the boxes around it; the level then gets phi's second
 // buffer.  Columns are ordered by z block, then Morton order in x / y, so that
 // each XCD's run of workgroups (xcd_box) is one compact patch whose halo
-// columns its own L2 holds.  Any face or tiling that does not fit: no records.
+// columns its own L2 holds.  A physical face (round 6) is a flag of the
+// column (kB3LenMask), the same for all its boxes, and the slot across it names
+// the box whose face it is.  Any face or tiling that does not fit: no records.
 void build_block3(omg_ctx* c, Level& L) {
   if (g_host_only || c->host_only || L.nc != 16 || L.n < c->b3_min_boxes || L.replicated || L.deep) return;
   // k_gsrb3 / k_gsrb4 address a variable with 32-bit byte offsets
   // (omg_block.hip b3_ld / b3_st): 95,325 boxes of 16^3 at most
   if (!block3_addressable(L.n + L.n_prox, L.stride)) return;
   for (int8_t k : L.h_nbk)
-    if (k != NB_LOCAL) return;
+    if (k != NB_LOCAL && !(k == NB_PHYS && !c->no_block3_phys)) return;
   const int n = L.n;
-  // face f: 0 x-, 1 x+, 2 y-, 3 y+, 4 z-, 5 z+
-  auto nb = [&](int b, int f) { return L.h_nba[(size_t)b * 6 + f]; };
+  // face f: 0 x-, 1 x+, 2 y-, 3 y+, 4 z-, 5 z+; across a physical face the box itself
+  auto phys = [&](int b, int f) { return L.h_nbk[(size_t)b * 6 + f] == NB_PHYS; };
+  auto nb = [&](int b, int f) { return phys(b, f) ? b : L.h_nba[(size_t)b * 6 + f]; };
   auto ixd = [&](int b, int d) { return c->ix[(size_t)(L.ids[b] - 1) * 3 + d] - 1; };
   auto spread = [](unsigned v) {
     unsigned long long r = 0;
@@ -2512,29 +2532,51 @@ void build_block3(omg_ctx* c, Level& L) {
   };
   std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
   std::vector<int> covered(n, 0);
+  bool any_phys = false;
   // columns of 16 boxes on levels of >= 32768 boxes, else 4: C3's level 1
   // 857 / 759 us per pass against 875 / 772 with 8 (1024 workgroups, fewer
   // halo planes per box; profiles/r05/s40_block3_z16_ab.txt) and 898 / 789
   // with 4 (s38); on its 4096-box level 8 gained nothing, and two-box columns,
   // twice the workgroups, took 110 us a pass against 102
-  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 16 : 4);
+  const int nzb = b3_column(c, L.n);
   static_assert(kB3MaxZ >= 16, "column records hold 16 boxes");
   for (int h = 0; h < n; h++) {
     if (ixd(h, 0) % kB3TX || ixd(h, 2) % nzb) continue;
     std::vector<int> zc{h};
-    while ((int)zc.size() < nzb) {
+    while ((int)zc.size() < nzb && !phys(zc.back(), 5)) {
       const int up = nb(zc.back(), 5);
       if (ixd(up, 2) % nzb == 0) break;   // the next column's first box
       zc.push_back(up);
     }
     const int len = (int)zc.size();
+    // the column's physical faces: x-, x+, y-, y+ alike for all its boxes (and
+    // none between the tile's boxes), z- of its first box, z+ of its last
+    int fl = (phys(zc[0], 4) ? 16 : 0) | (phys(zc[len - 1], 5) ? 32 : 0);
+    for (int z = 0; z < len; z++) {
+      int t[kB3TX];
+      t[0] = zc[z];
+      for (int xs = 1; xs < kB3TX; xs++) {
+        if (phys(t[xs - 1], 1)) return;
+        t[xs] = nb(t[xs - 1], 1);
+      }
+      int f = (phys(t[0], 0) ? 1 : 0) | (phys(t[kB3TX - 1], 1) ? 2 : 0);
+      for (int xs = 0; xs < kB3TX; xs++) {
+        const int fy = (phys(t[xs], 2) ? 4 : 0) | (phys(t[xs], 3) ? 8 : 0);
+        if (xs && fy != (f & 12)) return;
+        f |= fy;
+      }
+      if (z && f != (fl & 15)) return;
+      fl |= f;
+    }
+    any_phys |= fl != 0;
     std::vector<int> r(kB3Rec, 0);
-    r[0] = len;
+    r[0] = len | fl << 8;
     for (int zs = 0; zs <= len + 1; zs++) {
       const int cb = zs == 0 ? nb(zc[0], 4) : (zs == len + 1 ? nb(zc[len - 1], 5) : zc[zs - 1]);
       int* row = &r[1 + kB3S * zs];
       // the tile's row of boxes along x, then the rows below and above it in
       // y; a grid: the rows' x neighbours agree with the y neighbours' chain
+      // (except where a slot stands across a physical face)
       row[kB3TX + 2] = nb(cb, 0);
       for (int xs = 1; xs <= kB3TX + 1; xs++) row[(kB3TX + 2) + xs] = xs == 1 ? cb : nb(row[(kB3TX + 2) + xs - 1], 1);
       for (int xs = 0; xs < kB3TX + 2; xs++) {
@@ -2544,7 +2586,7 @@ void build_block3(omg_ctx* c, Level& L) {
         if (zs >= 1 && zs <= len && xs >= 1 && xs <= kB3TX) covered[mid]++;
       }
       for (int ys = 0; ys < 3; ys += 2)
-        for (int xs = 0; xs + 1 < kB3TX + 2; xs++)
+        for (int xs = (fl & 1) ? 1 : 0; xs + 1 < kB3TX + ((fl & 2) ? 1 : 2); xs++)
           if (nb(row[(kB3TX + 2) * ys + xs], 1) != row[(kB3TX + 2) * ys + xs + 1]) return;
     }
     const unsigned long long key = ((unsigned long long)(ixd(h, 2) / nzb) << 40) |
@@ -2558,9 +2600,50 @@ void build_block3(omg_ctx* c, Level& L) {
   flat.reserve(cols.size() * kB3Rec);
   for (auto& cr : cols) flat.insert(flat.end(), cr.second.begin(), cr.second.end());
   L.n_b3 = (int)cols.size();
+  L.b3_phys = any_phys;
   L.d_b3 = to_device(flat);
   L.h_b3 = std::move(flat);
   dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)L.n * L.stride, true);
+}
+
+// The ghost terms of the block passes' physical faces: bc_to_gc's c0 * b, c1,
+// c2 per face (m_ghost_cells.f90:665-766; k_gsrb_tile's phys_ghost, the same
+// expressions), for constant boundary values only; false when the level's
+// are tabulated (a boundary callback) or stored with phi.
+bool b3_phys_args(omg_ctx* c, int lvl, const Level& L, B3Phys& P) {
+  if (c->phi_bc_data_stored) return false;
+  auto it = c->d_face_off_lvl[0].find(lvl);
+  if (it != c->d_face_off_lvl[0].end() && it->second) return false;
+  for (int nb = 1; nb <= 6; nb++) {
+    const int type = c->bc[0].type[nb - 1];
+    const double bv = c->bc[0].value[nb - 1];
+    double c0, c1, c2;
+    if (type == OMG_BC_DIRICHLET) {
+      c0 = 2; c1 = -1; c2 = 0;
+    } else if (type == OMG_BC_NEUMANN) {
+      c0 = L.dr[(nb - 1) >> 1] * ((nb & 1) ? -1.0 : 1.0); c1 = 1; c2 = 0;
+    } else {
+      c0 = 0; c1 = 2; c2 = -1;
+    }
+    P.k[nb - 1] = c0 * bv;
+    P.c1[nb - 1] = c1;
+    P.c2[nb - 1] = c2;
+  }
+  return true;
+}
+
+// whether a block pass (k_gsrb3 / k_gsrb4) may smooth the level now: records,
+// consistent ghosts, an operator it has; ph: its physical faces' terms (null:
+// none), P their storage
+bool b3_usable(omg_ctx* c, int lvl, B3Phys& P, const B3Phys*& ph) {
+  const Level* L = level_ptr(c, lvl);
+  ph = nullptr;
+  if (!L || !L->d_b3 || !L->phi_gc_ok || !gsrb3_op_ok(c->op) || c->no_block3) return false;
+  if (L->b3_phys) {
+    if (!b3_phys_args(c, lvl, *L, P)) return false;
+    ph = &P;
+  }
+  return true;
 }
 
 // k_gsrb3's correct_children form (launch_gsrb3's ccols) for the columns of F:
@@ -2596,6 +2679,7 @@ void build_block3c(omg_ctx* c, Level& F, const Level& C) {
   std::vector<int> own(C.n, 0);
   for (int q = 0; q < F.n_b3; q++) {
     const int* r = &F.h_b3[(size_t)q * kB3Rec];
+    if (r[0] > kB3LenMask) return;   // (physical faces: the plain passes only)
     const int len = r[0], lenc = len / 2;
     if (len % 2) return;
     auto fine = [&](int zs, int xs) { return r[1 + kB3S * zs + (kB3TX + 2) + xs]; };
@@ -2799,7 +2883,7 @@ void plan_deep(omg_ctx* c, Level& L) {
     if (it == pidx.end()) throw OmgError("plan_deep: a column reads a box outside the proxies");
     return it->second;
   };
-  const int nzb = c->b3_col ? c->b3_col : (L.n / (kB3TX * 8) >= 2048 ? 16 : 4);
+  const int nzb = b3_column(c, L.n);
   std::vector<std::pair<unsigned long long, std::vector<int>>> cols;
   std::vector<int> covered(L.n, 0);
   auto spread = [](unsigned v) {
@@ -3274,11 +3358,13 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     // contexts too, whose plans the CPU tests pair up)
     auto plan_switches = [](omg_ctx* c) {
       c->no_block3 = env_flag("OMG_NO_BLOCK3");
+      c->no_block3_phys = env_flag("OMG_NO_BLOCK3_PHYS");
       c->no_deep = env_flag("OMG_NO_DEEP");
       // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
       if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));
       // (tests: the column length, 2 .. 16 boxes, even; OMG_BLOCK3_COLUMN)
       if (const char* v = getenv("OMG_BLOCK3_COLUMN")) c->b3_col = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
+      if (const char* v = getenv("OMG_BLOCK3_SMALL_COL")) c->b3_col_small = std::min(std::max(2, atoi(v) & ~1), kB3MaxZ);
     };
     if (device == OMG_DEVICE_NONE) {   // plan-only context: no HIP, no RCCL
       omg_ctx* c = new omg_ctx();
@@ -3319,6 +3405,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->no_block3r = env_flag("OMG_NO_BLOCK3R");
     c->block4 = !env_flag("OMG_NO_BLOCK4");
     c->no_block4p = env_flag("OMG_NO_BLOCK4P");
+    c->block4_phys = env_flag("OMG_BLOCK4_PHYS");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

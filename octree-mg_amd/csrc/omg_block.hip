@@ -96,6 +96,63 @@ __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
 }
 
+// The ghost across a physical face, bc_to_gc's c0 * b + c1 * x1 + c2 * x2
+// (m_ghost_cells.f90:665-766) in its order, k = c0 * b: x1 the cell next to
+// the face, x2 the one behind it
+__device__ __forceinline__ double b3_bc(double k, double c1, double c2, double x1, double x2) {
+  return (k + c1 * x1) + c2 * x2;
+}
+
+// A compute thread's share of a column's physical faces (PHYS passes).
+// Where the column has one, nothing lies beyond it: the reference reads the
+// ghost layer, filled by bc_to_gc after every substep from the cells next to
+// the face.  Substep 1 reads the ghosts as they are on entry (consistent), so
+// the thread whose pair is across the face loads its colour-(1-e) ghost
+// there instead of a neighbour's cell (the slot across the face names the
+// box whose face it is; xyq, kq: the ghost's offset from src and bytes per
+// plane).  Later substeps form the ghost where it is read: bx / by = 1 (2)
+// when the thread's pair is next to face x- (x+) / y- (y+), whose ghost
+// then comes from the cell's own value before the substep and the one behind
+// it.  Everything else beyond a physical face is computed and never used.
+// (The faces' k, c1, c2 are read from LDS where used, pk = B3Phys as 18
+// doubles: in registers they cost a workgroup per CU.)
+struct B3Face {
+  unsigned xyq, kq;
+  int bx, by;
+};
+__device__ __forceinline__ B3Face b3_face(int fl, int p, int npx, int y, int ih, int j, int e, unsigned xyb,
+                                          unsigned pb) {
+  B3Face f;
+  constexpr int HV = 8 * 16 * 16, FH = 8 * 16, FS = 2 * FH;
+  f.xyq = xyb;
+  f.kq = pb;
+  const int gx = (fl & 1) && p == 1 ? 1 : ((fl & 2) && p == npx - 2 ? 2 : 0);
+  const int gy = (fl & 4) && y == -1 ? 1 : ((fl & 8) && y == 16 ? 2 : 0);
+  if (gx || gy) {
+    // face gx-1 (x) at (j, k), or 1+gy (y) at (i, k): its colour-(1-e) half
+    const int o = gx ? 2 * HV + (gx - 1) * FS + (1 - e) * FH + ((j - 1) >> 1)
+                     : 2 * HV + (1 + gy) * FS + (1 - e) * FH + ih;
+    f.xyq = 8u * (unsigned)(o - (1 - e) * HV);
+    f.kq = 8u * 8u;
+  }
+  f.bx = (fl & 1) && p == 2 ? 1 : ((fl & 2) && p == npx - 3 ? 2 : 0);
+  f.by = (fl & 4) && y == 0 ? 1 : ((fl & 8) && y == 15 ? 2 : 0);
+  return f;
+}
+
+// the neighbours of a PHYS pass's update at plane ts across the column's
+// physical faces (own: the cell's value before the substep); lft: the pair's
+// active cell is its left one (n.xm is then the x- neighbour, else x+)
+__device__ __forceinline__ void b3_fix(Nbr7& n, const B3Face& f, const double* pk, int fl, bool lft, double own,
+                                       int ts, int zend) {
+  auto bc = [&](int q, double x2) { return b3_bc(pk[q], pk[6 + q], pk[12 + q], own, x2); };
+  if ((f.bx == 1 && lft) || (f.bx == 2 && !lft)) n.xm = bc(f.bx - 1, n.xp);
+  if (f.by == 1) n.ym = bc(2, n.yp);
+  else if (f.by == 2) n.yp = bc(3, n.ym);
+  if ((fl & 16) && ts == 0) n.zm = bc(4, n.zp);
+  if ((fl & 32) && ts == zend - 1) n.zp = bc(5, n.zm);
+}
+
 }  // namespace
 
 // Workgroup = B3NW compute waves and one store wave.  A compute thread holds
@@ -134,24 +191,33 @@ __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
 // takes PRO 2: with the final plane the compute waves form res = phi - old
 // (old loaded with the plane kB3Ahead ahead), and the store wave stores it
 // with its ghost faces like phi.
-template <int OP, int PRO, bool RES>
+template <int OP, int PRO, bool RES, bool PHYS>
 __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict__ dst,
                                                           const int* __restrict__ cols, double lambda, int e,
                                                           const double* __restrict__ shift, int push1, LevelView C,
-                                                          const int* __restrict__ ccols) {
+                                                          const int* __restrict__ ccols, B3Phys P) {
+  static_assert(!(PHYS && (PRO || RES)), "k_gsrb3: physical faces in the plain form only");
   __shared__ double pl[2][3][B3PL];
   // final plane: [row * B3CP + pair][colour e, 1-e (, their res)]
-  __shared__ double fin[2][B3NC * B3CP][RES ? 4 : 2];
+  // (PHYS: a ring of three, the z ghosts read the plane before)
+  __shared__ double fin[PHYS ? 3 : 2][B3NC * B3CP][RES ? 4 : 2];
+  auto fsl = [](int z) { return PHYS ? (z + 12) % 3 : z & 1; };
   __shared__ unsigned bo[kB3Rec];             // the record's boxes as byte offsets into a variable
   __shared__ double rc[PRO ? 4 : 1][PRO ? B3CT : 1];   // coarse phi - old, plane c in rc[c & 3]
   __shared__ unsigned cbo[PRO ? kB3CSlots : 1];   // the coarse record, byte offsets
-  __shared__ int len_s, cyo_s;
+  __shared__ int len_s, cyo_s, fl_s;
+  __shared__ double pk[PHYS ? 18 : 1];
   const int tid = threadIdx.x;
   const int cq = xcd_box(blockIdx.x, gridDim.x);
+  if (PHYS && tid >= B3BS - 18) pk[tid - (B3BS - 18)] = (&P.k[0])[tid - (B3BS - 18)];
   if (tid < kB3Rec) {
     const int v = cols[(long long)cq * kB3Rec + tid];
-    if (tid == 0) len_s = v;
-    else bo[tid - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+    if (tid == 0) {
+      len_s = v & kB3LenMask;
+      fl_s = v >> 8;
+    } else {
+      bo[tid - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+    }
   }
   if (PRO) {
     const int q = tid - kB3Rec;
@@ -165,6 +231,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   for (int q = tid; q < 2 * 3 * B3PL; q += B3BS) (&pl[0][0][0])[q] = 0.0;
   __syncthreads();
   const int len = len_s, zend = B3NC * len;
+  const int fl = PHYS ? fl_s : 0;
   constexpr unsigned PB = 8u * B3H * B3NC;   // bytes per plane of one colour
   auto zbox = [&](int t, int& k) {
     const int zs = t < 0 ? 0 : (t >= zend ? len + 1 : (t >> 4) + 1);
@@ -220,10 +287,13 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
       const int z = t - 4;
       if (z < 0 || z >= zend) return;
       int k;
-      const int r0 = kB3S * zbox(z, k);
-      const auto* F = fin[z & 1];
+      const int zsb = zbox(z, k), r0 = kB3S * zsb;
+      const auto* F = fin[fsl(z)];
       // colour e is the left cell of the pairs of row jr (0-based) at plane z
       auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
+      // PHYS: a physical z face of this box (no push across it; its ghosts,
+      // both colours, once the second cell layer in from it is here)
+      const bool zlo = PHYS && (fl & 16) && zsb == 1, zhi = PHYS && (fl & 32) && zsb == len;
       // push1 == 0: only the colour-e cells go to the neighbours' ghosts (the
       // caller's next kernel forms the other colour's ghosts itself)
       // the pairs: interior of both colours, and the z faces of the boxes
@@ -240,10 +310,11 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
           b3_st(rse, o, F[q][2]);
           b3_st(rso, o, F[q][3]);
         }
-        if (k == 1 || k == B3NC) {
-          const bool lf = leftv(jr);
-          const double vl = lf ? ve : vo, vr = lf ? vo : ve;
-          const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
+        const bool lf = leftv(jr);
+        const double vl = lf ? ve : vo, vr = lf ? vo : ve;
+        const int il = 2 * ih + 1;
+        if ((k == 1 && !zlo) || (k == B3NC && !zhi)) {
+          const int nb = k == 1 ? 6 : 5;
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
           if (push1 || lf) b3_st(dst, g + 8u * b3_gh(nb, il, j), vl);
           if (push1 || !lf) b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), vr);
@@ -253,6 +324,27 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
           }
         }
       }
+      if (PHYS && ((zlo && k == 2) || (zhi && k == B3NC))) {
+        // the ghosts of face 5 (6) from planes 1, 2 (16, 15): this plane and
+        // the one before, in which the pair's colours are swapped
+        const int f = k == 2 ? 4 : 5;
+        const auto* F0 = fin[fsl(z - 1)];
+#pragma unroll 1
+        for (int r = 0; r < B3NC * B3CP / 64; r++) {
+          const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
+          const int xs = 1 + pc / B3H, ih = pc % B3H, j = jr + 1, il = 2 * ih + 1;
+          const bool lf = leftv(jr);
+          const double vl = F[q][lf ? 0 : 1], vr = F[q][lf ? 1 : 0];
+          const double pl0 = F0[q][lf ? 1 : 0], pr0 = F0[q][lf ? 0 : 1];
+          const double gl = k == 2 ? b3_bc(pk[f], pk[6 + f], pk[12 + f], pl0, vl)
+                                   : b3_bc(pk[f], pk[6 + f], pk[12 + f], vl, pl0);
+          const double gr = k == 2 ? b3_bc(pk[f], pk[6 + f], pk[12 + f], pr0, vr)
+                                   : b3_bc(pk[f], pk[6 + f], pk[12 + f], vr, pr0);
+          const unsigned g = bo[r0 + xs + B3XS];
+          b3_st(dst, g + 8u * b3_gh(f + 1, il, j), gl);
+          b3_st(dst, g + 8u * b3_gh(f + 1, il + 1, j), gr);
+        }
+      }
       // x faces: per row the cells x = 0, 15, 16, 31 (lane: row l/4, which l%4)
       {
         const int jr = l >> 2, w = l & 3, j = jr + 1;
@@ -260,10 +352,17 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const int xs = 1 + pc / B3H;
         const bool lf = leftv(jr), wantl = (w & 1) == 0;   // x = 0, 16: a left cell; 15, 31: right
         const int s = (wantl == lf) ? 0 : 1;
-        const double v = fin[z & 1][jr * B3CP + pc][s];
-        const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
-        if (push1 || wantl == lf) b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
-        if (RES) b3_st(rsb, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), fin[z & 1][jr * B3CP + pc][2 + s]);
+        const double v = fin[fsl(z)][jr * B3CP + pc][s];
+        if (PHYS && ((w == 0 && (fl & 1)) || (w == 3 && (fl & 2)))) {
+          // x = 0 / 31 next to a physical face: its ghost, from it and x = 1 / 30
+          const int f = w == 0 ? 0 : 1;
+          const double v2 = fin[fsl(z)][jr * B3CP + pc][1 - s];
+          b3_st(dst, bo[r0 + xs + B3XS] + 8u * b3_gh(f + 1, j, k), b3_bc(pk[f], pk[6 + f], pk[12 + f], v, v2));
+        } else {
+          const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
+          if (push1 || wantl == lf) b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+          if (RES) b3_st(rsb, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), fin[fsl(z)][jr * B3CP + pc][2 + s]);
+        }
       }
       // y faces: the cells of rows j = 1 (lanes 0..31) and j = 16 (32..63)
       {
@@ -271,10 +370,18 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
         const int pc = x >> 1, xs = 1 + pc / B3H, i = x - B3NC * (xs - 1) + 1;
         const bool lf = leftv(jr), isl = (x & 1) == 0;
         const int s = (isl == lf) ? 0 : 1;
-        const double v = fin[z & 1][jr * B3CP + pc][s];
-        const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
-        if (push1 || isl == lf) b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
-        if (RES) b3_st(rsb, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), fin[z & 1][jr * B3CP + pc][2 + s]);
+        const double v = fin[fsl(z)][jr * B3CP + pc][s];
+        if (PHYS && ((jr == 0 && (fl & 4)) || (jr == B3NC - 1 && (fl & 8)))) {
+          // rows 1 / 16 next to a physical face: the ghost from the row and the
+          // one behind it (the same x, the other colour)
+          const int f = jr == 0 ? 2 : 3, jr2 = jr == 0 ? 1 : B3NC - 2;
+          const double v2 = fin[fsl(z)][jr2 * B3CP + pc][1 - s];
+          b3_st(dst, bo[r0 + xs + B3XS] + 8u * b3_gh(f + 1, i, k), b3_bc(pk[f], pk[6 + f], pk[12 + f], v, v2));
+        } else {
+          const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
+          if (push1 || isl == lf) b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+          if (RES) b3_st(rsb, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), fin[fsl(z)][jr * B3CP + pc][2 + s]);
+        }
       }
     };
     // PRO: res of the column's own coarse cells, plane cs in steps 2cs (rows
@@ -342,11 +449,19 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // plane t: colour 1-e of phi, both colours of rhs (no branch: the waits
   // for these loads are counted; planes past the end reload the last one);
   // RES: both colours of old at plane t-3 (final kB3Ahead steps later)
+  // PHYS: the thread's physical faces; planes -1 and zend across a physical z
+  // face load the ghost of face 5 / 6 of the column's first / last box
+  B3Face fc{};
+  if (PHYS) fc = b3_face(fl, p, B3NPX, y, ih, j, e, xyb, PB);
+  const unsigned zql = 8u * (2 * B3HV + 4 * B3FS + (1 - e) * B3FH - (1 - e) * B3HV), zqh = zql + 8u * B3FS;
   auto load = [&](int t, double& q, double& fe, double& fo, double& he, double& ho) {
     int k;
     const int zs = zbox(min(t, zend + 2), k);
     const unsigned po = PB * (k - 1);
-    q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    if (!PHYS) q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    else if ((fl & 16) && t == -1) q = b3_ld(src, bo[kB3S + slot] + zql + xyb);
+    else if ((fl & 32) && t == zend) q = b3_ld(src, bo[kB3S * len + slot] + zqh + xyb);
+    else q = b3_ld(src, bo[kB3S * zs + slot] + fc.xyq + fc.kq * (k - 1));
     fe = b3_ld(rhe, bo[kB3S * zs + sle] + xye + po);
     fo = b3_ld(rho, bo[kB3S * zs + slo] + xyo + po);
     if (RES) {
@@ -405,24 +520,28 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     const double* P2 = pl[t & 1][2];
     // the active cells are the pair's left ones (x0) when colour e is there
     // at plane t-1; the neighbour pair across is on that side
-    const int far = ((y + t) & 1) == e ? li - 1 : li + 1;
+    const bool lft = ((y + t) & 1) == e;
+    const int far = lft ? li - 1 : li + 1;
     Nbr7 n;
     n.c = 0.0;
     // substep 1 (colour e) at plane t-1
     n.xm = P0[far]; n.xp = ob;
     n.ym = P0[li - B3LP]; n.yp = P0[li + B3LP]; n.zm = oa; n.zp = ot;
     const double s1 = gs_value<OP>(K, n, re1);
-    // substep 2 (colour 1-e) at plane t-2
+    // substep 2 (colour 1-e) at plane t-2 (PHYS: the ghosts across physical
+    // faces from the cell's value before it, stage 0's, as in k_gsrb4)
     n.xm = P1[far]; n.xp = eb;
     n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
+    if (PHYS) b3_fix(n, fc, pk, fl, lft, oa, t - 2, zend);
     const double s2 = gs_value<OP>(K, n, ro2);
     // substep 3 (colour e) at plane t-3
     n.xm = P2[far]; n.xp = wb;
     n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
+    if (PHYS) b3_fix(n, fc, pk, fl, lft, ea, t - 3, zend);
     const double s3 = gs_value<OP>(K, n, re3);
     // plane t-3 is final (colour e = s3, colour 1-e = wb): to the store wave
     if (ctr) {
-      double* F = fin[(t - 3) & 1][fi];
+      double* F = fin[fsl(t - 3)][fi];
       F[0] = s3;
       F[1] = wb;
       if (RES) {
@@ -492,29 +611,39 @@ constexpr int B4CX = kB3TX * B3H + 2 * B4CO, B4CY = B3H + 2 * B4CO, B4CT = B4CX 
 constexpr int B4CL = (B4CT + 63) / 64;   // coarse cells per lane of the loader wave
 constexpr int b4_threads(int pro) { return pro ? B4BS + 64 : B4BS; }
 
-template <int OP, int PRO>
+template <int OP, int PRO, bool PHYS>
 __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* __restrict__ dst,
                                                const int* __restrict__ cols, double lambda, int e,
                                                const double* __restrict__ shift, LevelView C,
-                                               const int* __restrict__ ccols, double fac) {
+                                               const int* __restrict__ ccols, double fac, B3Phys P) {
   static_assert(PRO == 0 || PRO == 2, "k_gsrb4: plain or the correction from a stored coarse res");
+  static_assert(!(PRO && PHYS), "k_gsrb4: physical faces in the plain form only");
   __shared__ double pl[2][4][B4PL];
-  __shared__ double fin[2][B3NC * B3CP][2];   // final plane: [row * B3CP + pair][colour e, 1-e]
+  // final plane: [row * B3CP + pair][colour e, 1-e] (PHYS: a ring of three, the
+  // z ghosts read the plane before)
+  __shared__ double fin[PHYS ? 3 : 2][B3NC * B3CP][2];
+  auto fsl = [](int z) { return PHYS ? (z + 12) % 3 : z & 1; };
   __shared__ unsigned bo[kB3Rec];
   __shared__ double rc[PRO ? 4 : 1][PRO ? B4CT : 1];   // coarse res, plane c in rc[c & 3]
   __shared__ unsigned cbo[PRO ? kB3CSlots : 1];        // the coarse record, byte offsets
-  __shared__ int len_s, cyo_s;
+  __shared__ int len_s, cyo_s, fl_s;
+  __shared__ double pk[PHYS ? 18 : 1];
   const int tid = threadIdx.x;
   const int cq = xcd_box(blockIdx.x, gridDim.x);
   constexpr int BS = b4_threads(PRO);
+  if (PHYS && tid >= BS - 18) pk[tid - (BS - 18)] = (&P.k[0])[tid - (BS - 18)];
   // planes of loads in flight: the correction form 2 (its registers)
   constexpr int AH = PRO ? 2 : kB3Ahead;
   // steps of every wave's loop: planes -4-AH .. zend+4 in blocks of AH
   const int t0 = -4 - AH;
   for (int q = tid; q < kB3Rec; q += BS) {
     const int v = cols[(long long)cq * kB3Rec + q];
-    if (q == 0) len_s = v;
-    else bo[q - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+    if (q == 0) {
+      len_s = v & kB3LenMask;
+      fl_s = v >> 8;
+    } else {
+      bo[q - 1] = (unsigned)v * (unsigned)(L.stride * 8);
+    }
   }
   if (PRO) {
     for (int q = tid; q < 1 + kB3CSlots; q += BS) {
@@ -527,6 +656,7 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
   for (int q = tid; q < 2 * 4 * B4PL; q += BS) (&pl[0][0][0])[q] = 0.0;
   __syncthreads();
   const int len = len_s, zend = B3NC * len;
+  const int fl = PHYS ? fl_s : 0;
   constexpr unsigned PB = 8u * B3H * B3NC;
   auto zbox = [&](int t, int& k) {
     const int zs = t < 0 ? 0 : (t >= zend ? len + 1 : (t >> 4) + 1);
@@ -595,9 +725,12 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
       const int z = t - 5;
       if (z < 0 || z >= zend) return;
       int k;
-      const int r0 = kB3S * zbox(z, k);
-      const auto* F = fin[z & 1];
+      const int zsb = zbox(z, k), r0 = kB3S * zsb;
+      const auto* F = fin[fsl(z)];
       auto leftv = [&](int jr) { return ((jr + z + 1) & 1) == e; };
+      // PHYS: a physical z face of this box (no push across it; its ghosts
+      // once the second cell layer in from it is here)
+      const bool zlo = PHYS && (fl & 16) && zsb == 1, zhi = PHYS && (fl & 32) && zsb == len;
 #pragma unroll
       for (int r = 0; r < B3NC * B3CP / 64; r++) {
         const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
@@ -606,12 +739,34 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
         const double ve = F[q][0], vo = F[q][1];
         b3_st(dse, o, ve);
         b3_st(dso, o, vo);
-        if (k == 1 || k == B3NC) {
-          const bool lf = leftv(jr);
-          const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
+        const bool lf = leftv(jr);
+        const int il = 2 * ih + 1;
+        if ((k == 1 && !zlo) || (k == B3NC && !zhi)) {
+          const int nb = k == 1 ? 6 : 5;
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
           b3_st(dst, g + 8u * b3_gh(nb, il, j), lf ? ve : vo);
           b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), lf ? vo : ve);
+        }
+      }
+      if (PHYS && ((zlo && k == 2) || (zhi && k == B3NC))) {
+        // the ghosts of face 5 (6) from planes 1, 2 (16, 15): this plane and
+        // the one before, in which the pair's colours are swapped
+        const int f = k == 2 ? 4 : 5;
+        const auto* F0 = fin[fsl(z - 1)];
+#pragma unroll 1
+        for (int r = 0; r < B3NC * B3CP / 64; r++) {
+          const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
+          const int xs = 1 + pc / B3H, ih = pc % B3H, j = jr + 1, il = 2 * ih + 1;
+          const bool lf = leftv(jr);
+          const double vl = F[q][lf ? 0 : 1], vr = F[q][lf ? 1 : 0];
+          const double pl0 = F0[q][lf ? 1 : 0], pr0 = F0[q][lf ? 0 : 1];
+          const double gl = k == 2 ? b3_bc(pk[f], pk[6 + f], pk[12 + f], pl0, vl)
+                                   : b3_bc(pk[f], pk[6 + f], pk[12 + f], vl, pl0);
+          const double gr = k == 2 ? b3_bc(pk[f], pk[6 + f], pk[12 + f], pr0, vr)
+                                   : b3_bc(pk[f], pk[6 + f], pk[12 + f], vr, pr0);
+          const unsigned g = bo[r0 + xs + B3XS];
+          b3_st(dst, g + 8u * b3_gh(f + 1, il, j), gl);
+          b3_st(dst, g + 8u * b3_gh(f + 1, il + 1, j), gr);
         }
       }
       {
@@ -619,17 +774,34 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
         const int pc = w == 0 ? 0 : (w == 1 ? B3H - 1 : (w == 2 ? B3H : 2 * B3H - 1));
         const int xs = 1 + pc / B3H;
         const bool lf = leftv(jr), wantl = (w & 1) == 0;
-        const double v = fin[z & 1][jr * B3CP + pc][(wantl == lf) ? 0 : 1];
-        const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
-        b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+        const int s = (wantl == lf) ? 0 : 1;
+        const double v = fin[fsl(z)][jr * B3CP + pc][s];
+        if (PHYS && ((w == 0 && (fl & 1)) || (w == 3 && (fl & 2)))) {
+          // x = 0 / 31 next to a physical face: its ghost, from it and x = 1 / 30
+          const int f = w == 0 ? 0 : 1;
+          const double v2 = fin[fsl(z)][jr * B3CP + pc][1 - s];
+          b3_st(dst, bo[r0 + xs + B3XS] + 8u * b3_gh(f + 1, j, k), b3_bc(pk[f], pk[6 + f], pk[12 + f], v, v2));
+        } else {
+          const int nxs = wantl ? xs - 1 : xs + 1, nb = wantl ? 2 : 1;
+          b3_st(dst, bo[r0 + nxs + B3XS] + 8u * b3_gh(nb, j, k), v);
+        }
       }
       {
         const int jr = l < 32 ? 0 : B3NC - 1, x = l & 31;
         const int pc = x >> 1, xs = 1 + pc / B3H, i = x - B3NC * (xs - 1) + 1;
         const bool lf = leftv(jr), isl = (x & 1) == 0;
-        const double v = fin[z & 1][jr * B3CP + pc][(isl == lf) ? 0 : 1];
-        const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
-        b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+        const int s = (isl == lf) ? 0 : 1;
+        const double v = fin[fsl(z)][jr * B3CP + pc][s];
+        if (PHYS && ((jr == 0 && (fl & 4)) || (jr == B3NC - 1 && (fl & 8)))) {
+          // rows 1 / 16 next to a physical face: the ghost from the row and the
+          // one behind it (the same x, the other colour)
+          const int f = jr == 0 ? 2 : 3, jr2 = jr == 0 ? 1 : B3NC - 2;
+          const double v2 = fin[fsl(z)][jr2 * B3CP + pc][1 - s];
+          b3_st(dst, bo[r0 + xs + B3XS] + 8u * b3_gh(f + 1, i, k), b3_bc(pk[f], pk[6 + f], pk[12 + f], v, v2));
+        } else {
+          const int nys = jr == 0 ? 0 : 2, nb = jr == 0 ? 4 : 3;
+          b3_st(dst, bo[r0 + xs + B3XS * nys] + 8u * b3_gh(nb, i, k), v);
+        }
       }
     };
     for (int t = t0; t <= zend + 4; t += AH) {
@@ -668,11 +840,19 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
   const bool ndo = act && p >= 1 && p <= B3NPX - 2 && y >= -2 && y <= B3NC + 1;
   const int sle = nde ? slot : 1 + B3XS, slo = ndo ? slot : 1 + B3XS;
   const unsigned xye = nde ? xyb : 0u, xyo = ndo ? xyb : 0u;
+  // PHYS: the thread's physical faces; planes -1 and zend across a physical z
+  // face load the ghost of face 5 / 6 of the column's first / last box
+  B3Face fc{};
+  if (PHYS) fc = b3_face(fl, p, B3NPX, y, ih, j, e, xyb, PB);
+  const unsigned zql = 8u * (2 * B3HV + 4 * B3FS + (1 - e) * B3FH - (1 - e) * B3HV), zqh = zql + 8u * B3FS;
   auto load = [&](int t, double& q, double& fe, double& fo) {
     int k;
     const int zs = zbox(min(t, zend + 3), k);
     const unsigned po = PB * (k - 1);
-    q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    if (!PHYS) q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);
+    else if ((fl & 16) && t == -1) q = b3_ld(src, bo[kB3S + slot] + zql + xyb);
+    else if ((fl & 32) && t == zend) q = b3_ld(src, bo[kB3S * len + slot] + zqh + xyb);
+    else q = b3_ld(src, bo[kB3S * zs + slot] + fc.xyq + fc.kq * (k - 1));
     fe = b3_ld(rhe, bo[kB3S * zs + sle] + xye + po);
     fo = b3_ld(rho, bo[kB3S * zs + slo] + xyo + po);
   };
@@ -702,24 +882,30 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
     const double* P1 = pl[t & 1][1];
     const double* P2 = pl[t & 1][2];
     const double* P3 = pl[t & 1][3];
-    const int far = ((y + t) & 1) == e ? li - 1 : li + 1;
+    const bool lft = ((y + t) & 1) == e;
+    const int far = lft ? li - 1 : li + 1;
     Nbr7 n;
     n.c = 0.0;
     n.xm = P0[far]; n.xp = ob;
     n.ym = P0[li - B3LP]; n.yp = P0[li + B3LP]; n.zm = oa; n.zp = ot;
     const double s1 = gs_value<OP>(K, n, re1);
+    // (PHYS: substeps 2-4 form the ghosts across physical faces; the cell's
+    // value before substep s is stage s-2's)
     n.xm = P1[far]; n.xp = eb;
     n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
+    if (PHYS) b3_fix(n, fc, pk, fl, lft, oa, t - 2, zend);
     const double s2 = gs_value<OP>(K, n, ro2);
     n.xm = P2[far]; n.xp = wb;
     n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
+    if (PHYS) b3_fix(n, fc, pk, fl, lft, ea, t - 3, zend);
     const double s3 = gs_value<OP>(K, n, re3);
     n.xm = P3[far]; n.xp = xb;
     n.ym = P3[li - B3LP]; n.yp = P3[li + B3LP]; n.zm = xa; n.zp = s3;
+    if (PHYS) b3_fix(n, fc, pk, fl, lft, wa, t - 4, zend);
     const double s4 = gs_value<OP>(K, n, ro4);
     // plane t-4 is final (colour e = stage 3 of the last iteration, 1-e = s4)
     if (ctr) {
-      double* F = fin[(t - 4) & 1][fi];
+      double* F = fin[fsl(t - 4)][fi];
       F[0] = xb;
       F[1] = s4;
     }
@@ -756,27 +942,36 @@ static double op_fac(const LevelView& L, int op, double lambda) {
 }
 
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
-                  const double* shift, hipStream_t st, const LevelView* coarse, const int* ccols) {
+                  const double* shift, hipStream_t st, const LevelView* coarse, const int* ccols,
+                  const B3Phys* phys) {
   const double fac = op_fac(L, op, lambda);
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb4: box size must be 16");
   if (coarse && (coarse->nc != B3NC || !ccols || shift))
     throw std::runtime_error("launch_gsrb4: the correction form needs a 16^3 coarse level, its records, no shift");
+  if (phys && (coarse || shift))
+    throw std::runtime_error("launch_gsrb4: physical faces in the plain form without a shift only");
   const LevelView& C = coarse ? *coarse : L;
+  const B3Phys P = phys ? *phys : B3Phys{};
+#define OMG_B4(OPV, PMV, PHV, BS) \
+  k_gsrb4<OPV, PMV, PHV><<<n_cols, BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac, P)
   if (op == OP_HELM) {
-    if (coarse) k_gsrb4<OP_HELM, 2><<<n_cols, b4_threads(2), 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
-    else k_gsrb4<OP_HELM, 0><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+    if (coarse) OMG_B4(OP_HELM, 2, false, b4_threads(2));
+    else if (phys) OMG_B4(OP_HELM, 0, true, B4BS);
+    else OMG_B4(OP_HELM, 0, false, B4BS);
   } else {
-    if (coarse) k_gsrb4<OP_LPL, 2><<<n_cols, b4_threads(2), 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
-    else k_gsrb4<OP_LPL, 0><<<n_cols, B4BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac);
+    if (coarse) OMG_B4(OP_LPL, 2, false, b4_threads(2));
+    else if (phys) OMG_B4(OP_LPL, 0, true, B4BS);
+    else OMG_B4(OP_LPL, 0, false, B4BS);
   }
+#undef OMG_B4
 }
 
 bool gsrb3_op_ok(int op) { return op == OP_LPL || op == OP_HELM; }
 
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, bool push1, const LevelView* coarse, const int* ccols,
-                  int coarse_mode, bool res) {
+                  int coarse_mode, bool res, const B3Phys* phys) {
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb3: box size must be 16");
   const int p1 = push1 ? 1 : 0;
@@ -785,17 +980,23 @@ void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, 
     throw std::runtime_error("launch_gsrb3: the correction form needs a 16^3 coarse level, its records, no shift");
   if (res && (pm || !push1))
     throw std::runtime_error("launch_gsrb3: res = phi - old only on a plain pass that pushes both colours");
+  if (phys && (pm || res || shift))
+    throw std::runtime_error("launch_gsrb3: physical faces in the plain form without a shift only");
   const LevelView& C = coarse ? *coarse : L;
-#define OMG_B3(OPV, PMV, RV) k_gsrb3<OPV, PMV, RV><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, C, ccols)
+  const B3Phys P = phys ? *phys : B3Phys{};
+#define OMG_B3(OPV, PMV, RV, PHV) \
+  k_gsrb3<OPV, PMV, RV, PHV><<<n_cols, B3BS, 0, st>>>(L, dst, cols, lambda, e, shift, p1, C, ccols, P)
   const bool helm = op == OP_HELM;
   if (pm == 1) {
-    if (helm) OMG_B3(OP_HELM, 1, false); else OMG_B3(OP_LPL, 1, false);
+    if (helm) OMG_B3(OP_HELM, 1, false, false); else OMG_B3(OP_LPL, 1, false, false);
   } else if (pm == 2) {
-    if (helm) OMG_B3(OP_HELM, 2, false); else OMG_B3(OP_LPL, 2, false);
+    if (helm) OMG_B3(OP_HELM, 2, false, false); else OMG_B3(OP_LPL, 2, false, false);
   } else if (res) {
-    if (helm) OMG_B3(OP_HELM, 0, true); else OMG_B3(OP_LPL, 0, true);
+    if (helm) OMG_B3(OP_HELM, 0, true, false); else OMG_B3(OP_LPL, 0, true, false);
+  } else if (phys) {
+    if (helm) OMG_B3(OP_HELM, 0, false, true); else OMG_B3(OP_LPL, 0, false, true);
   } else {
-    if (helm) OMG_B3(OP_HELM, 0, false); else OMG_B3(OP_LPL, 0, false);
+    if (helm) OMG_B3(OP_HELM, 0, false, false); else OMG_B3(OP_LPL, 0, false, false);
   }
 #undef OMG_B3
 }

@@ -272,4 +272,28 @@ __device__ __forceinline__ void face_cell_fill(const LevelView& L, int iv, int b
   }
 }
 
+// The ghost fill of a 1^3 box (nc == 1), one thread: face_cell_fill's work in
+// the reference's order.  In a box of one cell the second cell behind a face
+// (bc_to_gc's x2, m_ghost_cells.f90:682-766) is the opposite face's ghost, and
+// set_ghost_cells fills faces 1..6 in turn (m_ghost_cells.f90:232-285): the
+// low face of a dimension reads the high ghost as it was before the fill, the
+// high face the low ghost it just set.  So the box sets its own ghosts in that
+// order, same-GPU faces by reading the neighbour's cell (no thread writes
+// another box's ghosts).  A remote neighbour's ghost arrives by the unpack
+// after the kernel, as with the other box sizes (a continuous high face behind
+// a remote low face then reads the ghost of the fill before: not in any
+// configuration here, levels of 1^3 boxes are coarse and on one rank).
+__device__ __forceinline__ void box1_fill(const LevelView& L, int iv, int b, const LevelView& C, const RBRec* rb,
+                                          const GcBC& bc, double* sendbuf) {
+  double* u = boxp(L, iv, b);
+  for (int nb = 1; nb <= 6; nb++) {
+    const long long f = (long long)b * 6 + nb - 1;
+    const int kind = L.nbk[f], arg = L.nba[f];
+    if (kind == NB_LOCAL)
+      u[off_gh(L, nb, 1, 1)] = boxp(L, iv, arg)[off_int(L, 1, 1, 1)];
+    else
+      face_cell_fill(L, iv, b, nb, 1, 1, 3, C, rb, bc, sendbuf);
+  }
+}
+
 }  // namespace omg

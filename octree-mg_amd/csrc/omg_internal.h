@@ -191,6 +191,9 @@ struct Level {
   int* d_b3 = nullptr;
   int n_b3 = 0;
   std::vector<int> h_b3;   // (host copy, for the coarse records below)
+  // some columns have physical faces (round 6): the passes take the ghosts
+  // there from constant boundary values (b3_phys, omg_api.cpp)
+  bool b3_phys = false;
   // k_gsrb3's correct_children form: per column the coarse boxes around it
   // (launch_gsrb3's ccols); null: the level's up-smoothing starts with
   // k_prolong_smooth
@@ -344,12 +347,15 @@ struct omg_ctx {
   bool no_fuse_down_bc = false;        // OMG_NO_FUSE_DOWN_BC: no fused down-step on levels with physical / rb faces
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
+  bool no_block3_phys = false;         // OMG_NO_BLOCK3_PHYS: no block passes on levels with physical faces
   bool no_deep = false;                // OMG_NO_DEEP: split levels keep one substep per launch (no deep halo)
   bool no_block3p = false;             // OMG_NO_BLOCK3P: correct_children by k_prolong_smooth, not k_gsrb3
   bool block4 = true;                  // the down-smoothing as k_gsrb4 + the unfused residual (OMG_NO_BLOCK4: off)
   bool no_block4p = false;             // OMG_NO_BLOCK4P: the up-smoothing's correction form with three substeps (k_gsrb3)
+  bool block4_phys = false;            // OMG_BLOCK4_PHYS: k_gsrb4 also on levels with physical faces (A/B)
   bool no_block3r = false;             // OMG_NO_BLOCK3R: no res from the coarse level's last pass (k_gsrb3 forms phi - old)
   int b3_min_boxes = omg::kB3MinBoxes;  // smallest level for k_gsrb3 (OMG_BLOCK3_MIN_BOXES, tests)
+  int b3_col_small = 2;                // column length on levels below kB3MinBoxes (OMG_BLOCK3_SMALL_COL)
   int b3_col = 0;                      // k_gsrb3 column length (0: by level size; OMG_BLOCK3_COLUMN, tests)
   bool rhs_cache_valid = false;        // red acc of rhs is the sum of the current rhs
   bool phi_shift_pending = false;      // some level has shift_pending

@@ -57,6 +57,16 @@ constexpr int kB3S = 3 * (kB3TX + 2);            // record slots per z slot
 constexpr int kB3MaxZ = 16;                      // boxes per column in z (at most)
 constexpr int kB3Rec = (1 + kB3S * (kB3MaxZ + 2) + 15) / 16 * 16;
 bool gsrb3_op_ok(int op);
+// Physical faces (round 6): [0] also holds the column's physical faces,
+// len | flags << 8 (bit f: face f+1 of the column, x-, x+, y-, y+ of its
+// boxes, z- of its first, z+ of its last); a slot across such a face names
+// the box whose face it is.  The ghost there is bc_to_gc's
+// (m_ghost_cells.f90:665-766) c0 * b + c1 * x1 + c2 * x2 with constant b per
+// face: k = c0 * b (formed on the host, the same product), c1, c2.
+constexpr int kB3LenMask = 255;
+struct B3Phys {
+  double k[6], c1[6], c2[6];
+};
 // four substeps (colours e, 1-e, e, 1-e) per pass, same columns (k_gsrb4,
 // omg_block.hip): the down-smoothing of a level whose residual + restriction
 // then runs unfused (the default; OMG_NO_BLOCK4)
@@ -65,7 +75,7 @@ bool gsrb3_op_ok(int op);
 // (k_gsrb3's coarse_mode 2; ccols as for launch_gsrb3)
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, const LevelView* coarse = nullptr,
-                  const int* ccols = nullptr);
+                  const int* ccols = nullptr, const B3Phys* phys = nullptr);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
 // halves are left stale: only for a pass that k_smooth_resid follows, which
 // reads colour e's and forms colour 1-e's itself)
@@ -87,7 +97,8 @@ constexpr int kB3CSlots = 9 * (kB3MaxZ / 2 + 2);                // coarse boxes 
 constexpr int kB3CRec = (1 + kB3CSlots + 15) / 16 * 16;
 void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, bool push1 = true, const LevelView* coarse = nullptr,
-                  const int* ccols = nullptr, int coarse_mode = 1, bool res = false);
+                  const int* ccols = nullptr, int coarse_mode = 1, bool res = false,
+                  const B3Phys* phys = nullptr);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,

@@ -32,6 +32,10 @@ static inline unsigned grid_for(long long work, int block = 256) {
 __global__ void __launch_bounds__(256) k_fill_gc(LevelView L, int iv, int colours, LevelView C,
                                                  const RBRec* rb, GcBC bc, double* sendbuf) {
   const int nc = L.nc, nc2 = nc * nc;
+  if (nc == 1) {   // (the reference's face order, box1_fill)
+    GRID_STRIDE(b, (long long)L.n) box1_fill(L, iv, (int)b, C, rb, bc, sendbuf);
+    return;
+  }
   GRID_STRIDE(t, (long long)L.n * 6 * nc2) {
     const int cell = (int)(t % nc2), f = (int)(t / nc2);
     face_cell_fill(L, iv, f / 6, f % 6 + 1, cell % nc + 1, cell / nc + 1, colours, C, rb, bc, sendbuf);
@@ -240,9 +244,21 @@ __global__ void __launch_bounds__(256) k_gs_sub(LevelView L, double lambda, int 
         u[o] = gs_value<OP>(K, s, f[o]);
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < 6 * nc * nc; p += blockDim.x) {
-      const int nb = p / (nc * nc) + 1, cell = p % (nc * nc);
-      face_cell_fill(L, 1, b, nb, cell % nc + 1, cell / nc + 1, colours, C, rb, bc, sendbuf);
+    if (nc == 1) {
+      // (the reference's face order, box1_fill; colours 0: odd box sizes push
+      // nothing and a full fill follows, which alone may set the ghosts, since
+      // a 1^3 box's physical ghosts read each other)
+      if (threadIdx.x == 0 && colours) {
+        box1_fill(L, 1, b, C, rb, bc, sendbuf);
+      } else if (threadIdx.x == 0) {   // (the remote faces still go out)
+        for (int nb = 1; nb <= 6; nb++)
+          if (L.nbk[(long long)b * 6 + nb - 1] == NB_REMOTE) face_cell_fill(L, 1, b, nb, 1, 1, 0, C, rb, bc, sendbuf);
+      }
+    } else {
+      for (int p = threadIdx.x; p < 6 * nc * nc; p += blockDim.x) {
+        const int nb = p / (nc * nc) + 1, cell = p % (nc * nc);
+        face_cell_fill(L, 1, b, nb, cell % nc + 1, cell / nc + 1, colours, C, rb, bc, sendbuf);
+      }
     }
     __syncthreads();
   }

@@ -1395,9 +1395,13 @@ __device__ void tail_fill(const TailArgs& A, int li) {
   const TailLevel& T = A.lv[li];
   const int nc = T.L.nc, nc2 = nc * nc;
   const LevelView none{};
-  for (int t = threadIdx.x; t < T.L.n * 6 * nc2; t += blockDim.x) {
-    const int cell = t % nc2, f = t / nc2;
-    face_cell_fill(T.L, 1, f / 6, f % 6 + 1, cell % nc + 1, cell / nc + 1, 3, none, nullptr, T.bc, nullptr);
+  if (nc == 1) {   // (the reference's face order, box1_fill)
+    for (int b = threadIdx.x; b < T.L.n; b += blockDim.x) box1_fill(T.L, 1, b, none, nullptr, T.bc, nullptr);
+  } else {
+    for (int t = threadIdx.x; t < T.L.n * 6 * nc2; t += blockDim.x) {
+      const int cell = t % nc2, f = t / nc2;
+      face_cell_fill(T.L, 1, f / 6, f % 6 + 1, cell % nc + 1, cell / nc + 1, 3, none, nullptr, T.bc, nullptr);
+    }
   }
   __syncthreads();
 }

@@ -24,7 +24,8 @@
 !     op       lpl | helm | vlpl | vhelm   (v*: coefficient eps in var 5, solution in 6)
 !              | ahelm (eps1..3 in vars 5..7, solution in 8; the dump holds rhs)
 !     bc       sol (callback Dirichlet u) | d0 (Dirichlet 0) | per (periodic)
-!              | n0 (Neumann 0) | c0 (continuous)
+!              | n0 (Neumann 0) | c0 (continuous) | mx1, mx2 (per-face types
+!              and constant values, tests/mgdriver.py MIXED_BC)
 !     rhs      sol (rhs = L u) | one (rhs = 1) | phi (phi = u incl. ghosts,
 !              rhs = 0: the initial state of a diffusion run)
 !     n_levels 1 = uniform, >1 = test_refinement's AMR tree
@@ -136,6 +137,15 @@ program omg_golden
   case ("c0")
      mg%bc(:, mg_iphi)%bc_type = mg_bc_continuous
      mg%bc(:, mg_iphi)%bc_value = 0.0_dp
+  case ("mx1")
+     ! per-face types and constant values (tests/mgdriver.py MIXED_BC)
+     mg%bc(:, mg_iphi)%bc_type = [mg_bc_dirichlet, mg_bc_dirichlet, mg_bc_neumann, &
+          mg_bc_neumann, mg_bc_continuous, mg_bc_continuous]
+     mg%bc(:, mg_iphi)%bc_value = [0.5_dp, -1.25_dp, 0.75_dp, -0.3_dp, 0.2_dp, 0.0_dp]
+  case ("mx2")
+     mg%bc(:, mg_iphi)%bc_type = [mg_bc_continuous, mg_bc_neumann, mg_bc_dirichlet, &
+          mg_bc_continuous, mg_bc_neumann, mg_bc_dirichlet]
+     mg%bc(:, mg_iphi)%bc_value = [0.0_dp, 1.5_dp, -0.625_dp, 0.0_dp, -2.0_dp, 0.125_dp]
   case default
      error stop "bad bc"
   end select

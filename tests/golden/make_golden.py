@@ -27,7 +27,7 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 # BIG: too large for the CPU oracle in the quick CPU suite (the device is
 # compared with the reference's numbers directly; tests/test_gpu_parity.py)
 BIG = {"c3_per512_box16", "c2_256_box16_gsrb_d0", "c2_256_box16_gs_d0", "c5_helm256_box16_gsrb_d0",
-       "per256_box16_helm_v", "per256_box16_gsrb_f"}
+       "per256_box16_helm_v", "per256_box16_gsrb_f", "mx1_256_box16"}
 CONFIGS = {
     # tests/test_uniform_grid 8 64 64 64 10 f, as shipped (GS)
     "c1_gs_v": ("8 64 64 64 10 v gs lpl 0 sol sol 1 lb 0", False, [1, 4]),
@@ -71,6 +71,15 @@ CONFIGS = {
     "c2_256_box16_gs_d0": ("16 256 256 256 3 v gs lpl 0 d0 sol 1 lb 0", True, [1]),
     # C5 at its own size: Helmholtz lambda = 10, 256^3, box 16
     "c5_helm256_box16_gsrb_d0": ("16 256 256 256 3 v gsrb helm 10 d0 sol 1 lb 1", True, [1]),
+    # per-face boundary types with nonzero constant values (omg_golden.f90 mx1 /
+    # mx2); at box 16 on non-cubic domains the finest level takes the block
+    # passes with physical faces (k_gsrb3) once their level bound is lowered
+    # (tests/test_gpu_block3.py), at 256^3 at the default bound
+    "mx1_box16_96x128x64": ("16 96 128 64 3 v gsrb lpl 0 mx1 sol 1 lb 0", True, [1, 2]),
+    "mx2_helm_box16_128x64x96": ("16 128 64 96 3 v gsrb helm 2 mx2 sol 1 lb 0", True, [1]),
+    "mx1_box8_gs": ("8 32 32 32 4 v gs lpl 0 mx1 sol 1 lb 0", True, [1]),
+    "mx2_box8_gsrb_f": ("8 32 32 32 3 f gsrb lpl 0 mx2 sol 1 lb 1", True, [1]),
+    "mx1_256_box16": ("16 256 256 256 3 v gsrb lpl 0 mx1 sol 1 lb 0", True, [1]),
     # C5: Helmholtz, lambda = 10
     "helm32_gsrb_v": ("8 32 32 32 8 v gsrb helm 10 sol sol 1 lb 1", True, [1]),
     "helm32_gsrb_n0": ("8 32 32 32 5 v gsrb helm 10 n0 sol 1 lb 0", True, [1, 2, 6]),

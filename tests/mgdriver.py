@@ -285,6 +285,15 @@ class DeviceBackend:
         return omg.diffusion_solve_acoeff(self.mg, dt, order, DIFF_TOL)
 
 
+# per face x-, x+, y-, y+, z-, z+: (type, constant value)
+MIXED_BC = {
+    "mx1": [(T.MG_BC_DIRICHLET, 0.5), (T.MG_BC_DIRICHLET, -1.25), (T.MG_BC_NEUMANN, 0.75),
+            (T.MG_BC_NEUMANN, -0.3), (T.MG_BC_CONTINUOUS, 0.2), (T.MG_BC_CONTINUOUS, 0.0)],
+    "mx2": [(T.MG_BC_CONTINUOUS, 0.0), (T.MG_BC_NEUMANN, 1.5), (T.MG_BC_DIRICHLET, -0.625),
+            (T.MG_BC_CONTINUOUS, 0.0), (T.MG_BC_NEUMANN, -2.0), (T.MG_BC_DIRICHLET, 0.125)],
+}
+
+
 def _apply_bc(cfg, tree, set_bc, set_faces):
     bc = cfg["bc"]
     if bc == "sol":
@@ -294,6 +303,11 @@ def _apply_bc(cfg, tree, set_bc, set_faces):
         t = {"d0": T.MG_BC_DIRICHLET, "n0": T.MG_BC_NEUMANN, "c0": T.MG_BC_CONTINUOUS}[bc]
         for nb in range(1, 7):
             set_bc(T.MG_IPHI, nb, t, 0.0)
+    elif bc in MIXED_BC:
+        # (not omg_golden's: per-face types and nonzero constant values, for
+        # the block passes' physical faces)
+        for nb, (t, v) in enumerate(MIXED_BC[bc], start=1):
+            set_bc(T.MG_IPHI, nb, t, v)
 
 
 def setup_problem(be):

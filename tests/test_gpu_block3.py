@@ -143,3 +143,68 @@ def test_block3_graph_failure_keeps_phi(monkeypatch, fail_at):
     for _ in range(3):
         assert dev.vcycle(True) == orc.vcycle(True)
         _assert_same(dev, orc)
+
+
+# Physical faces in the passes (round 6): a column with a
+# Dirichlet / Neumann / continuous face (bc_to_gc, m_ghost_cells.f90:665-766)
+# loads the ghosts there as they are on entry for its first substep and forms
+# them from the cells next to the face for the later ones; its store wave
+# writes them from the final cells.  Constant values: zero (omg_golden's d0 /
+# n0 / c0) and per-face types and nonzero values (mx1 / mx2).  Non-cubic
+# domains: columns shorter than the column length (both z faces physical in
+# one column at col8), x extents of 6 boxes.  The passes' launch counts show
+# that they ran on the finest level.
+PHYS_CASES = ["16 128 128 128 3 v gsrb lpl 0 d0 sol 1 lb 0",
+              "16 128 96 64 3 v gsrb helm 2 n0 sol 1 lb 0",
+              "16 128 128 128 3 v gsrb lpl 0 c0 sol 1 lb 0",
+              "16 96 128 64 3 v gsrb lpl 0 mx1 sol 1 lb 0",
+              "16 128 64 96 3 v gsrb helm 2 mx2 sol 1 lb 0"]
+
+
+def _block_launches(dev, lvl):
+    return {f: dev.mg.ctx.kernel_stats(f"{f}@{lvl}")[0] for f in ("smoother_gsrb3", "smoother_gsrb4")}
+
+
+@pytest.mark.parametrize("four", [False, True])
+@pytest.mark.parametrize("down,up", [(2, 2), (3, 1), (1, 3)])
+@pytest.mark.parametrize("args", PHYS_CASES)
+def test_block3_physical_faces_match_oracle(monkeypatch, args, down, up, four):
+    if four:
+        monkeypatch.setenv("OMG_BLOCK4_PHYS", "1")
+    dev, orc = _pair(args, down, up)
+    dev.mg.ctx.call("set_profiling", 1)
+    for _ in range(3):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc)
+    dev.mg.ctx.call("synchronize")
+    top = dev.tree.highest_lvl
+    n = _block_launches(dev, top)
+    if len(dev.my_ids(top)) >= int(__import__("os").environ["OMG_BLOCK3_MIN_BOXES"]):
+        assert n["smoother_gsrb3"] + n["smoother_gsrb4"] > 0, n
+        if four and down % 2 == 0:
+            assert n["smoother_gsrb4"] > 0, n
+
+
+@pytest.mark.parametrize("have_guess", [False, True])
+def test_block3_physical_faces_fmg_matches_oracle(have_guess):
+    dev, orc = _pair("16 128 128 128 2 f gsrb helm 2 mx1 sol 1 lb 0", 2, 2)
+    for _ in range(2):
+        assert dev.fmg(have_guess, True) == orc.fmg(have_guess, True)
+        _assert_same(dev, orc)
+
+
+def test_block3_physical_faces_switch_off_same_bits(monkeypatch):
+    """OMG_NO_BLOCK3_PHYS=1 (levels with physical faces take one substep per
+    launch) and the default give the same state after each cycle; an odd
+    number of boxes in x (5) declines the columns, the same bits again."""
+    for args in ("16 128 128 128 2 v gsrb lpl 0 mx2 sol 1 lb 0", "16 80 128 64 2 v gsrb lpl 0 mx1 sol 1 lb 0"):
+        monkeypatch.delenv("OMG_NO_BLOCK3_PHYS", raising=False)
+        dev, orc = _pair(args, 2, 2)
+        monkeypatch.setenv("OMG_NO_BLOCK3_PHYS", "1")
+        ref = DeviceBackend(parse(args))
+        ref.mg.n_cycle_down, ref.mg.n_cycle_up = 2, 2
+        ref.mg._push_methods()
+        setup_problem(ref)
+        for _ in range(2):
+            assert dev.vcycle(True) == ref.vcycle(True) == orc.vcycle(True)
+            _assert_same(dev, ref)

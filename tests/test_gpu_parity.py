@@ -67,6 +67,10 @@ OPS_CASES = [
     "8 32 32 32 1 v gsrb lpl 0 per sol 1 lb 0",
     "8 32 32 32 1 v gs lpl 0 c0 sol 3 lb 0",
     "4 24 16 8 1 v gsrb lpl 0 d0 sol 1 lb 0",
+    # per-face types with nonzero constant values (tests/mgdriver.py MIXED_BC)
+    "16 96 128 64 1 v gsrb lpl 0 mx1 sol 1 lb 0",
+    "8 32 32 32 1 v gs helm 3.5 mx2 sol 1 lb 0",
+    "16 64 64 64 1 v gsrb helm 2 mx2 sol 1 lb 0",
 ]
 
 

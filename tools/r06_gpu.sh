@@ -17,6 +17,17 @@ for s in "$@"; do
     c3multi) timeout -k 10 900 $PT tests/test_gpu_multirank.py -k c3_512 > ${O}_c3multi.log 2>&1; rc=$? ;;
     loop) { timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && \
             timeout -k 10 300 python tools/loopback_bench.py 2 512 5 && OMG_NO_DEEP=1 timeout -k 10 300 python tools/loopback_bench.py 2 512 5; } > ${O}_loop.log 2>&1; rc=$? ;;
+    mx) timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k mx > ${O}_mx.log 2>&1; rc=0 ;;
+    physnx) timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_block3.py -k physical > ${O}_physnx.log 2>&1; rc=0 ;;
+    phys) timeout -k 10 900 $PT tests/test_gpu_block3.py -k physical > ${O}_phys.log 2>&1; rc=$? ;;
+    cfgab) { for v in "" OMG_NO_BLOCK3_PHYS=1 OMG_BLOCK4_PHYS=1 "" OMG_NO_BLOCK3_PHYS=1 OMG_BLOCK4_PHYS=1; do
+               echo "== ${v:-default}"; env $v timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 C5-helm || exit 1; done; } > ${O}_cfgab.log 2>&1; rc=$? ;;
+    smallab) { for v in "" OMG_BLOCK3_MIN_BOXES=512 OMG_BLOCK3_MIN_BOXES=64 "OMG_BLOCK3_MIN_BOXES=512 OMG_BLOCK3_SMALL_COL=4" \
+                 "" OMG_BLOCK3_MIN_BOXES=512 OMG_BLOCK3_MIN_BOXES=64 "OMG_BLOCK3_MIN_BOXES=512 OMG_BLOCK3_SMALL_COL=4"; do
+               echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; } > ${O}_smallab.log 2>&1; rc=$? ;;
+    c2prof) for v in default OMG_NO_BLOCK3_PHYS; do
+              (cd /tmp && env $( [ $v = default ] || echo $v=1 ) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/${O}_c2prof_$v" -o run --output-format csv \
+                 -- python3 "$GRAFT_REPO_ROOT/tools/configs_bench.py" --no-cpu --only C2) >> ${O}_c2prof.log 2>&1 || { rc=1; break; }; rc=0; done ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
