@@ -114,14 +114,17 @@ __device__ __forceinline__ double b3_bc(double k, double c1, double c2, double x
 // when the thread's pair is next to face x- (x+) / y- (y+), whose ghost
 // then comes from the cell's own value before the substep and the one behind
 // it.  Everything else beyond a physical face is computed and never used.
-// (The faces' k, c1, c2 are read from LDS where used, pk = B3Phys as 18
-// doubles: in registers they cost a workgroup per CU.)
+// (k, c1, c2 of the thread's x and y faces are held in registers and every
+// substep forms both ghosts and selects them: in LDS, read in branches taken
+// by some lanes, the formation cost C2's 4096-box level 88 us a pass,
+// profiles/r06/s15_phys_variants.txt.)
 struct B3Face {
   unsigned xyq, kq;
   int bx, by;
+  double kx, c1x, c2x, ky, c1y, c2y;
 };
-__device__ __forceinline__ B3Face b3_face(int fl, int p, int npx, int y, int ih, int j, int e, unsigned xyb,
-                                          unsigned pb) {
+__device__ __forceinline__ B3Face b3_face(const B3Phys& P, int fl, int p, int npx, int y, int ih, int j, int e,
+                                          unsigned xyb, unsigned pb) {
   B3Face f;
   constexpr int HV = 8 * 16 * 16, FH = 8 * 16, FS = 2 * FH;
   f.xyq = xyb;
@@ -137,20 +140,24 @@ __device__ __forceinline__ B3Face b3_face(int fl, int p, int npx, int y, int ih,
   }
   f.bx = (fl & 1) && p == 2 ? 1 : ((fl & 2) && p == npx - 3 ? 2 : 0);
   f.by = (fl & 4) && y == 0 ? 1 : ((fl & 8) && y == 15 ? 2 : 0);
+  const bool hx = f.bx == 2, hy = f.by == 2;
+  f.kx = hx ? P.k[1] : P.k[0]; f.c1x = hx ? P.c1[1] : P.c1[0]; f.c2x = hx ? P.c2[1] : P.c2[0];
+  f.ky = hy ? P.k[3] : P.k[2]; f.c1y = hy ? P.c1[3] : P.c1[2]; f.c2y = hy ? P.c2[3] : P.c2[2];
   return f;
 }
 
 // the neighbours of a PHYS pass's update at plane ts across the column's
 // physical faces (own: the cell's value before the substep); lft: the pair's
 // active cell is its left one (n.xm is then the x- neighbour, else x+)
-__device__ __forceinline__ void b3_fix(Nbr7& n, const B3Face& f, const double* pk, int fl, bool lft, double own,
+__device__ __forceinline__ void b3_fix(Nbr7& n, const B3Face& f, const B3Phys& P, int fl, bool lft, double own,
                                        int ts, int zend) {
-  auto bc = [&](int q, double x2) { return b3_bc(pk[q], pk[6 + q], pk[12 + q], own, x2); };
-  if ((f.bx == 1 && lft) || (f.bx == 2 && !lft)) n.xm = bc(f.bx - 1, n.xp);
-  if (f.by == 1) n.ym = bc(2, n.yp);
-  else if (f.by == 2) n.yp = bc(3, n.ym);
-  if ((fl & 16) && ts == 0) n.zm = bc(4, n.zp);
-  if ((fl & 32) && ts == zend - 1) n.zp = bc(5, n.zm);
+  const double gx = b3_bc(f.kx, f.c1x, f.c2x, own, n.xp);
+  const double gy = b3_bc(f.ky, f.c1y, f.c2y, own, f.by == 2 ? n.ym : n.yp);
+  n.xm = ((f.bx == 1 && lft) || (f.bx == 2 && !lft)) ? gx : n.xm;
+  n.ym = f.by == 1 ? gy : n.ym;
+  n.yp = f.by == 2 ? gy : n.yp;
+  if ((fl & 16) && ts == 0) n.zm = b3_bc(P.k[4], P.c1[4], P.c2[4], own, n.zp);
+  if ((fl & 32) && ts == zend - 1) n.zp = b3_bc(P.k[5], P.c1[5], P.c2[5], own, n.zm);
 }
 
 }  // namespace
@@ -452,7 +459,7 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
   // PHYS: the thread's physical faces; planes -1 and zend across a physical z
   // face load the ghost of face 5 / 6 of the column's first / last box
   B3Face fc{};
-  if (PHYS) fc = b3_face(fl, p, B3NPX, y, ih, j, e, xyb, PB);
+  if (PHYS) fc = b3_face(P, fl, p, B3NPX, y, ih, j, e, xyb, PB);
   const unsigned zql = 8u * (2 * B3HV + 4 * B3FS + (1 - e) * B3FH - (1 - e) * B3HV), zqh = zql + 8u * B3FS;
   auto load = [&](int t, double& q, double& fe, double& fo, double& he, double& ho) {
     int k;
@@ -532,12 +539,12 @@ __global__ void __launch_bounds__(B3BS) k_gsrb3(LevelView L, double* __restrict_
     // faces from the cell's value before it, stage 0's, as in k_gsrb4)
     n.xm = P1[far]; n.xp = eb;
     n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
-    if (PHYS) b3_fix(n, fc, pk, fl, lft, oa, t - 2, zend);
+    if (PHYS) b3_fix(n, fc, P, fl, lft, oa, t - 2, zend);
     const double s2 = gs_value<OP>(K, n, ro2);
     // substep 3 (colour e) at plane t-3
     n.xm = P2[far]; n.xp = wb;
     n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
-    if (PHYS) b3_fix(n, fc, pk, fl, lft, ea, t - 3, zend);
+    if (PHYS) b3_fix(n, fc, P, fl, lft, ea, t - 3, zend);
     const double s3 = gs_value<OP>(K, n, re3);
     // plane t-3 is final (colour e = s3, colour 1-e = wb): to the store wave
     if (ctr) {
@@ -843,7 +850,7 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
   // PHYS: the thread's physical faces; planes -1 and zend across a physical z
   // face load the ghost of face 5 / 6 of the column's first / last box
   B3Face fc{};
-  if (PHYS) fc = b3_face(fl, p, B3NPX, y, ih, j, e, xyb, PB);
+  if (PHYS) fc = b3_face(P, fl, p, B3NPX, y, ih, j, e, xyb, PB);
   const unsigned zql = 8u * (2 * B3HV + 4 * B3FS + (1 - e) * B3FH - (1 - e) * B3HV), zqh = zql + 8u * B3FS;
   auto load = [&](int t, double& q, double& fe, double& fo) {
     int k;
@@ -893,15 +900,15 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
     // value before substep s is stage s-2's)
     n.xm = P1[far]; n.xp = eb;
     n.ym = P1[li - B3LP]; n.yp = P1[li + B3LP]; n.zm = ea; n.zp = s1;
-    if (PHYS) b3_fix(n, fc, pk, fl, lft, oa, t - 2, zend);
+    if (PHYS) b3_fix(n, fc, P, fl, lft, oa, t - 2, zend);
     const double s2 = gs_value<OP>(K, n, ro2);
     n.xm = P2[far]; n.xp = wb;
     n.ym = P2[li - B3LP]; n.yp = P2[li + B3LP]; n.zm = wa; n.zp = s2;
-    if (PHYS) b3_fix(n, fc, pk, fl, lft, ea, t - 3, zend);
+    if (PHYS) b3_fix(n, fc, P, fl, lft, ea, t - 3, zend);
     const double s3 = gs_value<OP>(K, n, re3);
     n.xm = P3[far]; n.xp = xb;
     n.ym = P3[li - B3LP]; n.yp = P3[li + B3LP]; n.zm = xa; n.zp = s3;
-    if (PHYS) b3_fix(n, fc, pk, fl, lft, wa, t - 4, zend);
+    if (PHYS) b3_fix(n, fc, P, fl, lft, wa, t - 4, zend);
     const double s4 = gs_value<OP>(K, n, ro4);
     // plane t-4 is final (colour e = stage 3 of the last iteration, 1-e = s4)
     if (ctr) {

@@ -28,6 +28,9 @@ for s in "$@"; do
     c2prof) for v in default OMG_NO_BLOCK3_PHYS; do
               (cd /tmp && env $( [ $v = default ] || echo $v=1 ) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/${O}_c2prof_$v" -o run --output-format csv \
                  -- python3 "$GRAFT_REPO_ROOT/tools/configs_bench.py" --no-cpu --only C2) >> ${O}_c2prof.log 2>&1 || { rc=1; break; }; rc=0; done ;;
+    phvar) { for r in 1 2; do for v in ${PHV:-default phnofix phnostore phnoload}; do
+               echo "== $v"; if [ $v = default ]; then L=; else L=OMG_LIB=$PWD/octree-mg_amd/_variants/libomg_$v.so; fi
+               env $L timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 || exit 1; done; done; } > ${O}_phvar.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;

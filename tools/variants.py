@@ -30,6 +30,14 @@ VARIANTS = {
     "sumslpw16": [("omg_tiles.hip", "constexpr int kSumsLPW = 32, kSumsR = 4;", "constexpr int kSumsLPW = 16, kSumsR = 4;")],
     "sumsr8": [("omg_tiles.hip", "constexpr int kSumsLPW = 32, kSumsR = 4;", "constexpr int kSumsLPW = 32, kSumsR = 8;")],
     "sumsr2": [("omg_tiles.hip", "constexpr int kSumsLPW = 32, kSumsR = 4;", "constexpr int kSumsLPW = 32, kSumsR = 2;")],
+    # physical faces in the block passes (r06; timing only, not parity-correct):
+    # no ghost formed in substeps 2-4 / no physical work in the store wave /
+    # the plain load
+    "phnofix": [("omg_block.hip", "if (PHYS) b3_fix(", "if (false) b3_fix(")] * 5,
+    "phnostore": [("omg_block.hip", "if (PHYS && ((zlo && k == 2) || (zhi && k == B3NC))) {", "if (false) {"),
+                  ("omg_block.hip", "if (PHYS && ((w == 0 && (fl & 1)) || (w == 3 && (fl & 2)))) {", "if (false) {"),
+                  ("omg_block.hip", "if (PHYS && ((jr == 0 && (fl & 4)) || (jr == B3NC - 1 && (fl & 8)))) {", "if (false) {")] * 2,
+    "phnoload": [("omg_block.hip", "    if (!PHYS) q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);", "    if (true) q = b3_ld(src, bo[kB3S * zs + slot] + xyb + po);")] * 2,
 }
 
 
@@ -43,7 +51,7 @@ def build(name):
         p = os.path.join(d, f)
         s = open(p).read()
         assert a in s, (name, a)
-        open(p, "w").write(s.replace(a, b))
+        open(p, "w").write(s.replace(a, b, 1))
     out = os.path.join(R, "octree-mg_amd", "_variants", f"libomg_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     for o in os.listdir(d):
