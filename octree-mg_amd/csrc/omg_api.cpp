@@ -555,11 +555,11 @@ void rb_stale_above(omg_ctx* c, int lvl) {
 }
 // phi was written on a level: its ghost faces may no longer match a fill
 void phi_dirty(omg_ctx* c, int lvl) {
-  if (Level* L = level_ptr(c, lvl)) L->phi_gc_ok = false;
+  if (Level* L = level_ptr(c, lvl)) L->phi_gc_ok = L->gc_deferred = false;
   rb_stale_above(c, lvl);
 }
 void phi_dirty_all(omg_ctx* c) {
-  for (auto& kv : c->levels) kv.second.phi_gc_ok = kv.second.rbgv_ok = false;
+  for (auto& kv : c->levels) kv.second.phi_gc_ok = kv.second.rbgv_ok = kv.second.gc_deferred = false;
 }
 
 // Refinement-boundary faces whose ghosts a host callback sets instead of
@@ -690,6 +690,7 @@ void fill_gc_lvl(omg_ctx* c, int lvl, int iv) {
   if (!L) return;
   if (iv == 1) {
     L->phi_gc_ok = true;
+    L->gc_deferred = false;
     rb_stale_above(c, lvl);   // (the ghosts it sets are read by lvl+1's interpolation)
   }
   if (L->n) {
@@ -795,7 +796,8 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
   // loads (the values it reads are dead afterwards); otherwise applied now
   // (not next to refinement boundaries: their ghosts read the coarse level;
   // nor before a block pass with physical faces, whose ghosts take no shift)
-  const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 1 && L->phi_gc_ok &&
+  const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 1 &&
+                      (L->phi_gc_ok || L->gc_deferred) &&
                       !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb) && !(L->d_b3 && L->b3_phys);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
@@ -892,6 +894,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
                      ph);
       }
       L->d_phi = other;
+      if (L->gc_deferred) L->phi_gc_ok = true, L->gc_deferred = false;   // (it wrote every ghost face)
       deep_after(c, L, defer_faces && n + 3 == n_sub);
       n += 3;
       continue;
@@ -912,11 +915,16 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       }
       res_done = res;
       L->d_phi = other;
+      // (its ghost faces: every one, colour e's only without push1, whose
+      // colour-(1-e) halves k_smooth_resid forms itself)
+      if (L->gc_deferred) L->phi_gc_ok = true, L->gc_deferred = false;
       deep_after(c, L);
       if (res) deep_res(c, L);
       n += 2;
       continue;
     }
+    // (the one-substep kernels read the ghosts: a deferred fill runs first)
+    if (L->gc_deferred) fill_gc_lvl(c, lvl, 1);
     if (L->n_bnd && L->n_int && !odd && gs_tiled(L->nc, c->op, L->has_rb)) {
       // boxes with faces on other GPUs first; their halo travels on the comm
       // stream while the interior boxes run (the substep reads only its own
@@ -1285,7 +1293,7 @@ bool block3c_ok(omg_ctx* c, const Level* F) {
 // k_gsrb4's correction form, substeps 1-4 (round 6: level 1 of C3 815 + 308
 // us for k_gsrb3's form + the one-substep launch before; OMG_NO_BLOCK4P: those)
 // Returns the substeps run (0: none, the caller corrects otherwise).
-int correct_block3(omg_ctx* c, int l, bool res_ready) {
+int correct_block3(omg_ctx* c, int l, bool res_ready, bool defer_gc = false) {
   Level* F = level_ptr(c, l);
   Level* C = level_ptr(c, l - 1);
   if (!block3c_ok(c, F) || !C || !C->phi_gc_ok || C->shift_pending) return 0;
@@ -1297,9 +1305,19 @@ int correct_block3(omg_ctx* c, int l, bool res_ready) {
   const LevelView cv = C->view();
   int done = 3;
   deep_before(c, F, 0);   // (the pass reads colour 0, before the correction)
+  // defer_gc: nothing reads the level's ghosts before its next pass, which
+  // reads none (the stand-alone V-cycle's last pass on its top level, see
+  // fas_vcycle): the pass writes the interior only (12 of the 44 KB it
+  // writes per box are ghost faces), and the ghosts are filled if anything
+  // else comes first (Level::gc_deferred)
+  bool deferred = false;
   if (res_ready && c->block4 && !c->no_block4p && c->n_cycle_up * c->n_substeps >= 4) {
+    // (one rank: every rank decides its fills alike, see fas_vcycle)
+    deferred = defer_gc && c->n_ranks == 1 && c->n_cycle_up * c->n_substeps == 4 && !F->deep && !F->b3_phys &&
+               !c->no_defer_gc;
     Prof p(c, "smoother_gsrb4p", 2.0 * F->n * F->nc * F->nc * F->nc, l);
-    launch_gsrb4(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, &cv, F->d_b3c);
+    launch_gsrb4(F->view(), other, F->d_b3, F->n_b3, c->op, c->lambda, 1, nullptr, c->stream, &cv, F->d_b3c,
+                 nullptr, !deferred);
     done = 4;
   } else {
     Prof p(c, "smoother_gsrb3p", 1.5 * F->n * F->nc * F->nc * F->nc, l);
@@ -1308,7 +1326,8 @@ int correct_block3(omg_ctx* c, int l, bool res_ready) {
   }
   F->d_phi = other;
   deep_after(c, F);
-  F->phi_gc_ok = true;
+  F->phi_gc_ok = !deferred;
+  F->gc_deferred = deferred;
   return done;
 }
 
@@ -1543,8 +1562,11 @@ void drop_rhs_cache(omg_ctx* c) {
 }
 // entry points other than the cycles: apply pending phi work first; `writes`
 // = the call may change rhs (the cached rhs sum is dropped)
+void fill_gc_lvl(omg_ctx* c, int lvl, int iv);
 void enter(omg_ctx* c, bool writes = true) {
   materialize_phi(c);
+  for (auto& kv : c->levels)
+    if (kv.second.gc_deferred) fill_gc_lvl(c, kv.first, 1);
   if (writes) drop_rhs_cache(c);
 }
 
@@ -1804,7 +1826,10 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     // shifts, materialised where a rank has boxes), so with more than one
     // rank such a level is then always refilled.
     Level* L = level_ptr(c, max_lvl);
-    const bool need = !(L && L->phi_gc_ok && (!L->any_rb || c->n_ranks == 1 || !c->subtract_mean));
+    bool need = !(L && L->phi_gc_ok && (!L->any_rb || c->n_ranks == 1 || !c->subtract_mean));
+    // (ghosts deferred by the last cycle: its first pass reads none, k_gsrb4 /
+    // k_gsrb3, and writes them all; smooth_boxes fills first otherwise)
+    if (L && L->gc_deferred && c->smoother == OMG_SMOOTHER_GSRB && tail_top(c, max_lvl) < max_lvl) need = false;
     if (c->n_ranks > 1 && c->check_collective && (allreduce(c, need ? 1.0 : 0.0, true) > 0.5) != need)
       throw OmgError("mg_fas_vcycle: the stand-alone fill decision differs across ranks "
                      "(an upload of phi was not made on every rank)");
@@ -1828,6 +1853,10 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     const bool four = c->block4 && c->smoother == OMG_SMOOTHER_GSRB && b3_usable(c, l, P3, ph) &&
                       (!ph || c->block4_phys) && (c->n_cycle_down * c->n_substeps) % 4 == 0;
     const bool fused = !four && smooth_resid_ok(c, l);
+    // (the down pass writes its ghosts, which the residual reads: leaving them
+    // to a residual that gathers the neighbours' boundary cells instead took
+    // C3's down pass 837 -> 713 us and the residual 590 -> 750 us, the x faces'
+    // cells 64 B apart in the neighbours' boxes; profiles/r06/s19_defer_down_ab.txt)
     smooth_boxes(c, l, c->n_cycle_down, 1, fused ? 1 : 0, false, four, four);
     update_coarse(c, l, fused, tail_crhs && l == top + 1);
     faces_join(c, level_ptr(c, l));   // (update_coarse joined them; defensive)
@@ -1864,13 +1893,18 @@ double fas_vcycle(omg_ctx* c, int highest_lvl, bool want_max_res, bool standalon
     const bool want_res = l < max_lvl && block3c_ok(c, level_ptr(c, l + 1)) && !c->no_block3r;
     bool done = false;
     int pro = 0;
-    if (!want_res && (pro = correct_block3(c, l, res_ready)) > 0) {
+    if (!want_res && (pro = correct_block3(c, l, res_ready, full && l == max_lvl && !want_max_res)) > 0) {
       done = smooth_boxes(c, l, c->n_cycle_up, pro + 1);
-    } else if (prolong_smooth(c, l - 1)) {
-      done = smooth_boxes(c, l, c->n_cycle_up, 2, 0, want_res);
     } else {
-      correct_and_fill(c, l - 1, c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_up >= 1);
-      done = smooth_boxes(c, l, c->n_cycle_up, 1, 0, want_res);
+      // (the other correction paths read the level's ghosts: deferred ones are
+      // filled first)
+      if (Level* Fd = level_ptr(c, l); Fd && Fd->gc_deferred) fill_gc_lvl(c, l, 1);
+      if (prolong_smooth(c, l - 1)) {
+        done = smooth_boxes(c, l, c->n_cycle_up, 2, 0, want_res);
+      } else {
+        correct_and_fill(c, l - 1, c->smoother == OMG_SMOOTHER_GSRB && c->n_cycle_up >= 1);
+        done = smooth_boxes(c, l, c->n_cycle_up, 1, 0, want_res);
+      }
     }
     res_ready = done;
   }
@@ -2638,7 +2672,9 @@ bool b3_phys_args(omg_ctx* c, int lvl, const Level& L, B3Phys& P) {
 bool b3_usable(omg_ctx* c, int lvl, B3Phys& P, const B3Phys*& ph) {
   const Level* L = level_ptr(c, lvl);
   ph = nullptr;
-  if (!L || !L->d_b3 || !L->phi_gc_ok || !gsrb3_op_ok(c->op) || c->no_block3) return false;
+  if (!L || !L->d_b3 || !(L->phi_gc_ok || (L->gc_deferred && !L->b3_phys)) || !gsrb3_op_ok(c->op) ||
+      c->no_block3)
+    return false;
   if (L->b3_phys) {
     if (!b3_phys_args(c, lvl, *L, P)) return false;
     ph = &P;
@@ -3406,6 +3442,7 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     c->block4 = !env_flag("OMG_NO_BLOCK4");
     c->no_block4p = env_flag("OMG_NO_BLOCK4P");
     c->block4_phys = env_flag("OMG_BLOCK4_PHYS");
+    c->no_defer_gc = env_flag("OMG_NO_DEFER_GC");
     c->no_fuse_down_bc = env_flag("OMG_NO_FUSE_DOWN_BC");
     c->roctx = env_flag("OMG_ROCTX");
     c->debug = env_flag("OMG_DEBUG");

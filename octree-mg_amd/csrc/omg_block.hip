@@ -622,7 +622,7 @@ template <int OP, int PRO, bool PHYS>
 __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* __restrict__ dst,
                                                const int* __restrict__ cols, double lambda, int e,
                                                const double* __restrict__ shift, LevelView C,
-                                               const int* __restrict__ ccols, double fac, B3Phys P) {
+                                               const int* __restrict__ ccols, double fac, B3Phys P, int push) {
   static_assert(PRO == 0 || PRO == 2, "k_gsrb4: plain or the correction from a stored coarse res");
   static_assert(!(PRO && PHYS), "k_gsrb4: physical faces in the plain form only");
   __shared__ double pl[2][4][B4PL];
@@ -748,7 +748,7 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
         b3_st(dso, o, vo);
         const bool lf = leftv(jr);
         const int il = 2 * ih + 1;
-        if ((k == 1 && !zlo) || (k == B3NC && !zhi)) {
+        if (push && ((k == 1 && !zlo) || (k == B3NC && !zhi))) {
           const int nb = k == 1 ? 6 : 5;
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
           b3_st(dst, g + 8u * b3_gh(nb, il, j), lf ? ve : vo);
@@ -776,6 +776,9 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
           b3_st(dst, g + 8u * b3_gh(f + 1, il + 1, j), gr);
         }
       }
+      // push 0: the interior only (the cycle's last pass on a level whose next
+      // reader is a pass that reads no ghosts; correct_block3's defer_gc)
+      if (!push) return;
       {
         const int jr = l >> 2, w = l & 3, j = jr + 1;
         const int pc = w == 0 ? 0 : (w == 1 ? B3H - 1 : (w == 2 ? B3H : 2 * B3H - 1));
@@ -950,7 +953,7 @@ static double op_fac(const LevelView& L, int op, double lambda) {
 
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, const LevelView* coarse, const int* ccols,
-                  const B3Phys* phys) {
+                  const B3Phys* phys, bool push) {
   const double fac = op_fac(L, op, lambda);
   if (n_cols <= 0) return;
   if (L.nc != B3NC) throw std::runtime_error("launch_gsrb4: box size must be 16");
@@ -958,10 +961,11 @@ void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, 
     throw std::runtime_error("launch_gsrb4: the correction form needs a 16^3 coarse level, its records, no shift");
   if (phys && (coarse || shift))
     throw std::runtime_error("launch_gsrb4: physical faces in the plain form without a shift only");
+  if (!push && phys) throw std::runtime_error("launch_gsrb4: physical faces need their ghosts written");
   const LevelView& C = coarse ? *coarse : L;
   const B3Phys P = phys ? *phys : B3Phys{};
 #define OMG_B4(OPV, PMV, PHV, BS) \
-  k_gsrb4<OPV, PMV, PHV><<<n_cols, BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac, P)
+  k_gsrb4<OPV, PMV, PHV><<<n_cols, BS, 0, st>>>(L, dst, cols, lambda, e, shift, C, ccols, fac, P, push ? 1 : 0)
   if (op == OP_HELM) {
     if (coarse) OMG_B4(OP_HELM, 2, false, b4_threads(2));
     else if (phys) OMG_B4(OP_HELM, 0, true, B4BS);

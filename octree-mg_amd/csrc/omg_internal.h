@@ -125,6 +125,11 @@ struct Level {
   double* d_data = nullptr;
   double* d_phi = nullptr;              // phi (d_data's var 1)
   bool phi_gc_ok = false;               // phi's ghost faces equal what a fill would give
+  // phi's ghost faces are stale only because the level's last pass left them
+  // unwritten (the V-cycle's last up pass, correct_block3's defer_gc): the
+  // reference's ghosts are a fill of the interior, which every ghost reader
+  // runs first (fill_gc_lvl); the block passes read no ghosts on such a level
+  bool gc_deferred = false;
   bool has_rb = false, has_remote = false, has_phys = false;
   // the same flags over the level's boxes on EVERY rank (from the global
   // tree): decisions that choose collective calls use these, never the local
@@ -353,6 +358,7 @@ struct omg_ctx {
   bool block4 = true;                  // the down-smoothing as k_gsrb4 + the unfused residual (OMG_NO_BLOCK4: off)
   bool no_block4p = false;             // OMG_NO_BLOCK4P: the up-smoothing's correction form with three substeps (k_gsrb3)
   bool block4_phys = false;            // OMG_BLOCK4_PHYS: k_gsrb4 also on levels with physical faces (A/B)
+  bool no_defer_gc = false;            // OMG_NO_DEFER_GC: the V-cycle's last up pass writes its ghosts
   bool no_block3r = false;             // OMG_NO_BLOCK3R: no res from the coarse level's last pass (k_gsrb3 forms phi - old)
   int b3_min_boxes = omg::kB3MinBoxes;  // smallest level for k_gsrb3 (OMG_BLOCK3_MIN_BOXES, tests)
   int b3_col_small = 2;                // column length on levels below kB3MinBoxes (OMG_BLOCK3_SMALL_COL)

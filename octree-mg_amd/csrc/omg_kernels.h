@@ -73,9 +73,11 @@ struct B3Phys {
 // coarse (PRO 2, round 6): the up-smoothing's correct_children form with all
 // four substeps, the correction from the coarse res its last pass stored
 // (k_gsrb3's coarse_mode 2; ccols as for launch_gsrb3)
+// push false: the interior only, no ghost face written (the caller marks the
+// level's ghosts deferred: Level::gc_deferred)
 void launch_gsrb4(const LevelView& L, double* dst, const int* cols, int n_cols, int op, double lambda, int e,
                   const double* shift, hipStream_t st, const LevelView* coarse = nullptr,
-                  const int* ccols = nullptr, const B3Phys* phys = nullptr);
+                  const int* ccols = nullptr, const B3Phys* phys = nullptr, bool push = true);
 // push1 false: the ghost faces get the colour-e cells only (the colour-(1-e)
 // halves are left stale: only for a pass that k_smooth_resid follows, which
 // reads colour e's and forms colour 1-e's itself)

@@ -90,7 +90,8 @@ def test_block3_fmg_matches_oracle(have_guess):
         _assert_same(dev, orc)
 
 
-@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P", "OMG_NO_BLOCK3R", "OMG_NO_BLOCK4P"])
+@pytest.mark.parametrize("switch", ["OMG_NO_BLOCK3", "OMG_NO_BLOCK3P", "OMG_NO_BLOCK3R", "OMG_NO_BLOCK4P",
+                                    "OMG_NO_DEFER_GC"])
 def test_block3_switch_off_same_bits(monkeypatch, switch):
     """OMG_NO_BLOCK3=1 (one substep per launch) / OMG_NO_BLOCK3P=1 (the
     correction by k_prolong_smooth) / OMG_NO_BLOCK3R=1 (no res from the coarse
@@ -208,3 +209,45 @@ def test_block3_physical_faces_switch_off_same_bits(monkeypatch):
         for _ in range(2):
             assert dev.vcycle(True) == ref.vcycle(True) == orc.vcycle(True)
             _assert_same(dev, ref)
+
+
+# Deferred ghosts (round 6): the stand-alone V-cycle without the max residual
+# ends with k_gsrb4's correction form writing the top level's interior only;
+# the next cycle's first pass reads no ghosts and writes them all, and every
+# other reader fills them first (Level::gc_deferred).  Cycles without the
+# max residual back to back, then each other reader in turn: the download
+# (every stored cell, here after each step), the max-residual cycle, FMG,
+# mg_apply_op, a fill, and the stand-alone fill decision after an upload.
+def test_block3_deferred_ghosts_match_oracle():
+    dev, orc = _pair("16 128 128 128 3 v gsrb lpl 0 per sol 1 lb 0", 2, 2)
+    for _ in range(2):
+        dev.vcycle(False); orc.vcycle(False)
+    _assert_same(dev, orc)
+    for want in (False, True, False):
+        assert dev.vcycle(want) == orc.vcycle(want)
+        _assert_same(dev, orc)
+    dev.vcycle(False); orc.vcycle(False)
+    assert dev.fmg(True, True) == orc.fmg(True, True)
+    _assert_same(dev, orc)
+    dev.vcycle(False); orc.vcycle(False)
+    dev.apply_op(4); orc.apply_op(4)
+    _assert_same(dev, orc)
+    dev.vcycle(False); orc.vcycle(False)
+    dev.fill_ghost_cells(1); orc.fill_ghost_cells(1)
+    for lvl in dev.levels():   # an upload of phi (interior and ghosts) between cycles
+        if len(dev.my_ids(lvl)):
+            dev.set_level(lvl, 1, orc.get_level(lvl, 1))
+    for _ in range(2):
+        assert dev.vcycle(True) == orc.vcycle(True)
+        _assert_same(dev, orc)
+    # a cycle whose first substeps on the top level are one-substep launches
+    # (one down-smoothing cycle: no block pass) right after a deferring cycle
+    import pyoracle
+    dev.vcycle(False); orc.vcycle(False)
+    dev.mg.n_cycle_down, dev.mg.n_cycle_up = 1, 1
+    dev.mg._push_methods()
+    orc.o.configure(op=OPS["lpl"], lam=0.0, smoother=pyoracle.GSRB, n_cycle_down=1, n_cycle_up=1,
+                    subtract_mean=True)
+    for _ in range(2):
+        dev.vcycle(False); orc.vcycle(False)
+        _assert_same(dev, orc)
