@@ -92,6 +92,11 @@ __device__ __forceinline__ double b3_take(double v) {
 __device__ __forceinline__ void b3_st(double* base, unsigned off, double v) {
   asm volatile("global_store_dwordx2 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(v), "s"(base));
 }
+// two consecutive doubles, 16-B aligned (the store wave's interior and z-face
+// stores: two neighbouring pairs of a row per lane)
+__device__ __forceinline__ void b3_st2(double* base, unsigned off, v2d v) {
+  asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"(off), "v"(v), "s"(base));
+}
 __device__ __forceinline__ double b3_ld(const double* base, unsigned off) {
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
 }
@@ -738,21 +743,23 @@ __global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4(LevelView L, double* 
       // PHYS: a physical z face of this box (no push across it; its ghosts
       // once the second cell layer in from it is here)
       const bool zlo = PHYS && (fl & 16) && zsb == 1, zhi = PHYS && (fl & 32) && zsb == len;
+      // (a lane stores pairs q, q+1 of a row, ih even: 16-B stores, of each
+      // colour and, on a box's first / last plane, of each parity half of the
+      // z face's ghosts next door; 8-B stores per pair were the round-5 form)
 #pragma unroll
-      for (int r = 0; r < B3NC * B3CP / 64; r++) {
-        const int q = l + 64 * r, jr = q / B3CP, pc = q % B3CP;
+      for (int r = 0; r < B3NC * B3CP / 128; r++) {
+        const int q = 2 * (l + 64 * r), jr = q / B3CP, pc = q % B3CP;
         const int xs = 1 + pc / B3H, ih = pc % B3H, j = jr + 1;
         const unsigned o = bo[r0 + xs + B3XS] + 8u * (ih + B3H * (j - 1)) + PB * (k - 1);
-        const double ve = F[q][0], vo = F[q][1];
-        b3_st(dse, o, ve);
-        b3_st(dso, o, vo);
-        const bool lf = leftv(jr);
-        const int il = 2 * ih + 1;
+        const v2d ve = {F[q][0], F[q + 1][0]}, vo = {F[q][1], F[q + 1][1]};
+        b3_st2(dse, o, ve);
+        b3_st2(dso, o, vo);
         if (push && ((k == 1 && !zlo) || (k == B3NC && !zhi))) {
-          const int nb = k == 1 ? 6 : 5;
+          const bool lf = leftv(jr);
+          const int il = 2 * ih + 1, nb = k == 1 ? 6 : 5;
           const unsigned g = bo[r0 + (k == 1 ? -kB3S : kB3S) + xs + B3XS];
-          b3_st(dst, g + 8u * b3_gh(nb, il, j), lf ? ve : vo);
-          b3_st(dst, g + 8u * b3_gh(nb, il + 1, j), lf ? vo : ve);
+          b3_st2(dst, g + 8u * b3_gh(nb, il, j), lf ? ve : vo);
+          b3_st2(dst, g + 8u * b3_gh(nb, il + 1, j), lf ? vo : ve);
         }
       }
       if (PHYS && ((zlo && k == 2) || (zhi && k == B3NC))) {

@@ -33,6 +33,9 @@ for s in "$@"; do
                env $L timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 || exit 1; done; done; } > ${O}_phvar.log 2>&1; rc=$? ;;
     deferab) { for v in "" OMG_NO_DEFER_GC=1 "" OMG_NO_DEFER_GC=1; do
                echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; } > ${O}_deferab.log 2>&1; rc=$? ;;
+    libab) { for r in 1 2; do for v in default ${LIBV:-head}; do
+               echo "== $v"; if [ $v = default ]; then L=; else L=OMG_LIB=$PWD/octree-mg_amd/_variants/libomg_$v.so; fi
+               env $L timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; done; } > ${O}_libab.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
