@@ -36,6 +36,13 @@ for s in "$@"; do
     libab) { for r in 1 2; do for v in default ${LIBV:-head}; do
                echo "== $v"; if [ $v = default ]; then L=; else L=OMG_LIB=$PWD/octree-mg_amd/_variants/libomg_$v.so; fi
                env $L timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; done; } > ${O}_libab.log 2>&1; rc=$? ;;
+    c4prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/${O}_c4prof" -o run --output-format csv \
+                 -- python3 "$GRAFT_REPO_ROOT/tools/configs_bench.py" --no-cpu --only C4) > ${O}_c4prof.log 2>&1; rc=$? ;;
+    graphab) { for v in "" OMG_GRAPH=1 "" OMG_GRAPH=1; do
+               echo "== ${v:-default}"; env $v timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C4 C2 C5-helm C1-gsrb || exit 1; done; } > ${O}_graphab.log 2>&1; rc=$? ;;
+    smallab2) { for v in "" OMG_NO_SMALL3=1 "" OMG_NO_SMALL3=1; do
+               echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1
+               env $v timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 C5-helm C1-gsrb || exit 1; done; } > ${O}_smallab2.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
