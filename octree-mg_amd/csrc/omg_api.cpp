@@ -798,8 +798,7 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
   // nor before a block pass with physical faces, whose ghosts take no shift)
   const bool absorb = L->shift_pending && c->smoother == OMG_SMOOTHER_GSRB && n_sub >= 1 &&
                       (L->phi_gc_ok || L->gc_deferred) &&
-                      !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb) && !(L->d_b3 && L->b3_phys) &&
-                      !(L->small3 && L->any_phys);
+                      !L->has_rb && gs_tiled(L->nc, c->op, L->has_rb) && !(L->d_b3 && L->b3_phys);
   if (L->shift_pending && !absorb) materialize_level(c, L);
   if (c->smoother != OMG_SMOOTHER_GSRB) {
     // the register-ring kernel reads rhs from its ring-order copy, rebuilt
@@ -921,20 +920,6 @@ bool smooth_boxes(omg_ctx* c, int lvl, int n_cycle, int first_substep = 1, int s
       if (L->gc_deferred) L->phi_gc_ok = true, L->gc_deferred = false;
       deep_after(c, L);
       if (res) deep_res(c, L);
-      n += 2;
-      continue;
-    }
-    // three substeps in one launch on a small level (k_gsrb_small): it forms
-    // the physical ghosts from the level's consistent ghosts on entry, and
-    // writes the whole box (both colours of every ghost face) to the other buffer
-    if (n + 2 <= n_sub && L->small3 && L->phi_gc_ok && !want_res && gsrb_small_ok(L->nc, c->op) &&
-        !(shift && L->any_phys)) {
-      double* other = L->d_phi == L->d_data ? L->d_phi_buf : L->d_data;
-      {
-        Prof p(c, "smoother_small3", 1.5 * L->n * L->nc * L->nc * L->nc, lvl);
-        launch_gsrb_small(L->view(), other, c->op, c->lambda, e, shift, bc_for(c, lvl, 1), c->stream);
-      }
-      L->d_phi = other;
       n += 2;
       continue;
     }
@@ -2520,7 +2505,7 @@ void free_levels(omg_ctx* c) {
     dfree(L.d_rhs_lex);
     dfree(L.d_xlay);
     dfree(L.d_galt);
-    dfree(L.d_phi_buf); dfree(L.d_b3); dfree(L.d_b3c); L.n_b3 = 0; L.h_b3.clear(); L.small3 = false;
+    dfree(L.d_phi_buf); dfree(L.d_b3); dfree(L.d_b3c); L.n_b3 = 0; L.h_b3.clear();
     dfree(L.d_physbox);
     dfree(L.d_rbsend); dfree(L.d_rbrecv); dfree(L.d_bnd); dfree(L.d_int); dfree(L.d_push0); dfree(L.d_bndface);
     for (Transfer* T : {&L.halo, &L.restr, &L.prol, &L.rbx, &L.repl, &L.deep_phi, &L.deep_rhs}) {
@@ -2652,21 +2637,6 @@ void build_block3(omg_ctx* c, Level& L) {
   L.b3_phys = any_phys;
   L.d_b3 = to_device(flat);
   L.h_b3 = std::move(flat);
-  dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)L.n * L.stride, true);
-}
-
-// k_gsrb_small's levels (omg_small.hip): 16^3 boxes, below the column passes
-// (no records), every face a same-GPU box or physical, not replicated; the
-// level gets phi's second buffer.  The largest such level bound: kSmallMaxBoxes
-// (the pass runs one 1024-thread workgroup per CU, 149 KB of LDS).
-constexpr int kSmallMaxBoxes = 4095;
-void build_small(omg_ctx* c, Level& L) {
-  if (g_host_only || c->host_only || L.nc != 16 || L.n < 1 || L.n > kSmallMaxBoxes || L.d_b3 || L.replicated ||
-      L.deep || c->no_small3)
-    return;
-  for (int8_t k : L.h_nbk)
-    if (k != NB_LOCAL && k != NB_PHYS) return;
-  L.small3 = true;
   dmalloc(&L.d_phi_buf, sizeof(double) * (size_t)L.n * L.stride, true);
 }
 
@@ -3221,7 +3191,6 @@ void build_plan(omg_ctx* c) {
     }
     L.d_phi = L.d_data;
     build_block3(c, L);
-    build_small(c, L);
     L.d_sendpos = to_device(sendpos);
     L.d_nbk = to_device(L.h_nbk);
     L.d_nba = to_device(L.h_nba);
@@ -3426,7 +3395,6 @@ int omg_ctx_create(omg_ctx** out, int device, int rank, int n_ranks, const void*
     auto plan_switches = [](omg_ctx* c) {
       c->no_block3 = env_flag("OMG_NO_BLOCK3");
       c->no_block3_phys = env_flag("OMG_NO_BLOCK3_PHYS");
-      c->no_small3 = env_flag("OMG_NO_SMALL3");
       c->no_deep = env_flag("OMG_NO_DEEP");
       // (tests: the smallest level k_gsrb3 serves; OMG_BLOCK3_MIN_BOXES)
       if (const char* v = getenv("OMG_BLOCK3_MIN_BOXES")) c->b3_min_boxes = std::max(1, atoi(v));

@@ -199,10 +199,6 @@ struct Level {
   // some columns have physical faces (round 6): the passes take the ghosts
   // there from constant boundary values (b3_phys, omg_api.cpp)
   bool b3_phys = false;
-  // k_gsrb_small's levels (below the column passes' bound, every face a
-  // same-GPU box or physical, 16^3 boxes; d_phi_buf allocated): three
-  // substeps per launch (build_small)
-  bool small3 = false;
   // k_gsrb3's correct_children form: per column the coarse boxes around it
   // (launch_gsrb3's ccols); null: the level's up-smoothing starts with
   // k_prolong_smooth
@@ -357,7 +353,6 @@ struct omg_ctx {
   bool no_gs_dbl = false;              // OMG_NO_GS_DBL: a fill after every register-ring sweep (no ghost sets)
   bool no_block3 = false;              // OMG_NO_BLOCK3: one red-black substep per launch everywhere
   bool no_block3_phys = false;         // OMG_NO_BLOCK3_PHYS: no block passes on levels with physical faces
-  bool no_small3 = false;              // OMG_NO_SMALL3: one substep per launch on the small levels
   bool no_deep = false;                // OMG_NO_DEEP: split levels keep one substep per launch (no deep halo)
   bool no_block3p = false;             // OMG_NO_BLOCK3P: correct_children by k_prolong_smooth, not k_gsrb3
   bool block4 = true;                  // the down-smoothing as k_gsrb4 + the unfused residual (OMG_NO_BLOCK4: off)

@@ -101,14 +101,6 @@ void launch_gsrb3(const LevelView& L, double* dst, const int* cols, int n_cols, 
                   const double* shift, hipStream_t st, bool push1 = true, const LevelView* coarse = nullptr,
                   const int* ccols = nullptr, int coarse_mode = 1, bool res = false,
                   const B3Phys* phys = nullptr);
-// Three red-black substeps (colours e, 1-e, e) of a small level in one launch,
-// one workgroup per box with a 3-cell halo of its neighbours' cells in LDS
-// (k_gsrb_small, omg_small.hip): reads L.phi, writes dst (the level's other
-// phi buffer) whole: interior, same-GPU neighbours' ghost faces, physical
-// ghosts.  16^3 boxes whose faces are same-GPU boxes or physical.
-bool gsrb_small_ok(int nc, int op);
-void launch_gsrb_small(const LevelView& L, double* dst, int op, double lambda, int e, const double* shift,
-                       const GcBC& bc, hipStream_t st);
 void launch_gs_sub(const LevelView& L, int op, double lambda, int e, int colours, const LevelView& C,
                    const RBRec* rb, const GcBC& bc, double* sendbuf, hipStream_t st);
 // rl: rhs copy in ring order (launch_rhs_lex) for the register-ring kernel,
