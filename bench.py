@@ -90,13 +90,13 @@ DEEP_FAMILIES = ("deep_phi", "deep_rhs", "deep_faces")
 # beside 12 KiB of ghost faces per box
 PASSES = {
     "smoother_gsrb4": ("k_gsrb4<OP_LPL, 0> (the down-smoothing: four red-black substeps per pass)", 2.0,
-                       r"void omg::k_gsrb4<1(, 0)?>", 20.0),
+                       r"void omg::k_gsrb4<1(, 0)?(, false)?>", 20.0),
     "smoother_gsrb4p": ("k_gsrb4<OP_LPL, 2> (the up-smoothing: correction + four substeps per pass)", 2.0,
-                        r"void omg::k_gsrb4<1, 2>", 21.0),
+                        r"void omg::k_gsrb4<1, 2(, false)?>", 21.0),
     "smoother_gsrb3p": ("k_gsrb3<OP_LPL, 2, false> (the up-smoothing: correction + three substeps per pass)", 1.5,
-                        r"void omg::k_gsrb3<1, 2, false>", 21.0),
+                        r"void omg::k_gsrb3<1, 2, false(, false)?>", 21.0),
     "smoother_gsrb3": ("k_gsrb3<OP_LPL, 0, false> (three red-black substeps per pass)", 1.5,
-                       r"void omg::k_gsrb3<1, 0, false>", 20.0),
+                       r"void omg::k_gsrb3<1, 0, false(, false)?>", 20.0),
 }
 
 
