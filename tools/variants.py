@@ -33,6 +33,9 @@ VARIANTS = {
     # physical faces in the block passes (r06; timing only, not parity-correct):
     # no ghost formed in substeps 2-4 / no physical work in the store wave /
     # the plain load
+    # paired 16-B loads in k_gsrb4's plain form, at 5 waves per SIMD (spills)
+    "pairw5": [("omg_block.hip", "__global__ void __launch_bounds__(b4_threads(PRO)) k_gsrb4",
+                "__global__ void __launch_bounds__(b4_threads(PRO)) __attribute__((amdgpu_waves_per_eu(5))) k_gsrb4")],
     "phnofix": [("omg_block.hip", "if (PHYS) b3_fix(", "if (false) b3_fix(")] * 5,
     "phnostore": [("omg_block.hip", "if (PHYS && ((zlo && k == 2) || (zhi && k == B3NC))) {", "if (false) {"),
                   ("omg_block.hip", "if (PHYS && ((w == 0 && (fl & 1)) || (w == 3 && (fl & 2)))) {", "if (false) {"),
