@@ -44,6 +44,7 @@ for s in "$@"; do
                echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1
                env $v timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 C5-helm C1-gsrb || exit 1; done; } > ${O}_smallab2.log 2>&1; rc=$? ;;
     pmcb) timeout -k 10 900 bash tools/pmc.sh k_gsrb vcycle 3 > ${O}_pmcb.log 2>&1; rc=$? ;;
+    configs) timeout -k 10 900 python tools/configs_bench.py --cpu-ranks 16 > ${O}_configs.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
