@@ -26,9 +26,11 @@
 // In place would race (the halo columns are other workgroups' boxes), so the
 // pass reads one phi buffer and writes the level's other one (the host swaps
 // Level::d_phi): every interior cell, and every box's six ghost faces, pushed
-// by the box that owns the cell.  Levels whose faces are all same-GPU boxes,
-// 16^3 boxes, Laplacian / Helmholtz, with consistent ghosts on entry (they
-// are not read: a neighbour's cells are read in its box).
+// by the box that owns the cell.  Levels whose faces are all same-GPU boxes
+// (or proxies of other GPUs' boxes, the deep halo) or physical (round 6:
+// constant boundary values, B3Phys), 16^3 boxes, Laplacian / Helmholtz, with
+// consistent ghosts on entry (same-GPU ones are not read: a neighbour's cells
+// are read in its box; physical ones are, by the first substep).
 #include <stdexcept>
 
 #include "omg_device.h"
