@@ -251,3 +251,29 @@ def test_block3_deferred_ghosts_match_oracle():
     for _ in range(2):
         dev.vcycle(False); orc.vcycle(False)
         _assert_same(dev, orc)
+
+
+# The full-size goldens with physical faces take the passes at the default
+# level bound (their 4096-box finest level): each configuration's history and
+# final phi against the reference's run, with the launch counts showing that
+# the finest level's substeps ran as k_gsrb3 passes
+@pytest.mark.parametrize("name", ["c2_256_box16_gsrb_d0", "c5_helm256_box16_gsrb_d0", "mx1_256_box16"])
+def test_block3_physical_goldens_take_the_passes(monkeypatch, name):
+    import json
+    import os
+    from tests.mgdriver import _cycles, phi_digest
+    monkeypatch.delenv("OMG_BLOCK3_MIN_BOXES", raising=False)
+    monkeypatch.delenv("OMG_BLOCK3_COLUMN", raising=False)
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["configs"][name]
+    cfg = parse(g["args"])
+    dev = DeviceBackend(cfg)
+    setup_problem(dev)
+    dev.mg.ctx.call("set_profiling", 1)
+    hist = _cycles(dev, cfg, None)
+    dev.mg.ctx.call("synchronize")
+    run = g["runs"]["1"]
+    assert hist == run["history"]
+    assert phi_digest(dev) == run["phi_sha256"]
+    top = dev.tree.highest_lvl
+    n = dev.mg.ctx.kernel_stats(f"smoother_gsrb3@{top}")[0]
+    assert n >= 2 * cfg["n_its"], n   # (down and up, every cycle)
