@@ -45,6 +45,13 @@ for s in "$@"; do
                env $v timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 C5-helm C1-gsrb || exit 1; done; } > ${O}_smallab2.log 2>&1; rc=$? ;;
     pmcb) timeout -k 10 900 bash tools/pmc.sh k_gsrb vcycle 3 > ${O}_pmcb.log 2>&1; rc=$? ;;
     configs) timeout -k 10 900 python tools/configs_bench.py --cpu-ranks 16 > ${O}_configs.log 2>&1; rc=$? ;;
+    pmcc2) OUT=$PWD/gpurun_out/pmc_c2; mkdir -p $OUT; i=0; rc=0
+           for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
+                      "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS GRBM_GUI_ACTIVE"; do
+             i=$((i+1))
+             (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_gsrb" -d "$OUT/p$i" -o pmc --output-format csv \
+                -- python3 "$GRAFT_REPO_ROOT/tools/configs_bench.py" --no-cpu --only C2) > ${O}_pmcc2_p$i.log 2>&1 || { rc=1; break; }
+           done ;;
     bench) timeout -k 10 600 python bench.py --no-cpu-baseline > ${O}_bench.json 2> ${O}_bench.err; rc=$? ;;
     suite) timeout -k 10 1100 $PT tests -m gpu > ${O}_pytest_gpu.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 600 python bench.py > ${O}_benchfull.json 2> ${O}_benchfull.err; rc=$? ;;
