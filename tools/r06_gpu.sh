@@ -33,6 +33,10 @@ for s in "$@"; do
                env $L timeout -k 10 300 python tools/configs_bench.py --no-cpu --only C2 || exit 1; done; done; } > ${O}_phvar.log 2>&1; rc=$? ;;
     deferab) { for v in "" OMG_NO_DEFER_GC=1 "" OMG_NO_DEFER_GC=1; do
                echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; } > ${O}_deferab.log 2>&1; rc=$? ;;
+    sumsab) { for v in "" OMG_NO_FUSED_SUMS=1 "" OMG_NO_FUSED_SUMS=1 "" OMG_NO_FUSED_SUMS=1; do
+               echo "== ${v:-default}"; env $v timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; } > ${O}_sumsab.log 2>&1; rc=$? ;;
+    sumsprof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/${O}_sumsprof" -o run --output-format csv \
+             -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-parity) > ${O}_sumsprof.log 2>&1; rc=$? ;;
     libab) { for r in 1 2; do for v in default ${LIBV:-head}; do
                echo "== $v"; if [ $v = default ]; then L=; else L=OMG_LIB=$PWD/octree-mg_amd/_variants/libomg_$v.so; fi
                env $L timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-parity || exit 1; done; done; } > ${O}_libab.log 2>&1; rc=$? ;;
